@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""bench.py -- create-streaming encode throughput on MI355X (BASELINE.json metric, config C4).
+
+One step = one pass of the hot path over one batch of synthetic input: every band-1 tile of this rank's
+slab of a 40000 x 40000 x 4 int16 raster (tile 512, level 5, blocksize 4096) is encoded into FLAC frames
+in HBM (tile min/max, analysis, frame coding, offsets, CRC), the per-tile sizes come back to the host and,
+for N > 1, are all-gathered over RCCL so every rank knows every tile's byte offset in the streaming file.
+The raster is generated on the device before timing (inputs resident in HBM); nothing is cached between
+steps.
+
+Weak scaling: with N ranks the raster is N*40000 rows tall and rank r encodes its contiguous run of tile
+rows (~40000 rows, 6241 tiles at N=1), so per-GPU work is fixed.
+
+Also reported (DESIGN.md "Measurement"):
+  roofline      dominant kernel's algorithmic bytes / its HIP-event-timed average duration vs 8 TB/s
+  cpu_baseline  the CPU oracle (C restatement, oracle/) on a bounded sample of the same tiles, rank 0,
+                checked byte-for-byte against the GPU frames of those tiles
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E peak 8.0 TB/s
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--height", type=int, default=40000, help="rows per rank (C4: 40000)")
+    ap.add_argument("--width", type=int, default=40000)
+    ap.add_argument("--bands", type=int, default=4)
+    ap.add_argument("--tile", type=int, default=512)
+    ap.add_argument("--cpu-tiles", type=int, default=316, help="tiles in the CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=1)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic", type=float, default=None, help="measured HBM bytes per encode launch (PMC)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl")  # RCCL over xGMI
+        dist = tdist
+
+    from flac_raster_amd import _native
+
+    ctx = _native.Context(local_rank)
+    T = args.tile
+    W = args.width
+    full_h = args.height * world
+    trows = (full_h + T - 1) // T
+    tr0 = rank * trows // world
+    tr1 = (rank + 1) * trows // world
+    row0 = tr0 * T
+    rows = min(tr1 * T, full_h) - row0
+    B = args.bands
+
+    raster = ctx.alloc(B * rows * W * 2)
+    ctx.synth_raster(raster, B, rows, W, row0=row0, full_height=full_h, seed=1234)
+    desc = ctx.make_desc(rows, W, np.int16, nbands=1, band0=0, tile_h=T, tile_w=T, sample_rate=44100,
+                         bits_per_sample=16)
+    ntiles = desc.tile_end - desc.tile_begin
+    arena = ctx.alloc(ctx.arena_bound(desc))
+    ctx.sync()
+
+    sizes_dev = None
+    if dist is not None:
+        import torch
+        sizes_dev = torch.zeros(world, trows * ((W + T - 1) // T) // world + (W + T - 1) // T * 2,
+                                dtype=torch.int64, device=f"cuda:{local_rank}")
+
+    def step():
+        off, mn, mx, bps = ctx.encode_tiles_device(raster.ptr, desc, arena)
+        if dist is not None:
+            import torch
+            # spatial-index exchange: every rank's per-tile byte sizes -> global offsets (RCCL all-gather)
+            mine = torch.zeros(sizes_dev.shape[1], dtype=torch.int64, device=sizes_dev.device)
+            sz = torch.from_numpy(np.diff(off)).to(sizes_dev.device)
+            mine[: sz.numel()] = sz
+            gathered = [torch.empty_like(mine) for _ in range(world)]
+            dist.all_gather(gathered, mine)
+            torch.cuda.synchronize()
+        return off
+
+    for _ in range(args.warmup):
+        off = step()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+            import torch
+            torch.cuda.synchronize()
+        ctx.sync()
+
+    ctx.profile(True)
+    ctx.profile_reset()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        off = step()
+    barrier()
+    t1 = time.perf_counter()
+    ctx.profile(False)
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        px = torch.tensor([rows * W], dtype=torch.int64, device=f"cuda:{local_rank}")
+        dist.all_reduce(px)
+        total_px = int(px.item())
+    else:
+        total_px = rows * W
+
+    kernels = {k: ctx.profile_avg_ms(k) for k in ("stats", "analyze", "encode", "compact")}
+    comp_bytes = int(off[-1])
+    px_rank = rows * W
+    # algorithmic bytes per launch: stats reads 2 B/px; analyze reads 2 B/px; encode reads
+    # 2 B/px and writes the frames; compact reads + writes the frames.
+    algo = {"stats": 2 * px_rank, "analyze": 2 * px_rank, "encode": 2 * px_rank + comp_bytes,
+            "compact": 2 * comp_bytes}
+    dom = max((k for k in kernels if kernels[k] > 0), key=lambda k: kernels[k])
+    dom_ms = kernels[dom]
+    achieved = algo[dom] / (dom_ms * 1e-3) / 1e9
+    ms_per_step = elapsed / args.steps * 1e3
+    value = total_px / (elapsed / args.steps) / 1e6
+
+    result = {
+        "metric": "Mpixels/sec encode (create-streaming), band-1 tiles of a 40000x40000x4 int16 raster, tile 512, level 5",
+        "value": round(value, 1),
+        "unit": "Mpixels/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int16",
+        "data": "synthetic (on-device DEM recipe of SURVEY.md 8d, seed 1234)",
+        "config": {"workload": "C4 create-streaming encode", "raster": f"{full_h}x{W}x{B} int16",
+                   "tile_size": T, "tiles_per_rank": int(ntiles), "blocksize": 4096, "compression_level": 5,
+                   "parallelism": f"tile-rows sharded x{world}", "compressed_bytes_rank0": comp_bytes},
+        "kernels_ms": {k: round(v, 4) for k, v in kernels.items()},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": args.traffic},
+    }
+
+    if rank == 0 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(ctx, raster, rows, W, T, off, arena, args)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(ctx, raster, rows, W, T, off, arena, args):
+    """Time the oracle on the first `cpu_tiles` tiles (whole tile rows) of the same raster bytes."""
+    from oracle import oracle as O
+
+    tcols = (W + T - 1) // T
+    nrows_t = max(1, min((args.cpu_tiles + tcols - 1) // tcols, (rows + T - 1) // T))
+    h = min(nrows_t * T, rows)
+    band = np.empty((h, W), dtype=np.int16)
+    raster.download(h * W * 2, 0, out=band.view(np.uint8).reshape(-1))
+    t0 = time.perf_counter()
+    o_arena, o_off, _, _ = O.encode_tiles(band, T, threads=args.cpu_threads)
+    dt = time.perf_counter() - t0
+    nt = len(o_off) - 1
+    gpu = arena.download(int(off[nt]), 0)
+    parity = bool(np.array_equal(o_off, off[: nt + 1]) and gpu.tobytes() == o_arena.tobytes())
+    return {"value": round(h * W / dt / 1e6, 2), "unit": "Mpixels/s", "cores": args.cpu_threads, "kind": "port",
+            "sample": f"{nt} band-1 tiles ({h}x{W} px) of the benchmark raster, oracle/flac_oracle.c",
+            "seconds": round(dt, 3), "bit_exact_vs_gpu": parity}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,287 @@
+// frs_abi.hip -- exported C-ABI (include/flac_raster_amd.h): contexts, argument checks, host staging,
+// profiling.  The product has no CPU fallback: without a gfx950 device every entry point fails with
+// FRS_E_NODEV and the Python host raises.
+#include <string.h>
+
+#include <string>
+
+#include "frs_internal.h"
+
+namespace frs {
+
+void prof_begin(frs_ctx *ctx, const char *name, hipEvent_t *start) {
+    (void)name;
+    *start = nullptr;
+    if (!ctx->prof) return;
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return;
+    hipEventRecord(e, ctx->stream);
+    *start = e;
+}
+
+void prof_end(frs_ctx *ctx, const char *name, hipEvent_t start) {
+    if (!ctx->prof || !start) return;
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return;
+    hipEventRecord(e, ctx->stream);
+    ctx->ev_pending.push_back({std::string(name), {start, e}});
+}
+
+void prof_collect(frs_ctx *ctx) {
+    for (auto &p : ctx->ev_pending) {
+        float ms = 0.f;
+        hipEventSynchronize(p.second.second);
+        if (hipEventElapsedTime(&ms, p.second.first, p.second.second) == hipSuccess) {
+            ProfEntry &e = ctx->prof_tab[p.first];
+            e.total_ms += ms;
+            e.count += 1;
+        }
+        hipEventDestroy(p.second.first);
+        hipEventDestroy(p.second.second);
+    }
+    ctx->ev_pending.clear();
+}
+
+}  // namespace frs
+
+static bool is_gfx950(int dev) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return false;
+    return strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+}
+
+static int check_desc(frs_ctx *ctx, const frs_encode_desc *d) {
+    if (!d) { ctx->err = "null desc"; return FRS_E_ARG; }
+    if (d->height <= 0 || d->width <= 0 || d->tile_h <= 0 || d->tile_w <= 0) { ctx->err = "bad geometry"; return FRS_E_ARG; }
+    if (d->row_stride < d->width) { ctx->err = "row_stride < width"; return FRS_E_ARG; }
+    if (d->nbands < 1 || d->nbands > frs::kMaxChannels) { ctx->err = "nbands must be 1..8 (FLAC channels)"; return FRS_E_ARG; }
+    if (frs::dtype_size(d->dtype) == 0) { ctx->err = "bad dtype"; return FRS_E_ARG; }
+    if (d->blocksize != 4096) { ctx->err = "blocksize must be 4096 (converter.py:205)"; return FRS_E_UNSUPPORTED; }
+    if (d->compression_level != 5) { ctx->err = "only compression level 5 is implemented"; return FRS_E_UNSUPPORTED; }
+    if (d->bits_per_sample != 16 && d->bits_per_sample != 24) { ctx->err = "bits_per_sample must be 16 or 24"; return FRS_E_ARG; }
+    if (d->sample_rate <= 0 || d->sample_rate > 655350) { ctx->err = "bad sample rate"; return FRS_E_ARG; }
+    const int64_t tiles = ((d->height + d->tile_h - 1) / d->tile_h) * ((d->width + d->tile_w - 1) / d->tile_w);
+    if (d->tile_begin < 0 || d->tile_end > tiles || d->tile_begin > d->tile_end) { ctx->err = "bad tile range"; return FRS_E_ARG; }
+    if (d->nbands > 1 && d->band_stride < d->row_stride * d->height) { ctx->err = "band_stride too small"; return FRS_E_ARG; }
+    return FRS_OK;
+}
+
+extern "C" {
+
+int frs_abi_version(void) { return FRS_ABI_VERSION; }
+
+int frs_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    int k = 0;
+    for (int i = 0; i < n; i++)
+        if (is_gfx950(i)) k++;
+    return k;
+}
+
+int frs_ctx_create(int device, frs_ctx **out) {
+    if (!out) return FRS_E_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return FRS_E_NODEV;
+    if (!is_gfx950(device)) return FRS_E_NODEV;
+    frs_ctx *ctx = new frs_ctx();
+    ctx->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return FRS_E_HIP;
+    }
+    *out = ctx;
+    return FRS_OK;
+}
+
+void frs_ctx_destroy(frs_ctx *ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+    frs::prof_collect(ctx);
+    DevBuf *bufs[] = {&ctx->tiles, &ctx->norms, &ctx->analysis, &ctx->slots, &ctx->frame_bytes, &ctx->frame_off,
+                      &ctx->scan_tmp, &ctx->window, &ctx->tile_sizes, &ctx->raster_stage, &ctx->arena_stage,
+                      &ctx->dec_cand, &ctx->dec_count, &ctx->dec_blob, &ctx->dec_pcm, &ctx->dec_soff, &ctx->dec_poff};
+    for (DevBuf *b : bufs) b->release();
+    hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char *frs_last_error(const frs_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+void *frs_ctx_stream(frs_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int frs_profile_enable(frs_ctx *ctx, int on) {
+    if (!ctx) return FRS_E_ARG;
+    ctx->prof = on != 0;
+    return FRS_OK;
+}
+
+double frs_profile_avg_ms(frs_ctx *ctx, const char *kernel) {
+    if (!ctx || !kernel) return -1.0;
+    auto it = ctx->prof_tab.find(kernel);
+    if (it == ctx->prof_tab.end() || it->second.count == 0) return -1.0;
+    return it->second.total_ms / it->second.count;
+}
+
+void frs_profile_reset(frs_ctx *ctx) {
+    if (ctx) ctx->prof_tab.clear();
+}
+
+int64_t frs_encode_arena_bound(const frs_encode_desc *desc) {
+    if (!desc) return -1;
+    return frs::arena_bound(desc);
+}
+
+int frs_encode_tiles_device(frs_ctx *ctx, const frs_encode_desc *desc, const void *raster_dev, void *arena_dev,
+                            int64_t arena_cap, int64_t *tile_off, double *tile_min, double *tile_max,
+                            int32_t *stream_bps) {
+    if (!ctx) return FRS_E_ARG;
+    int rc = check_desc(ctx, desc);
+    if (rc) return rc;
+    if (!raster_dev || !arena_dev || !tile_off || !tile_min || !tile_max) { ctx->err = "null pointer"; return FRS_E_ARG; }
+    if (hipSetDevice(ctx->device) != hipSuccess) return FRS_E_HIP;
+    return frs::encode_job(ctx, desc, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max, stream_bps);
+}
+
+int frs_encode_tiles(frs_ctx *ctx, const frs_encode_desc *desc, const void *raster_host, uint8_t *arena_host,
+                     int64_t arena_cap, int64_t *tile_off, double *tile_min, double *tile_max, int32_t *stream_bps) {
+    if (!ctx) return FRS_E_ARG;
+    int rc = check_desc(ctx, desc);
+    if (rc) return rc;
+    if (!raster_host || !arena_host || !tile_off) { ctx->err = "null pointer"; return FRS_E_ARG; }
+    FRS_HIP(hipSetDevice(ctx->device));
+    const int es = frs::dtype_size(desc->dtype);
+    const int64_t nb = desc->nbands > 1 ? desc->band0 + desc->nbands : desc->band0 + 1;
+    const int64_t elems = (nb - 1) * desc->band_stride + (desc->height - 1) * desc->row_stride + desc->width;
+    const size_t rbytes = (size_t)elems * es;
+    FRS_HIP(ctx->raster_stage.ensure(rbytes));
+    FRS_HIP(hipMemcpyAsync(ctx->raster_stage.ptr, raster_host, rbytes, hipMemcpyHostToDevice, ctx->stream));
+    const int64_t bound = frs::arena_bound(desc);
+    FRS_HIP(ctx->arena_stage.ensure((size_t)bound));
+    const int64_t ntiles = desc->tile_end - desc->tile_begin;
+    rc = frs::encode_job(ctx, desc, ctx->raster_stage.ptr, ctx->arena_stage.ptr, bound, tile_off, tile_min, tile_max,
+                         stream_bps);
+    if (rc) return rc;
+    const int64_t total = tile_off[ntiles];
+    if (total > arena_cap) {
+        ctx->err = "arena too small";
+        return FRS_E_NOSPACE;
+    }
+    FRS_HIP(hipMemcpyAsync(arena_host, ctx->arena_stage.ptr, (size_t)total, hipMemcpyDeviceToHost, ctx->stream));
+    FRS_HIP(hipStreamSynchronize(ctx->stream));
+    return FRS_OK;
+}
+
+int frs_decode_frames_device(frs_ctx *ctx, const uint8_t *blob_dev, const int64_t *stream_off, int32_t nstreams,
+                             int32_t channels, int32_t bps, int32_t blocksize, int32_t *pcm_dev, const int64_t *pcm_off) {
+    if (!ctx) return FRS_E_ARG;
+    if (!blob_dev || !stream_off || !pcm_dev || !pcm_off || nstreams < 0 || channels < 1 || channels > 8 ||
+        blocksize < 16 || blocksize > 65535) {
+        ctx->err = "bad decode arguments";
+        return FRS_E_ARG;
+    }
+    FRS_HIP(hipSetDevice(ctx->device));
+    const int64_t nbytes = nstreams ? stream_off[nstreams] - stream_off[0] : 0;
+    (void)nbytes;
+    return frs::decode_job(ctx, blob_dev, nstreams ? stream_off[nstreams] : 0, stream_off, nstreams, channels, bps,
+                           blocksize, pcm_dev, pcm_off);
+}
+
+int frs_decode_frames(frs_ctx *ctx, const uint8_t *blob_host, const int64_t *stream_off, int32_t nstreams,
+                      int32_t channels, int32_t bps, int32_t blocksize, int32_t *pcm_host, const int64_t *pcm_off) {
+    if (!ctx) return FRS_E_ARG;
+    if (!blob_host || !stream_off || !pcm_host || !pcm_off || nstreams < 0) { ctx->err = "bad decode arguments"; return FRS_E_ARG; }
+    FRS_HIP(hipSetDevice(ctx->device));
+    const int64_t nbytes = nstreams ? stream_off[nstreams] : 0;
+    const int64_t nsamp = nstreams ? pcm_off[nstreams] : 0;
+    FRS_HIP(ctx->raster_stage.ensure((size_t)nbytes + 16));
+    FRS_HIP(ctx->dec_pcm.ensure((size_t)nsamp * channels * 4 + 16));
+    FRS_HIP(hipMemcpyAsync(ctx->raster_stage.ptr, blob_host, (size_t)nbytes, hipMemcpyHostToDevice, ctx->stream));
+    int rc = frs_decode_frames_device(ctx, ctx->raster_stage.as<uint8_t>(), stream_off, nstreams, channels, bps,
+                                      blocksize, ctx->dec_pcm.as<int32_t>(), pcm_off);
+    if (rc) return rc;
+    FRS_HIP(hipMemcpyAsync(pcm_host, ctx->dec_pcm.ptr, (size_t)nsamp * channels * 4, hipMemcpyDeviceToHost, ctx->stream));
+    FRS_HIP(hipStreamSynchronize(ctx->stream));
+    return FRS_OK;
+}
+
+int frs_denormalize_device(frs_ctx *ctx, const int32_t *pcm_dev, int64_t n, double data_min, double data_max,
+                           int32_t out_dtype, void *out_dev) {
+    if (!ctx) return FRS_E_ARG;
+    if (!pcm_dev || !out_dev || n < 0) { ctx->err = "bad denormalize arguments"; return FRS_E_ARG; }
+    FRS_HIP(hipSetDevice(ctx->device));
+    return frs::denormalize_job(ctx, pcm_dev, n, data_min, data_max, out_dtype, out_dev);
+}
+
+int frs_denormalize(frs_ctx *ctx, const int32_t *pcm_host, int64_t n, double data_min, double data_max,
+                    int32_t out_dtype, void *out_host) {
+    if (!ctx) return FRS_E_ARG;
+    const int es = frs::dtype_size(out_dtype);
+    if (!pcm_host || !out_host || n < 0 || es == 0) { ctx->err = "bad denormalize arguments"; return FRS_E_ARG; }
+    FRS_HIP(hipSetDevice(ctx->device));
+    FRS_HIP(ctx->dec_pcm.ensure((size_t)n * 4 + 16));
+    FRS_HIP(ctx->raster_stage.ensure((size_t)n * es + 16));
+    FRS_HIP(hipMemcpyAsync(ctx->dec_pcm.ptr, pcm_host, (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream));
+    int rc = frs::denormalize_job(ctx, ctx->dec_pcm.as<int32_t>(), n, data_min, data_max, out_dtype, ctx->raster_stage.ptr);
+    if (rc) return rc;
+    FRS_HIP(hipMemcpyAsync(out_host, ctx->raster_stage.ptr, (size_t)n * es, hipMemcpyDeviceToHost, ctx->stream));
+    FRS_HIP(hipStreamSynchronize(ctx->stream));
+    return FRS_OK;
+}
+
+void *frs_dev_malloc(frs_ctx *ctx, int64_t bytes) {
+    if (!ctx || bytes <= 0) return nullptr;
+    if (hipSetDevice(ctx->device) != hipSuccess) return nullptr;
+    void *p = nullptr;
+    hipError_t e = hipMalloc(&p, (size_t)bytes);
+    if (e != hipSuccess) {
+        ctx->err = std::string("hipMalloc: ") + hipGetErrorString(e);
+        return nullptr;
+    }
+    return p;
+}
+
+void frs_dev_free(frs_ctx *ctx, void *ptr) {
+    if (!ctx || !ptr) return;
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+    hipFree(ptr);
+}
+
+int frs_memcpy_h2d(frs_ctx *ctx, void *dst_dev, const void *src_host, int64_t bytes) {
+    if (!ctx) return FRS_E_ARG;
+    if (bytes <= 0) return FRS_OK;
+    FRS_HIP(hipSetDevice(ctx->device));
+    FRS_HIP(hipMemcpyAsync(dst_dev, src_host, (size_t)bytes, hipMemcpyHostToDevice, ctx->stream));
+    FRS_HIP(hipStreamSynchronize(ctx->stream));
+    return FRS_OK;
+}
+
+int frs_memcpy_d2h(frs_ctx *ctx, void *dst_host, const void *src_dev, int64_t bytes) {
+    if (!ctx) return FRS_E_ARG;
+    if (bytes <= 0) return FRS_OK;
+    FRS_HIP(hipSetDevice(ctx->device));
+    FRS_HIP(hipMemcpyAsync(dst_host, src_dev, (size_t)bytes, hipMemcpyDeviceToHost, ctx->stream));
+    FRS_HIP(hipStreamSynchronize(ctx->stream));
+    return FRS_OK;
+}
+
+int frs_ctx_sync(frs_ctx *ctx) {
+    if (!ctx) return FRS_E_ARG;
+    FRS_HIP(hipStreamSynchronize(ctx->stream));
+    return FRS_OK;
+}
+
+int frs_synth_raster_device(frs_ctx *ctx, int16_t *dev, int32_t bands, int64_t height, int64_t width, int64_t row0,
+                            int64_t full_height, uint64_t seed) {
+    if (!ctx || !dev || bands < 1 || height < 0 || width < 1 || row0 < 0 || row0 + height > full_height) {
+        if (ctx) ctx->err = "bad synth arguments";
+        return FRS_E_ARG;
+    }
+    FRS_HIP(hipSetDevice(ctx->device));
+    return frs::synth_job(ctx, dev, bands, height, width, row0, full_height, seed);
+}
+
+}  // extern "C"

@@ -1,0 +1,86 @@
+// frs_common.h -- shared structs and device helpers of the gfx950 spatial-FLAC codec.
+//
+// Exactness rules (libFLAC 1.4.3 parity, see DESIGN.md "Numerics"):
+//   * the whole library is compiled with -ffp-contract=off: libFLAC's x86-64 build has no FMA, so every
+//     fp64 multiply/add/divide here is a separate correctly rounded IEEE operation;
+//   * fma() is used only where a product is exact (float x float in double: autocorrelation), where it
+//     equals the separate multiply + add bit for bit.
+#pragma once
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+namespace frs {
+
+constexpr int kMaxLpc = 8;
+constexpr int kMaxChannels = 8;
+constexpr int kMaxPartOrder = 5;   // level 5: max_residual_partition_order
+constexpr int kMaxBlock = 4096;    // blocksize fixed by the reference (converter.py:205)
+
+// Per-tile geometry (host-built).
+struct TileGeom {
+    int64_t r0, c0;      // pixel origin in the raster
+    int32_t h, w;        // tile size (edge tiles truncated, cli.py:694-696)
+    int64_t frame_base;  // index of the tile's first frame in the job's frame list
+    int32_t nframes;
+    int32_t pad;
+};
+
+// Per-tile normalisation parameters (k_tile_stats).
+struct TileNorm {
+    int64_t imin, imax;  // integer min / max, or order-preserving bits of float min / max
+    double dmin, dmax;   // float(np.min(tile)), float(np.max(tile))
+    double den;          // (double)(dtype)(max - min)  -- numpy same-kind (wrapping) subtraction
+    int32_t has_range;   // max > min
+    int32_t pad;
+};
+
+// Per-subframe decision inputs produced by the analysis kernel (lane = subframe).
+struct SubAnalysis {
+    int32_t n;           // samples in the block
+    int32_t wasted;      // get_wasted_bits_
+    int32_t flags;       // kFlag*
+    int32_t fixed_order; // fixed predictor guess
+    int32_t lpc_order, lpc_prec, lpc_shift;
+    int32_t q[kMaxLpc];  // quantised LPC coefficients
+};
+constexpr int kFlagConstant = 1;  // CONSTANT subframe (all samples equal and fixed bits[1] == 0)
+constexpr int kFlagFixedOk = 2;   // fixed estimate < subframe bps -> evaluate FIXED
+constexpr int kFlagLpcOk = 4;     // LPC estimate < subframe bps and quantisation succeeded
+
+// Encode job parameters passed to kernels by value.
+struct EncodeParams {
+    int64_t row_stride, band_stride;
+    int32_t band0, nch;
+    int32_t blocksize;
+    int32_t sample_rate;
+    int32_t bps;          // stream bits per sample: 16 or 32
+    int32_t scale_bits;   // 16 -> *32767, 24 -> *8388607 (converter.py:78-83)
+    int32_t qlp_precision;
+    int32_t slot_words;   // capacity of one frame slot in 32-bit words
+    int64_t nframes;
+    int32_t ntiles;
+    int32_t pad;
+};
+
+__host__ __device__ inline int ilog2_u32(uint32_t v) { return 31 - __builtin_clz(v); }
+__host__ __device__ inline int ilog2_u64(uint64_t v) { return 63 - __builtin_clzll(v); }
+
+// numpy's float64 -> int32 cast as compiled on x86-64 (cvttsd2si): truncation, out of range or NaN
+// gives INT32_MIN ("integer indefinite").  The gfx950 v_cvt_i32_f64 saturates instead, so guard it.
+__device__ inline int32_t cast_f64_i32_x86(double v) {
+    if (!(v > -2147483649.0 && v < 2147483648.0)) return INT32_MIN;
+    return (int32_t)v;
+}
+
+// libm-compatible lround (half away from zero) without the floor(x+0.5) double rounding trap.
+__device__ inline int64_t lround_exact(double e) {
+    double r = trunc(e);
+    double f = e - r;  // exact
+    if (f >= 0.5) r += 1.0;
+    else if (f <= -0.5) r -= 1.0;
+    return (int64_t)r;
+}
+
+}  // namespace frs
+

@@ -1,0 +1,468 @@
+// frs_decode.hip -- gfx950 decode path: FLAC frames -> int32 PCM -> de-normalised raster samples.
+//
+// Reference path replaced: converter.py:241-242 (pyflac.FileDecoder -> libFLAC
+// FLAC__stream_decoder_process_until_end_of_stream, docs/sonos-pyflac.txt:1584-1640, 1809-1854) and
+// converter.py:88-110 (_denormalize_from_audio), as used by cli.py:1022-1023 (extract-streaming).
+//
+// Frames carry no size field and STREAMINFO min/max framesize are 0 in these files, so frames are
+// located in parallel: k_flag_sync marks every byte that starts a sync code with a parseable,
+// CRC-8-correct header; the marks are compacted into sorted candidates; k_span_crc finds for each
+// candidate the first later candidate (or stream end) whose preceding two bytes are the CRC-16 of the
+// span; k_chain follows those spans from each stream's first byte (so false syncs inside frame data are
+// never used); k_decode_frames decodes the true frames (one lane per frame, all channels) and checks
+// that the subframes end exactly at the CRC footer.
+#include <hipcub/hipcub.hpp>
+
+#include "frs_internal.h"
+
+namespace frs {
+
+__constant__ uint8_t d_crc8[256];
+__constant__ uint16_t d_crc16[256];
+
+struct FrameHdr {
+    int32_t ok;
+    int32_t frame_no;  // frame number from the header
+    int32_t bs;        // block size
+    int32_t hdr_len;   // header bytes incl. CRC-8
+    int32_t chass;     // channel assignment
+    int32_t bps;       // sample size
+};
+
+__device__ inline int stream_of(const int64_t *soff, int ns, int64_t p) {
+    int lo = 0, hi = ns - 1;
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (soff[mid] <= p) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// Parse + CRC-8-check a frame header at p (RFC 9639 9.1); end = end of the containing stream.
+__device__ FrameHdr parse_header(const uint8_t *blob, int64_t p, int64_t end, int channels, int stream_bps) {
+    FrameHdr h;
+    h.ok = 0;
+    if (p + 6 > end) return h;
+    if (blob[p] != 0xFF || (blob[p + 1] & 0xFE) != 0xF8) return h;
+    const uint8_t b2 = blob[p + 2], b3 = blob[p + 3];
+    const int bsc = b2 >> 4, src = b2 & 15, chass = b3 >> 4, ssc = (b3 >> 1) & 7;
+    if (bsc == 0 || src == 15 || chass > 10 || ssc == 3 || (b3 & 1)) return h;
+    int64_t q = p + 4;
+    uint32_t v = blob[q++];
+    int extra = 0;
+    if (v & 0x80) {
+        if ((v & 0xE0) == 0xC0) { extra = 1; v &= 0x1F; }
+        else if ((v & 0xF0) == 0xE0) { extra = 2; v &= 0x0F; }
+        else if ((v & 0xF8) == 0xF0) { extra = 3; v &= 0x07; }
+        else if ((v & 0xFC) == 0xF8) { extra = 4; v &= 0x03; }
+        else if ((v & 0xFE) == 0xFC) { extra = 5; v &= 0x01; }
+        else return h;
+    }
+    for (int i = 0; i < extra; i++) {
+        if (q >= end) return h;
+        const uint8_t c = blob[q++];
+        if ((c & 0xC0) != 0x80) return h;
+        v = (v << 6) | (c & 0x3F);
+    }
+    int bs;
+    if (bsc == 1) bs = 192;
+    else if (bsc >= 2 && bsc <= 5) bs = 576 << (bsc - 2);
+    else if (bsc == 6) { if (q >= end) return h; bs = blob[q++] + 1; }
+    else if (bsc == 7) { if (q + 1 >= end) return h; bs = ((blob[q] << 8) | blob[q + 1]) + 1; q += 2; }
+    else bs = 256 << (bsc - 8);
+    if (src == 12) q += 1;
+    else if (src == 13 || src == 14) q += 2;
+    if (q >= end) return h;
+    uint8_t c = 0;
+    for (int64_t i = p; i < q; i++) c = d_crc8[c ^ blob[i]];
+    if (c != blob[q]) return h;
+    const int nch = chass < 8 ? chass + 1 : 2;
+    if (nch != channels) return h;
+    h.ok = 1;
+    h.frame_no = (int32_t)v;
+    h.bs = bs;
+    h.hdr_len = (int32_t)(q + 1 - p);
+    h.chass = chass;
+    h.bps = ssc == 1 ? 8 : ssc == 2 ? 12 : ssc == 4 ? 16 : ssc == 5 ? 20 : ssc == 6 ? 24 : ssc == 7 ? 32 : stream_bps;
+    return h;
+}
+
+// flags[p] = 1 where a sync code starts a valid header
+__global__ void k_flag_sync(const uint8_t *blob, int64_t nbytes, const int64_t *soff, int ns, int channels,
+                            int stream_bps, uint8_t *flags) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= nbytes) return;
+    uint8_t f = 0;
+    if (blob[p] == 0xFF && p + 1 < nbytes && (blob[p + 1] & 0xFE) == 0xF8) {
+        const int s = stream_of(soff, ns, p);
+        f = parse_header(blob, p, soff[s + 1], channels, stream_bps).ok ? 1 : 0;
+    }
+    flags[p] = f;
+}
+
+// For candidate i find the first later position e (a candidate start or the stream end) such that the
+// CRC-16 of [pos_i, e-2) equals the two bytes before e.  ends[i] = e or -1.
+__global__ void k_span_crc(const uint8_t *blob, const int64_t *soff, int ns, const uint8_t *flags,
+                           const int64_t *cpos, const int *ncand, int64_t max_frame, int64_t *ends) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *ncand) return;
+    const int64_t p = cpos[i];
+    const int s = stream_of(soff, ns, p);
+    const int64_t send = soff[s + 1];
+    const int64_t lim = min(send, p + max_frame);
+    uint32_t crc = 0;
+    int64_t e = -1;
+    for (int64_t b = p; b + 2 <= lim; b++) {
+        // crc covers [p, b)
+        if (b > p + 4 && (b + 2 == send || flags[b + 2])) {
+            const uint32_t got = ((uint32_t)blob[b] << 8) | blob[b + 1];
+            if (crc == got) {
+                e = b + 2;
+                break;
+            }
+        }
+        crc = ((crc << 8) & 0xFFFFu) ^ d_crc16[((crc >> 8) ^ blob[b]) & 0xFF];
+    }
+    ends[i] = e;
+}
+
+__device__ inline int find_pos(const int64_t *cpos, int n, int64_t p) {
+    int lo = 0, hi = n - 1;
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cpos[mid] == p) return mid;
+        if (cpos[mid] < p) lo = mid + 1;
+        else hi = mid - 1;
+    }
+    return -1;
+}
+
+// Follow the frame chain of each stream from its first byte: frame k of stream s -> true[fbase[s]+k].
+__global__ void k_chain(const int64_t *soff, int ns, const int64_t *cpos, const int *ncand, const int64_t *ends,
+                        const int64_t *fbase, int64_t *frame_cand, int *bad) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ns) return;
+    const int nc = *ncand;
+    int64_t cur = soff[s];
+    const int64_t nf = fbase[s + 1] - fbase[s];
+    for (int64_t k = 0; k < nf; k++) {
+        const int idx = find_pos(cpos, nc, cur);
+        if (idx < 0 || ends[idx] < 0) {
+            atomicAdd(bad, 1);
+            return;
+        }
+        frame_cand[fbase[s] + k] = idx;
+        cur = ends[idx];
+    }
+    if (cur != soff[s + 1]) atomicAdd(bad, 1);
+}
+
+// MSB-first bit reader over global bytes (bounded)
+struct BitReader {
+    const uint8_t *base;
+    int64_t pos_bits;
+    int64_t end_bits;
+    uint64_t cache;   // left-aligned
+    int avail;
+    bool err;
+    __device__ void init(const uint8_t *b, int64_t start_byte, int64_t end_byte) {
+        base = b;
+        pos_bits = start_byte * 8;
+        end_bits = end_byte * 8;
+        cache = 0;
+        avail = 0;
+        err = false;
+    }
+    __device__ inline void refill() {
+        while (avail <= 56) {
+            const int64_t byte = (pos_bits + avail) >> 3;
+            uint64_t b = 0;
+            if (byte < (end_bits >> 3)) b = base[byte];
+            else if (byte >= (end_bits >> 3) + 8) {
+                err = true;
+                return;
+            }
+            cache |= b << (56 - avail);
+            avail += 8;
+        }
+    }
+    __device__ inline uint32_t bits(int n) {  // n <= 32
+        if (n == 0) return 0;
+        if (avail < n) refill();
+        const uint32_t v = (uint32_t)(cache >> (64 - n));
+        cache <<= n;
+        avail -= n;
+        pos_bits += n;
+        return v;
+    }
+    __device__ inline int32_t sbits(int n) {
+        if (n == 0) return 0;
+        uint32_t v = bits(n);
+        if (n < 32 && (v >> (n - 1))) v |= ~0u << n;
+        return (int32_t)v;
+    }
+    __device__ inline uint32_t unary() {  // count zeros before the next 1
+        uint32_t q = 0;
+        for (;;) {
+            if (avail < 32) refill();
+            if (err) return q;
+            if (cache) {
+                const int z = __builtin_clzll(cache);
+                if (z < avail) {
+                    q += z;
+                    cache <<= (z + 1);
+                    avail -= z + 1;
+                    pos_bits += z + 1;
+                    return q;
+                }
+            }
+            q += avail;
+            pos_bits += avail;
+            cache = 0;
+            avail = 0;
+            if (pos_bits > end_bits + 64) {
+                err = true;
+                return q;
+            }
+        }
+    }
+};
+
+__global__ void __launch_bounds__(64) k_decode_frames(const uint8_t *blob, const int64_t *soff, int ns,
+                                                     const int64_t *poff, const int64_t *cpos, const int64_t *ends,
+                                                     const int64_t *fbase, const int64_t *frame_cand, int64_t nframes,
+                                                     int channels, int stream_bps, int32_t *pcm, int blocksize,
+                                                     int *nvalid) {
+    const int64_t fi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (fi >= nframes) return;
+    const int64_t ci = frame_cand[fi];
+    const int64_t fpos = cpos[ci];
+    const int64_t fend_known = ends[ci];
+    const int s = stream_of(soff, ns, fpos);
+    const int64_t send = soff[s + 1];
+    const FrameHdr cd = parse_header(blob, fpos, send, channels, stream_bps);
+    const int64_t nsamp = poff[s + 1] - poff[s];
+    const int64_t kk = fi - fbase[s];
+    const int64_t first = kk * blocksize;
+    if (!cd.ok || cd.frame_no != kk || cd.bs > blocksize || first + cd.bs > nsamp) return;
+    int32_t *outb = pcm + (poff[s] + first) * channels;
+    BitReader br;
+    br.init(blob, fpos + cd.hdr_len, fend_known);
+    const int nch = channels;
+    // decode subframes straight into the output (interleaved), then verify the CRC
+    for (int c = 0; c < nch; c++) {
+        int sbps = cd.bps;
+        if ((cd.chass == 8 && c == 1) || (cd.chass == 9 && c == 0) || (cd.chass == 10 && c == 1)) sbps++;
+        br.bits(1);
+        const int t = (int)br.bits(6);
+        int w = 0;
+        if (br.bits(1)) w = (int)br.unary() + 1;
+        sbps -= w;
+        if (br.err || sbps <= 0 || sbps > 33) return;
+        int32_t *x = outb + c;
+        const int bs = cd.bs;
+        if (t == 0) {
+            const int32_t v = br.sbits(sbps);
+            for (int i = 0; i < bs; i++) x[(int64_t)i * nch] = v;
+        } else if (t == 1) {
+            for (int i = 0; i < bs; i++) x[(int64_t)i * nch] = br.sbits(sbps);
+        } else if ((t >= 8 && t <= 12) || t >= 32) {
+            const bool lpc = t >= 32;
+            const int o = lpc ? t - 31 : t - 8;
+            if (o > bs) return;
+            int32_t q[32];
+            int shift = 0;
+            for (int i = 0; i < o; i++) x[(int64_t)i * nch] = br.sbits(sbps);
+            if (lpc) {
+                const int prec = (int)br.bits(4) + 1;
+                if (prec == 16) return;
+                shift = br.sbits(5);
+                if (shift < 0) return;
+                for (int i = 0; i < o; i++) q[i] = br.sbits(prec);
+            }
+            const int method = (int)br.bits(2);
+            if (method > 1) return;
+            const int po = (int)br.bits(4);
+            const int pb = method == 0 ? 4 : 5, esc = (1 << pb) - 1;
+            if ((bs >> po) < o || (bs & ((1 << po) - 1))) return;
+            int i = o;
+            // history for reconstruction kept in registers (up to 32 taps read back from output)
+            for (int p = 0; p < (1 << po); p++) {
+                const int ns = (bs >> po) - (p == 0 ? o : 0);
+                const int kp = (int)br.bits(pb);
+                int nb = 0;
+                if (kp == esc) nb = (int)br.bits(5);
+                for (int j = 0; j < ns; j++, i++) {
+                    int32_t r;
+                    if (kp == esc) r = nb ? br.sbits(nb) : 0;
+                    else {
+                        const uint32_t qq = br.unary();
+                        const uint32_t u = (qq << kp) | br.bits(kp);
+                        r = (int32_t)((u >> 1) ^ (uint32_t)(-(int32_t)(u & 1)));
+                    }
+                    int64_t pred = 0;
+                    if (lpc) {
+                        for (int m = 0; m < o; m++) pred += (int64_t)q[m] * x[(int64_t)(i - 1 - m) * nch];
+                        pred >>= shift;
+                    } else {
+                        switch (o) {
+                        case 0: pred = 0; break;
+                        case 1: pred = x[(int64_t)(i - 1) * nch]; break;
+                        case 2: pred = 2 * (int64_t)x[(int64_t)(i - 1) * nch] - x[(int64_t)(i - 2) * nch]; break;
+                        case 3: pred = 3 * (int64_t)x[(int64_t)(i - 1) * nch] - 3 * (int64_t)x[(int64_t)(i - 2) * nch] + x[(int64_t)(i - 3) * nch]; break;
+                        default: pred = 4 * (int64_t)x[(int64_t)(i - 1) * nch] - 6 * (int64_t)x[(int64_t)(i - 2) * nch] + 4 * (int64_t)x[(int64_t)(i - 3) * nch] - x[(int64_t)(i - 4) * nch]; break;
+                        }
+                    }
+                    x[(int64_t)i * nch] = (int32_t)(r + pred);
+                    if (br.err) return;
+                }
+            }
+        } else {
+            return;
+        }
+        if (w)
+            for (int i = 0; i < bs; i++) x[(int64_t)i * nch] = (int32_t)((uint32_t)x[(int64_t)i * nch] << w);
+    }
+    if (cd.chass >= 8) {
+        for (int i = 0; i < cd.bs; i++) {
+            int32_t *pr = outb + (int64_t)i * nch;
+            const int64_t a = pr[0], sd = pr[1];
+            if (cd.chass == 8) pr[1] = (int32_t)(a - sd);
+            else if (cd.chass == 9) pr[0] = (int32_t)(a + sd);
+            else {
+                const int64_t mid = (a * 2) | (sd & 1);
+                pr[0] = (int32_t)((mid + sd) >> 1);
+                pr[1] = (int32_t)((mid - sd) >> 1);
+            }
+        }
+    }
+    // the decoded subframes must end exactly at the CRC-16 footer found by k_span_crc
+    const int64_t fend = (br.pos_bits + 7) >> 3;
+    if (br.err || fend + 2 != fend_known) return;
+    atomicAdd(nvalid, 1);
+}
+
+// converter.py:88-110 (fp32, round half to even) after soundfile's pcm/32768 scaling.
+template <typename O>
+__global__ void k_denormalize(const int32_t *pcm, int64_t n, float rng, float fmn, int is_float, O *out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float v = (float)((double)pcm[i] / 32768.0);
+    if (is_float) {
+        out[i] = (O)v;
+        return;
+    }
+    float a = __fadd_rn(v, 1.0f);
+    a = __fdiv_rn(a, 2.0f);
+    a = __fmul_rn(a, rng);
+    a = __fadd_rn(a, fmn);
+    const float r = rintf(a);
+    out[i] = (O)(int64_t)r;
+}
+
+static bool g_dec_tables[64];
+
+int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const int64_t *stream_off,
+               int32_t nstreams, int32_t channels, int32_t bps, int32_t blocksize, int32_t *pcm_dev,
+               const int64_t *pcm_off) {
+    hipStream_t st = ctx->stream;
+    if (!g_dec_tables[ctx->device]) {
+        uint8_t t8[256];
+        uint16_t t16[256];
+        for (int i = 0; i < 256; i++) {
+            uint8_t c = (uint8_t)i;
+            for (int k = 0; k < 8; k++) c = (c & 0x80) ? (uint8_t)((c << 1) ^ 0x07) : (uint8_t)(c << 1);
+            t8[i] = c;
+            uint16_t d = (uint16_t)(i << 8);
+            for (int k = 0; k < 8; k++) d = (d & 0x8000) ? (uint16_t)((d << 1) ^ 0x8005) : (uint16_t)(d << 1);
+            t16[i] = d;
+        }
+        FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(d_crc8), t8, sizeof(t8), 0, hipMemcpyHostToDevice, st));
+        FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(d_crc16), t16, sizeof(t16), 0, hipMemcpyHostToDevice, st));
+        g_dec_tables[ctx->device] = true;
+    }
+    if (blob_bytes <= 0 || nstreams <= 0) return FRS_OK;
+    std::vector<int64_t> fbase(nstreams + 1, 0);
+    for (int s = 0; s < nstreams; s++) fbase[s + 1] = fbase[s] + (pcm_off[s + 1] - pcm_off[s] + blocksize - 1) / blocksize;
+    const int64_t frames = fbase[nstreams];
+    const int64_t max_frame = (int64_t)blocksize * channels * 5 + 4096;
+    // scratch: flags (1 B/byte), candidate positions, ends, chain
+    FRS_HIP(ctx->dec_blob.ensure((size_t)blob_bytes + 64));
+    uint8_t *flags = ctx->dec_blob.as<uint8_t>();
+    FRS_HIP(ctx->dec_cand.ensure(sizeof(int64_t) * (size_t)(2 * blob_bytes / 16 + 2 * frames + 1024)));
+    FRS_HIP(ctx->dec_count.ensure(sizeof(int) * 4));
+    FRS_HIP(ctx->dec_soff.ensure(sizeof(int64_t) * (nstreams + 1) * 3 + sizeof(int64_t) * frames));
+    FRS_HIP(ctx->dec_poff.ensure(sizeof(int64_t) * (nstreams + 1)));
+    int64_t *dsoff = ctx->dec_soff.as<int64_t>();
+    int64_t *dfbase = dsoff + (nstreams + 1);
+    int64_t *dchain = dfbase + (nstreams + 1);
+    FRS_HIP(hipMemcpyAsync(dsoff, stream_off, sizeof(int64_t) * (nstreams + 1), hipMemcpyHostToDevice, st));
+    FRS_HIP(hipMemcpyAsync(dfbase, fbase.data(), sizeof(int64_t) * (nstreams + 1), hipMemcpyHostToDevice, st));
+    FRS_HIP(hipMemcpyAsync(ctx->dec_poff.ptr, pcm_off, sizeof(int64_t) * (nstreams + 1), hipMemcpyHostToDevice, st));
+    FRS_HIP(hipMemsetAsync(ctx->dec_count.ptr, 0, sizeof(int) * 4, st));
+    int *ncand = ctx->dec_count.as<int>();
+    int *nvalid = ncand + 1;
+    int *bad = ncand + 2;
+    hipEvent_t ev;
+    prof_begin(ctx, "decode", &ev);
+    k_flag_sync<<<(unsigned)((blob_bytes + 255) / 256), 256, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams, channels,
+                                                                     bps, flags);
+    // compact candidate positions (sorted)
+    const size_t cand_cap = (size_t)(2 * blob_bytes / 16 + 2 * frames + 1024) / 2;
+    int64_t *cpos = ctx->dec_cand.as<int64_t>();
+    int64_t *ends = cpos + cand_cap;
+    size_t tmp = 0;
+    hipcub::CountingInputIterator<int64_t> it(0);
+    FRS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmp, it, flags, cpos, ncand, (int)blob_bytes, st));
+    FRS_HIP(ctx->scan_tmp.ensure(tmp));
+    FRS_HIP(hipcub::DeviceSelect::Flagged(ctx->scan_tmp.ptr, tmp, it, flags, cpos, ncand, (int)blob_bytes, st));
+    int hc = 0;
+    FRS_HIP(hipMemcpyAsync(&hc, ncand, sizeof(int), hipMemcpyDeviceToHost, st));
+    FRS_HIP(hipStreamSynchronize(st));
+    if ((size_t)hc > cand_cap) {
+        ctx->err = "too many frame sync candidates";
+        return FRS_E_CORRUPT;
+    }
+    if (hc > 0) {
+        k_span_crc<<<(hc + 63) / 64, 64, 0, st>>>(blob_dev, dsoff, nstreams, flags, cpos, ncand, max_frame, ends);
+        k_chain<<<(nstreams + 63) / 64, 64, 0, st>>>(dsoff, nstreams, cpos, ncand, ends, dfbase, dchain, bad);
+        k_decode_frames<<<(unsigned)((frames + 63) / 64), 64, 0, st>>>(blob_dev, dsoff, nstreams,
+                                                                      ctx->dec_poff.as<int64_t>(), cpos, ends, dfbase,
+                                                                      dchain, frames, channels, bps, pcm_dev, blocksize,
+                                                                      nvalid);
+    }
+    prof_end(ctx, "decode", ev);
+    int hv[3] = {0, 0, 0};
+    FRS_HIP(hipMemcpyAsync(hv, ncand, sizeof(int) * 3, hipMemcpyDeviceToHost, st));
+    FRS_HIP(hipStreamSynchronize(st));
+    prof_collect(ctx);
+    if (hv[2] != 0 || hv[1] != frames) {
+        ctx->err = "decoded " + std::to_string(hv[1]) + " valid frames, expected " + std::to_string(frames) +
+                   (hv[2] ? " (broken frame chain)" : "");
+        return FRS_E_CORRUPT;
+    }
+    return FRS_OK;
+}
+
+int denormalize_job(frs_ctx *ctx, const int32_t *pcm_dev, int64_t n, double dmin, double dmax, int32_t out_dtype,
+                    void *out_dev) {
+    hipStream_t st = ctx->stream;
+    const float rng = (float)(dmax - dmin), fmn = (float)dmin;
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    if (n == 0) return FRS_OK;
+    switch (out_dtype) {
+    case FRS_DT_U8: k_denormalize<uint8_t><<<grid, 256, 0, st>>>(pcm_dev, n, rng, fmn, 0, (uint8_t *)out_dev); break;
+    case FRS_DT_U16: k_denormalize<uint16_t><<<grid, 256, 0, st>>>(pcm_dev, n, rng, fmn, 0, (uint16_t *)out_dev); break;
+    case FRS_DT_I16: k_denormalize<int16_t><<<grid, 256, 0, st>>>(pcm_dev, n, rng, fmn, 0, (int16_t *)out_dev); break;
+    case FRS_DT_I32: k_denormalize<int32_t><<<grid, 256, 0, st>>>(pcm_dev, n, rng, fmn, 0, (int32_t *)out_dev); break;
+    case FRS_DT_U32: k_denormalize<uint32_t><<<grid, 256, 0, st>>>(pcm_dev, n, rng, fmn, 0, (uint32_t *)out_dev); break;
+    case FRS_DT_F32: k_denormalize<float><<<grid, 256, 0, st>>>(pcm_dev, n, rng, fmn, 1, (float *)out_dev); break;
+    case FRS_DT_F64: k_denormalize<double><<<grid, 256, 0, st>>>(pcm_dev, n, rng, fmn, 1, (double *)out_dev); break;
+    default: ctx->err = "bad dtype"; return FRS_E_ARG;
+    }
+    FRS_HIP(hipGetLastError());
+    return FRS_OK;
+}
+
+}  // namespace frs

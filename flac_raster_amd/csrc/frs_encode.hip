@@ -1,0 +1,1329 @@
+// frs_encode.hip -- gfx950 encode path: raster tiles -> libFLAC-1.4.3-level-5-identical FLAC frames.
+//
+// Reference path replaced (Youssef-Harby/flac-raster): cli.py:690-763 (create_streaming tile loop, band 1),
+// converter.py:56-86 (normalise to int16), converter.py:185-216 (interleave + pyflac StreamEncoder ->
+// libFLAC FLAC__stream_encoder_process_interleaved/finish at level 5, blocksize 4096).
+//
+// Kernels (one encode job = a set of tiles; every tile is one FLAC stream):
+//   k_stats_init / k_tile_stats / k_tile_finalize   per-tile min/max (np.min/np.max) + normalisation params
+//   k_analyze        lane = (frame, channel) subframe: wasted bits, fixed-predictor totals and the
+//                    tukey(0.5)-windowed autocorrelation (fp64, libFLAC's per-lag sequential order),
+//                    Levinson-Durbin, order guess, qlp quantisation        [fp64-VALU bound]
+//   k_encode_frames  workgroup = frame: candidate residuals, partition sums, Rice parameters, choice,
+//                    exact bit positions (block prefix scan) and LDS bit packing into a frame slot
+//   (scan)           exclusive scan of frame sizes -> arena offsets (tiles are consecutive frame runs)
+//   k_compact        workgroup = frame: CRC-16 (parallel GF(2) combine) + copy slot -> arena offset
+#include <hipcub/hipcub.hpp>
+
+#include "frs_internal.h"
+
+namespace frs {
+
+// ------------------------------------------------------------------------------------------- dtypes
+template <int DT> struct Elem;
+template <> struct Elem<FRS_DT_U8> { using T = uint8_t; static constexpr bool is_float = false; };
+template <> struct Elem<FRS_DT_U16> { using T = uint16_t; static constexpr bool is_float = false; };
+template <> struct Elem<FRS_DT_I16> { using T = int16_t; static constexpr bool is_float = false; };
+template <> struct Elem<FRS_DT_I32> { using T = int32_t; static constexpr bool is_float = false; };
+template <> struct Elem<FRS_DT_U32> { using T = uint32_t; static constexpr bool is_float = false; };
+template <> struct Elem<FRS_DT_F32> { using T = float; static constexpr bool is_float = true; };
+template <> struct Elem<FRS_DT_F64> { using T = double; static constexpr bool is_float = true; };
+
+// order-preserving int64 key of a double (for atomic min/max of float rasters)
+__device__ inline int64_t f2key(double v) {
+    int64_t b = __double_as_longlong(v);
+    return b >= 0 ? b : (b ^ 0x7FFFFFFFFFFFFFFFll);
+}
+__host__ __device__ inline double key2f(int64_t k) {
+    int64_t b = k >= 0 ? k : (k ^ 0x7FFFFFFFFFFFFFFFll);
+    double d;
+    memcpy(&d, &b, 8);
+    return d;
+}
+
+template <int DT> __device__ inline int64_t elem_key(typename Elem<DT>::T v) {
+    if constexpr (Elem<DT>::is_float) return f2key((double)v);
+    else return (int64_t)v;
+}
+
+// converter.py:56-86 for one element.  numpy 2 (NEP 50): x - min and max - min are evaluated in the
+// raster dtype (wrapping), promoted to float64 by 2.0*(...); the cast to int16/int32 truncates.
+template <int DT> struct Normalizer {
+    using T = typename Elem<DT>::T;
+    T mn;
+    double den;
+    double scale;
+    int has_range;
+    int bps16;
+    __device__ inline int32_t operator()(T x) const {
+        if constexpr (DT == FRS_DT_F32) {
+            float v = x * 8388607.0f;  // float data used as-is, float32 product (converter.py:61-64, 81)
+            return cast_f64_i32_x86((double)v);
+        } else if constexpr (DT == FRS_DT_F64) {
+            return cast_f64_i32_x86(x * 8388607.0);
+        } else {
+            if (!has_range) return 0;
+            T d = (T)((int64_t)x - (int64_t)mn);
+            double v = (2.0 * (double)d) / den - 1.0;
+            v = v * scale;
+            int32_t c = cast_f64_i32_x86(v);
+            return bps16 ? (int32_t)(int16_t)c : c;
+        }
+    }
+};
+
+template <int DT> __device__ inline Normalizer<DT> make_norm(const TileNorm &tn, int scale_bits) {
+    Normalizer<DT> nz;
+    using T = typename Elem<DT>::T;
+    if constexpr (!Elem<DT>::is_float) nz.mn = (T)tn.imin;
+    else nz.mn = (T)0;
+    nz.den = tn.den;
+    nz.scale = scale_bits == 16 ? 32767.0 : 8388607.0;
+    nz.has_range = tn.has_range;
+    nz.bps16 = scale_bits == 16;
+    return nz;
+}
+
+// tile of frame f (binary search over frame_base)
+__device__ inline int tile_of_frame(const TileGeom *tiles, int ntiles, int64_t f) {
+    int lo = 0, hi = ntiles - 1;
+    while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (tiles[mid].frame_base <= f) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// ------------------------------------------------------------------------------------ tile stats
+__global__ void k_stats_init(TileNorm *norms, int ntiles) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < ntiles) {
+        norms[t].imin = INT64_MAX;
+        norms[t].imax = INT64_MIN;
+    }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) k_tile_stats(const typename Elem<DT>::T *raster, EncodeParams P,
+                                                   const TileGeom *tiles, TileNorm *norms, int splits) {
+    const int t = blockIdx.y;
+    const TileGeom g = tiles[t];
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    const int64_t rows = (int64_t)g.h * P.nch;
+    for (int64_t rr = blockIdx.x; rr < rows; rr += splits) {
+        const int ch = (int)(rr / g.h);
+        const int64_t r = rr - (int64_t)ch * g.h;
+        const typename Elem<DT>::T *row =
+            raster + (int64_t)(P.band0 + ch) * P.band_stride + (g.r0 + r) * P.row_stride + g.c0;
+        for (int c = threadIdx.x; c < g.w; c += blockDim.x) {
+            int64_t k = elem_key<DT>(row[c]);
+            lo = k < lo ? k : lo;
+            hi = k > hi ? k : hi;
+        }
+    }
+    // wave reduce then one atomic per wave
+    for (int o = 32; o > 0; o >>= 1) {
+        int64_t l2 = __shfl_xor(lo, o), h2 = __shfl_xor(hi, o);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin((long long *)&norms[t].imin, (long long)lo);
+        atomicMax((long long *)&norms[t].imax, (long long)hi);
+    }
+}
+
+template <int DT> __global__ void k_tile_finalize(TileNorm *norms, int ntiles) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntiles) return;
+    TileNorm n = norms[t];
+    using T = typename Elem<DT>::T;
+    if constexpr (Elem<DT>::is_float) {
+        n.dmin = key2f(n.imin);
+        n.dmax = key2f(n.imax);
+        n.den = 0.0;
+        n.has_range = n.dmax > n.dmin;
+    } else {
+        n.dmin = (double)n.imin;
+        n.dmax = (double)n.imax;
+        n.has_range = n.imax > n.imin;
+        n.den = (double)(T)(n.imax - n.imin);  // data_max - data_min in the dtype (wraps for int16)
+    }
+    norms[t] = n;
+}
+
+// ------------------------------------------------------------------------------- LPC helpers (fp64)
+// FLAC__lpc_compute_lp_coefficients (lpc.c): returns the number of orders computed (early stop on
+// err == 0); err[i] = prediction error after order i+1.
+__device__ int levinson_errors(const double *autoc, int max_order, double *err) {
+    double lpc[kMaxLpc];
+    double e = autoc[0];
+    int done = max_order;
+#pragma unroll
+    for (int i = 0; i < kMaxLpc; i++) {
+        if (i < done) {
+            double r = -autoc[i + 1];
+#pragma unroll
+            for (int j = 0; j < kMaxLpc; j++)
+                if (j < i) r -= lpc[j] * autoc[i - j];
+            r /= e;
+            lpc[i] = r;
+#pragma unroll
+            for (int j = 0; j < kMaxLpc / 2; j++) {
+                if (j < (i >> 1)) {
+                    double tmp = lpc[j];
+                    lpc[j] += r * lpc[i - 1 - j];
+                    lpc[i - 1 - j] += r * tmp;
+                }
+            }
+            if (i & 1) lpc[i >> 1] += lpc[i >> 1] * r;
+            e *= (1.0 - r * r);
+            err[i] = e;
+            if (e == 0.0) done = i + 1;
+        }
+    }
+    return done;
+}
+
+// same recursion, returns the predictor coefficients of order `order` as floats (lp_coeff[order-1])
+__device__ void levinson_coefs(const double *autoc, int order, float *lp) {
+    double lpc[kMaxLpc];
+    double e = autoc[0];
+#pragma unroll
+    for (int i = 0; i < kMaxLpc; i++) {
+        if (i < order) {
+            double r = -autoc[i + 1];
+#pragma unroll
+            for (int j = 0; j < kMaxLpc; j++)
+                if (j < i) r -= lpc[j] * autoc[i - j];
+            r /= e;
+            lpc[i] = r;
+#pragma unroll
+            for (int j = 0; j < kMaxLpc / 2; j++) {
+                if (j < (i >> 1)) {
+                    double tmp = lpc[j];
+                    lpc[j] += r * lpc[i - 1 - j];
+                    lpc[i - 1 - j] += r * tmp;
+                }
+            }
+            if (i & 1) lpc[i >> 1] += lpc[i >> 1] * r;
+            e *= (1.0 - r * r);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kMaxLpc; j++) lp[j] = j < order ? (float)(-lpc[j]) : 0.0f;
+}
+
+// FLAC__lpc_compute_expected_bits_per_residual_sample_with_error_scale
+__device__ inline double expected_bits(double lpc_error, double error_scale) {
+    if (lpc_error > 0.0) {
+        double b = 0.5 * log(error_scale * lpc_error) / M_LN2;
+        return b >= 0.0 ? b : 0.0;
+    } else if (lpc_error < 0.0) {
+        return 1e32;
+    }
+    return 0.0;
+}
+
+// ------------------------------------------------------------------------------------ k_analyze
+// One lane per subframe; lanes of a wave walk their blocks in lockstep so the window sample is uniform.
+template <int DT, bool WIDE>
+__global__ void __launch_bounds__(128) k_analyze(const typename Elem<DT>::T *raster, EncodeParams P,
+                                                const TileGeom *tiles, const TileNorm *norms,
+                                                const float *__restrict__ window, SubAnalysis *out) {
+    using T = typename Elem<DT>::T;
+    const int64_t sub = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nsub = P.nframes * P.nch;
+    const bool live = sub < nsub;
+    const int64_t f = live ? sub / P.nch : 0;
+    const int ch = live ? (int)(sub - f * P.nch) : 0;
+    const int t = tile_of_frame(tiles, P.ntiles, f);
+    const TileGeom g = tiles[t];
+    const int64_t s0 = (f - g.frame_base) * P.blocksize;
+    const int64_t tile_px = (int64_t)g.h * g.w;
+    const int n = live ? (int)((tile_px - s0) < P.blocksize ? (tile_px - s0) : P.blocksize) : 0;
+    const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits);
+
+    int64_t row = s0 / g.w;
+    int col = (int)(s0 - row * g.w);
+    const T *rowp = raster + (int64_t)(P.band0 + ch) * P.band_stride + (g.r0 + row) * P.row_stride + g.c0;
+
+    uint32_t or_acc = 0, diff = 0;
+    int32_t x0 = 0, x1 = 0, p1 = 0, p2 = 0, p3 = 0;
+    uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+    double acc[kMaxLpc + 1];
+#pragma unroll
+    for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
+    double prev[8], cur[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) prev[j] = 0.0;
+
+    const int nloop = P.blocksize;  // uniform trip count; lanes with shorter blocks are predicated off
+    for (int i0 = 0; i0 < nloop; i0 += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int i = i0 + j;
+            int32_t x = 0;
+            if (i < n) {
+                x = nz(rowp[col]);
+                if (++col == g.w) {
+                    col = 0;
+                    rowp += P.row_stride;
+                }
+                if (i == 0) x0 = x;
+                or_acc |= (uint32_t)x;
+                diff |= (uint32_t)(x ^ x0);
+                if constexpr (!WIDE) {
+                    // 16-bit streams: |e_k| < 2^20, totals over samples 4..n-1 (fixed.c, data+4)
+                    const int32_t e1 = x - x1, e2 = e1 - p1, e3 = e2 - p2, e4 = e3 - p3;
+                    if (i >= 4) {
+                        t0 += (uint32_t)abs(x);
+                        t1 += (uint32_t)abs(e1);
+                        t2 += (uint32_t)abs(e2);
+                        t3 += (uint32_t)abs(e3);
+                        t4 += (uint32_t)abs(e4);
+                    }
+                    p3 = e3;
+                    p2 = e2;
+                    p1 = e1;
+                    x1 = x;
+                }
+            }
+            // inactive lanes have x == 0 -> contribute exact zeros; window index is wave-uniform
+            cur[j] = (double)((float)x * window[i]);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+#pragma unroll
+            for (int l = 0; l <= kMaxLpc; l++) {
+                const double other = (j - l >= 0) ? cur[j - l] : prev[8 + j - l];
+                acc[l] = fma(cur[j], other, acc[l]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) prev[j] = cur[j];
+    }
+    if (!live) return;
+
+    SubAnalysis A;
+    A.n = n;
+    int w = 0;
+    if (or_acc) w = __builtin_ctz(or_acc);
+    if (w > P.bps) w = P.bps;
+    const int sbps = P.bps - w;
+    A.wasted = w;
+    A.flags = 0;
+    A.fixed_order = 0;
+    A.lpc_order = 0;
+    A.lpc_prec = 0;
+    A.lpc_shift = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxLpc; j++) A.q[j] = 0;
+
+    if (n > 4) {
+        // fixed predictor guess (FLAC__fixed_compute_best_predictor on the shifted signal)
+        float fb[5];
+        int guess;
+        {
+            const uint64_t T0 = t0 >> w, T1 = t1 >> w, T2 = t2 >> w, T3 = t3 >> w, T4 = t4 >> w;
+            uint64_t m = T1 < T2 ? T1 : T2;
+            m = m < T3 ? m : T3;
+            m = m < T4 ? m : T4;
+            if (T0 <= m) guess = 0;
+            else {
+                uint64_t m2_ = T2 < T3 ? T2 : T3;
+                m2_ = m2_ < T4 ? m2_ : T4;
+                if (T1 <= m2_) guess = 1;
+                else if (T2 <= (T3 < T4 ? T3 : T4)) guess = 2;
+                else if (T3 <= T4) guess = 3;
+                else guess = 4;
+            }
+            const uint64_t Ts[5] = {T0, T1, T2, T3, T4};
+            const double dn = (double)(n - 4);
+#pragma unroll
+            for (int k = 0; k < 5; k++)
+                fb[k] = (float)(Ts[k] > 0 ? log(M_LN2 * (double)Ts[k] / dn) / M_LN2 : 0.0);
+        }
+        // 32-bit streams: constant / fixed decisions come from k_analyze_fixed_wide (limit_residual
+        // estimator); a constant block there clears the LPC candidate again.
+        if (!WIDE && fb[1] == 0.0f && diff == 0) {
+            A.flags |= kFlagConstant;
+        } else {
+            A.fixed_order = guess;
+            float fg = fb[0];
+#pragma unroll
+            for (int k = 1; k < 5; k++)
+                if (k == guess) fg = fb[k];
+            if (!(fg >= (float)sbps)) A.flags |= kFlagFixedOk;
+
+            int max_order = kMaxLpc < n ? kMaxLpc : n - 1;
+            // autocorrelation of the shifted signal = autoc * 4^-w exactly (power-of-two scaling)
+            double autoc[kMaxLpc + 1];
+            const double sc = ldexp(1.0, -2 * w);
+#pragma unroll
+            for (int l = 0; l <= kMaxLpc; l++) autoc[l] = acc[l] * sc;
+            if (max_order > 0 && autoc[0] != 0.0) {
+                double err[kMaxLpc];
+                const int mo = levinson_errors(autoc, max_order, err);
+                // FLAC__lpc_compute_best_order with overhead = subframe_bps + qlp_coeff_precision
+                const double es = 0.5 / (double)n;
+                const int ovh = sbps + P.qlp_precision;
+                int best = 0;
+                double best_bits = (double)(unsigned)(-1);
+#pragma unroll
+                for (int i = 0; i < kMaxLpc; i++) {
+                    if (i < mo) {
+                        const int o = i + 1;
+                        const double b = expected_bits(err[i], es) * (double)(n - o) + (double)(o * ovh);
+                        if (b < best_bits) {
+                            best = i;
+                            best_bits = b;
+                        }
+                    }
+                }
+                const int o = best + 1;
+                double eo = err[0];
+#pragma unroll
+                for (int i = 1; i < kMaxLpc; i++)
+                    if (i == best) eo = err[i];
+                const double lbits = expected_bits(eo, 0.5 / (double)(n - o));
+                if (!(lbits >= (double)sbps)) {
+                    int prec = P.qlp_precision;
+                    if (sbps <= 17) {
+                        const int lim = 32 - sbps - ilog2_u32((uint32_t)o);
+                        prec = lim < prec ? lim : prec;
+                    }
+                    float lp[kMaxLpc];
+                    levinson_coefs(autoc, o, lp);
+                    // FLAC__lpc_quantize_coefficients
+                    const int pm1 = prec - 1;
+                    const int32_t qmax = (1 << pm1) - 1, qmin = -(1 << pm1);
+                    double cmax = 0.0;
+#pragma unroll
+                    for (int j = 0; j < kMaxLpc; j++)
+                        if (j < o) {
+                            const double d = fabs((double)lp[j]);
+                            if (d > cmax) cmax = d;
+                        }
+                    if (cmax > 0.0) {
+                        const int log2cmax = ilogb(cmax);  // frexp exponent - 1
+                        int shift = pm1 - log2cmax - 1;
+                        bool ok = true;
+                        if (shift > 15) shift = 15;
+                        else if (shift < -16) ok = false;
+                        if (ok) {
+                            double error = 0.0;
+                            if (shift >= 0) {
+                                const float m = (float)(1 << shift);
+#pragma unroll
+                                for (int j = 0; j < kMaxLpc; j++)
+                                    if (j < o) {
+                                        error += (double)(lp[j] * m);
+                                        int64_t qi = lround_exact(error);
+                                        if (qi > qmax) qi = qmax;
+                                        else if (qi < qmin) qi = qmin;
+                                        error -= (double)qi;
+                                        A.q[j] = (int32_t)qi;
+                                    }
+                            } else {
+                                const float m = (float)(1 << (-shift));
+#pragma unroll
+                                for (int j = 0; j < kMaxLpc; j++)
+                                    if (j < o) {
+                                        error += (double)(lp[j] / m);
+                                        int64_t qi = lround_exact(error);
+                                        if (qi > qmax) qi = qmax;
+                                        else if (qi < qmin) qi = qmin;
+                                        error -= (double)qi;
+                                        A.q[j] = (int32_t)qi;
+                                    }
+                                shift = 0;
+                            }
+                            A.lpc_order = o;
+                            A.lpc_prec = prec;
+                            A.lpc_shift = shift;
+                            A.flags |= kFlagLpcOk;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    out[sub] = A;
+}
+
+// 32-bit streams (bits_per_sample 24 -> pyflac bps 32) use libFLAC's limit_residual fixed estimator;
+// it needs 64-bit errors and validity tracking, done in a separate exact pass per lane.
+template <int DT>
+__global__ void __launch_bounds__(128) k_analyze_fixed_wide(const typename Elem<DT>::T *raster, EncodeParams P,
+                                                           const TileGeom *tiles, const TileNorm *norms,
+                                                           SubAnalysis *out) {
+    using T = typename Elem<DT>::T;
+    const int64_t sub = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (sub >= P.nframes * P.nch) return;
+    const int64_t f = sub / P.nch;
+    const int ch = (int)(sub - f * P.nch);
+    const int t = tile_of_frame(tiles, P.ntiles, f);
+    const TileGeom g = tiles[t];
+    const int64_t s0 = (f - g.frame_base) * P.blocksize;
+    const int64_t tile_px = (int64_t)g.h * g.w;
+    const int n = (int)((tile_px - s0) < P.blocksize ? (tile_px - s0) : P.blocksize);
+    const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits);
+    SubAnalysis A = out[sub];
+    if (n <= 4) return;
+    const int w = A.wasted;
+    const int sbps = P.bps - w;
+    int64_t row = s0 / g.w;
+    int col = (int)(s0 - row * g.w);
+    const T *rowp = raster + (int64_t)(P.band0 + ch) * P.band_stride + (g.r0 + row) * P.row_stride + g.c0;
+    int64_t h1 = 0, h2 = 0, h3 = 0, h4 = 0;
+    uint64_t tt[5] = {0, 0, 0, 0, 0};
+    bool valid[5] = {true, true, true, true, true};
+    for (int i = 0; i < n; i++) {
+        const int64_t x = (int64_t)(nz(rowp[col]) >> w);
+        if (++col == g.w) {
+            col = 0;
+            rowp += P.row_stride;
+        }
+        uint64_t e[5];
+        e[0] = (uint64_t)(x < 0 ? -x : x);
+        int64_t v;
+        v = x - h1;
+        e[1] = i >= 1 ? (uint64_t)(v < 0 ? -v : v) : 0;
+        v = x - 2 * h1 + h2;
+        e[2] = i >= 2 ? (uint64_t)(v < 0 ? -v : v) : 0;
+        v = x - 3 * h1 + 3 * h2 - h3;
+        e[3] = i >= 3 ? (uint64_t)(v < 0 ? -v : v) : 0;
+        v = x - 4 * h1 + 6 * h2 - 4 * h3 + h4;
+        e[4] = i >= 4 ? (uint64_t)(v < 0 ? -v : v) : 0;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            tt[k] += e[k];
+            if (e[k] > (uint64_t)INT32_MAX) valid[k] = false;
+        }
+        h4 = h3;
+        h3 = h2;
+        h2 = h1;
+        h1 = x;
+    }
+    // CHECK_ORDER_IS_VALID (fixed.c, limit_residual): estimate uses total_error_0 for every order
+    uint64_t smallest = UINT64_MAX;
+    int order = 0;
+    float fb[5];
+    const double dn = (double)(n - 4);
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        if (valid[k] && tt[k] < smallest) {
+            order = k;
+            smallest = tt[k];
+            fb[k] = (float)(tt[0] > 0 ? log(M_LN2 * (double)tt[0] / dn) / M_LN2 : 0.0);
+        } else {
+            fb[k] = 34.0f;
+        }
+    }
+    int flags = A.flags & ~(kFlagConstant | kFlagFixedOk);
+    bool constant = false;
+    if (fb[1] == 0.0f) {
+        // all samples equal?  (rare; re-walk)
+        row = s0 / g.w;
+        col = (int)(s0 - row * g.w);
+        rowp = raster + (int64_t)(P.band0 + ch) * P.band_stride + (g.r0 + row) * P.row_stride + g.c0;
+        int32_t first = 0;
+        constant = true;
+        for (int i = 0; i < n; i++) {
+            int32_t x = nz(rowp[col]);
+            if (++col == g.w) {
+                col = 0;
+                rowp += P.row_stride;
+            }
+            if (i == 0) first = x;
+            else if (x != first) {
+                constant = false;
+                break;
+            }
+        }
+    }
+    if (constant) {
+        A.flags = (flags & ~kFlagLpcOk) | kFlagConstant;
+    } else {
+        A.fixed_order = order;
+        float fg = fb[0];
+#pragma unroll
+        for (int k = 1; k < 5; k++)
+            if (k == order) fg = fb[k];
+        if (!(fg >= (float)sbps)) flags |= kFlagFixedOk;
+        A.flags = flags;
+    }
+    out[sub] = A;
+}
+
+// ------------------------------------------------------------------------------ k_encode_frames
+constexpr int kEncThreads = 256;
+constexpr int kBitWords = 4096 + 64;  // one 32-bit subframe (4096 x 32 bits) + headers + carry
+
+__constant__ uint8_t c_crc8[256];
+
+struct RiceChoice {
+    uint32_t bits;   // estimated residual bits (find_best_partition_order_)
+    int order;       // partition order
+    int rice2;
+    uint8_t k[32];   // parameters
+};
+
+// set_partitioned_rice_ for every order in [0, max_po] from the max-order partition sums; returns best.
+__device__ void rice_search(const uint64_t *sums_max, int max_po, int n, int pred_order, int rice_limit,
+                            RiceChoice *rc) {
+    uint64_t sums[64];
+    const int parts = 1 << max_po;
+    for (int p = 0; p < parts; p++) sums[p] = sums_max[p];
+    int from = 0, to = parts, pp = parts;
+    for (int po = max_po - 1; po >= 0; po--) {
+        pp >>= 1;
+        for (int i = 0; i < pp; i++) {
+            sums[to++] = sums[from] + sums[from + 1];
+            from += 2;
+        }
+    }
+    uint32_t best_bits = 0;
+    int sumoff = 0;
+    for (int po = max_po; po >= 0; po--) {
+        const int np = 1 << po;
+        const uint32_t pbase = (uint32_t)(n >> po);
+        const uint32_t div_base = 0x40000u / pbase;
+        uint32_t bits = 2 + 4;
+        uint8_t ks[32];
+        bool ok = true;
+        for (int p = 0; p < np; p++) {
+            uint32_t ns = pbase, div = div_base;
+            if (p == 0) {
+                if (ns <= (uint32_t)pred_order) {
+                    ok = false;
+                    break;
+                }
+                ns -= (uint32_t)pred_order;
+                div = 0x40000u / ns;
+            }
+            const uint64_t mean = sums[sumoff + p];
+            uint32_t k;
+            if (mean < 2 || (((mean - 1) * div) >> 18) == 0) k = 0;
+            else k = (uint32_t)ilog2_u64(((mean - 1) * div) >> 18) + 1;
+            if (k >= (uint32_t)rice_limit) k = (uint32_t)rice_limit - 1;
+            uint64_t pb = 4 + (uint64_t)(1 + k) * ns + (k ? (mean >> (k - 1)) : (mean << 1)) - (ns >> 1);
+            if (pb > 0xFFFFFFFFull) pb = 0xFFFFFFFFull;
+            bits += (uint32_t)pb;
+            ks[p] = (uint8_t)k;
+        }
+        if (!ok) break;
+        sumoff += np;
+        if (best_bits == 0 || bits < best_bits) {
+            best_bits = bits;
+            rc->order = po;
+            for (int p = 0; p < np; p++) rc->k[p] = ks[p];
+        }
+    }
+    rc->bits = best_bits;
+    rc->rice2 = 0;
+    for (int p = 0; p < (1 << rc->order); p++)
+        if (rc->k[p] >= 15) rc->rice2 = 1;
+}
+
+// LDS bit writer: MSB-first bit positions relative to the word-aligned buffer base.
+__device__ inline void put_bits(uint32_t *buf, uint64_t pos, uint32_t val, int nbits) {
+    if (nbits <= 0) return;
+    const uint32_t wi = (uint32_t)(pos >> 5);
+    const int off = (int)(pos & 31);
+    const uint64_t v = (uint64_t)val << (64 - off - nbits);
+    atomicOr(&buf[wi], (uint32_t)(v >> 32));
+    const uint32_t lo = (uint32_t)v;
+    if (lo) atomicOr(&buf[wi + 1], lo);
+}
+
+__device__ inline uint32_t mask_bits(int64_t v, int n) { return n >= 32 ? (uint32_t)v : (uint32_t)v & ((1u << n) - 1u); }
+
+struct EncShared {
+    int32_t xs[kMaxBlock];
+    uint32_t bits[kBitWords];
+    uint64_t psum[2][32];
+    uint32_t scan[kEncThreads];
+    RiceChoice rc[2];
+    int lpc_bad;
+    int choice;        // subframe type: 0 const, 1 verbatim, 2 fixed, 3 lpc
+    uint32_t est[4];
+};
+
+template <int DT>
+__global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename Elem<DT>::T *raster, EncodeParams P,
+                                                             const TileGeom *tiles, const TileNorm *norms,
+                                                             const SubAnalysis *ana, uint32_t *slots,
+                                                             int64_t *frame_bytes, int *error_flag) {
+    using T = typename Elem<DT>::T;
+    __shared__ EncShared S;
+    const int tid = threadIdx.x;
+    const int64_t f = blockIdx.x;
+    const int t = tile_of_frame(tiles, P.ntiles, f);
+    const TileGeom g = tiles[t];
+    const int64_t fk = f - g.frame_base;  // frame number within the tile's stream
+    const int64_t s0 = fk * P.blocksize;
+    const int64_t tile_px = (int64_t)g.h * g.w;
+    const int n = (int)((tile_px - s0) < P.blocksize ? (tile_px - s0) : P.blocksize);
+    const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits);
+    uint32_t *slot = slots + (size_t)f * P.slot_words;
+    const int rice_limit = P.bps > 16 ? 31 : 15;
+    const int max_po_block = min(kMaxPartOrder, __builtin_ctz((unsigned)n));
+
+    for (int i = tid; i < kBitWords; i += kEncThreads) S.bits[i] = 0;
+    __syncthreads();
+
+    // ---- frame header (RFC 9639 9.1; libFLAC FLAC__frame_add_header), thread 0
+    uint64_t fb = 0;  // frame bit cursor relative to S.bits word 0
+    int64_t w0 = 0;   // global slot word index of S.bits[0]
+    {
+        __shared__ int hdr_bits;
+        if (tid == 0) {
+            uint8_t h[16];
+            int hb = 0;
+            int bsc, bsx = 0;
+            switch (n) {
+            case 192: bsc = 1; break;
+            case 576: bsc = 2; break;
+            case 1152: bsc = 3; break;
+            case 2304: bsc = 4; break;
+            case 4608: bsc = 5; break;
+            case 256: bsc = 8; break;
+            case 512: bsc = 9; break;
+            case 1024: bsc = 10; break;
+            case 2048: bsc = 11; break;
+            case 4096: bsc = 12; break;
+            case 8192: bsc = 13; break;
+            case 16384: bsc = 14; break;
+            case 32768: bsc = 15; break;
+            default: bsc = bsx = (n <= 256 ? 6 : 7); break;
+            }
+            int src, srx = 0;
+            const int sr = P.sample_rate;
+            switch (sr) {
+            case 88200: src = 1; break;
+            case 176400: src = 2; break;
+            case 192000: src = 3; break;
+            case 8000: src = 4; break;
+            case 16000: src = 5; break;
+            case 22050: src = 6; break;
+            case 24000: src = 7; break;
+            case 32000: src = 8; break;
+            case 44100: src = 9; break;
+            case 48000: src = 10; break;
+            case 96000: src = 11; break;
+            default:
+                if (sr <= 255000 && sr % 1000 == 0) src = srx = 12;
+                else if (sr % 10 == 0 && sr / 10 <= 65535) src = srx = 14;
+                else src = srx = 13;
+            }
+            int bpc = P.bps == 8 ? 1 : P.bps == 12 ? 2 : P.bps == 16 ? 4 : P.bps == 20 ? 5 : P.bps == 24 ? 6 : P.bps == 32 ? 7 : 0;
+            h[hb++] = 0xFF;
+            h[hb++] = 0xF8;
+            h[hb++] = (uint8_t)((bsc << 4) | src);
+            h[hb++] = (uint8_t)(((P.nch - 1) << 4) | (bpc << 1));
+            const uint32_t v = (uint32_t)fk;
+            if (v < 0x80) h[hb++] = (uint8_t)v;
+            else if (v < 0x800) { h[hb++] = (uint8_t)(0xC0 | (v >> 6)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+            else if (v < 0x10000) { h[hb++] = (uint8_t)(0xE0 | (v >> 12)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+            else if (v < 0x200000) { h[hb++] = (uint8_t)(0xF0 | (v >> 18)); h[hb++] = (uint8_t)(0x80 | ((v >> 12) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+            else if (v < 0x4000000) { h[hb++] = (uint8_t)(0xF8 | (v >> 24)); h[hb++] = (uint8_t)(0x80 | ((v >> 18) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 12) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+            else { h[hb++] = (uint8_t)(0xFC | (v >> 30)); h[hb++] = (uint8_t)(0x80 | ((v >> 24) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 18) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 12) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+            if (bsx == 6) h[hb++] = (uint8_t)(n - 1);
+            else if (bsx == 7) { h[hb++] = (uint8_t)((n - 1) >> 8); h[hb++] = (uint8_t)(n - 1); }
+            if (srx == 12) h[hb++] = (uint8_t)(sr / 1000);
+            else if (srx == 13) { h[hb++] = (uint8_t)(sr >> 8); h[hb++] = (uint8_t)sr; }
+            else if (srx == 14) { h[hb++] = (uint8_t)((sr / 10) >> 8); h[hb++] = (uint8_t)(sr / 10); }
+            uint8_t c = 0;
+            for (int i = 0; i < hb; i++) c = c_crc8[c ^ h[i]];
+            h[hb++] = c;
+            for (int i = 0; i < hb; i++) put_bits(S.bits, (uint64_t)i * 8, h[i], 8);
+            hdr_bits = hb * 8;
+        }
+        __syncthreads();
+        fb = (uint64_t)hdr_bits;
+    }
+
+    for (int c = 0; c < P.nch; c++) {
+        const SubAnalysis A = ana[f * P.nch + c];
+        const int w = A.wasted;
+        const int sbps = P.bps - w;
+        // ---- load + normalise the block into LDS (strided over threads: coalesced row segments)
+        {
+            const T *base = raster + (int64_t)(P.band0 + c) * P.band_stride + g.r0 * P.row_stride + g.c0;
+            for (int i = tid; i < n; i += kEncThreads) {
+                const int64_t p = s0 + i;
+                const int64_t r = p / g.w;
+                const int cc = (int)(p - r * g.w);
+                S.xs[i] = nz(base[r * P.row_stride + cc]) >> w;
+            }
+        }
+        if (tid < 64) {
+            S.psum[tid >> 5][tid & 31] = 0;
+        }
+        if (tid == 0) S.lpc_bad = 0;
+        __syncthreads();
+
+        // ---- candidate residual partition sums (FIXED guess and LPC)
+        const bool cand_fixed = n > 4 && !(A.flags & kFlagConstant) && (A.flags & kFlagFixedOk);
+        const bool cand_lpc = n > 4 && !(A.flags & kFlagConstant) && (A.flags & kFlagLpcOk);
+        int mpo[2] = {0, 0};
+        {
+            int o = A.fixed_order;
+            int m = max_po_block;
+            while (m > 0 && (n >> m) <= o) m--;
+            mpo[0] = m;
+            o = A.lpc_order;
+            m = max_po_block;
+            while (m > 0 && (n >> m) <= o) m--;
+            mpo[1] = m;
+        }
+        const int chunk = (n + kEncThreads - 1) / kEncThreads;
+        const int i_beg = tid * chunk, i_end = min(n, i_beg + chunk);
+        for (int cand = 0; cand < 2; cand++) {
+            if (cand == 0 && !cand_fixed) continue;
+            if (cand == 1 && !cand_lpc) continue;
+            const int o = cand == 0 ? A.fixed_order : A.lpc_order;
+            const int ps = n >> mpo[cand];
+            int cur_p = -1;
+            uint64_t acc = 0;
+            for (int i = max(i_beg, o); i < i_end; i++) {
+                int64_t r;
+                if (cand == 0) {
+                    const int64_t x = S.xs[i];
+                    switch (o) {
+                    case 0: r = x; break;
+                    case 1: r = x - S.xs[i - 1]; break;
+                    case 2: r = x - 2 * (int64_t)S.xs[i - 1] + S.xs[i - 2]; break;
+                    case 3: r = x - 3 * (int64_t)S.xs[i - 1] + 3 * (int64_t)S.xs[i - 2] - S.xs[i - 3]; break;
+                    default: r = x - 4 * (int64_t)S.xs[i - 1] + 6 * (int64_t)S.xs[i - 2] - 4 * (int64_t)S.xs[i - 3] + S.xs[i - 4]; break;
+                    }
+                    r = (int32_t)r;  // libFLAC stores fixed residuals as int32
+                } else {
+                    int64_t s = 0;
+                    for (int j = 0; j < o; j++) s += (int64_t)A.q[j] * S.xs[i - 1 - j];
+                    r = (int64_t)S.xs[i] - (s >> A.lpc_shift);
+                    if (r <= INT32_MIN || r > INT32_MAX) S.lpc_bad = 1;
+                }
+                const int p = i / ps;
+                if (p != cur_p) {
+                    if (cur_p >= 0) atomicAdd((unsigned long long *)&S.psum[cand][cur_p], (unsigned long long)acc);
+                    cur_p = p;
+                    acc = 0;
+                }
+                acc += (uint64_t)(r < 0 ? -r : r);
+            }
+            if (cur_p >= 0) atomicAdd((unsigned long long *)&S.psum[cand][cur_p], (unsigned long long)acc);
+        }
+        __syncthreads();
+
+        // ---- decisions (process_subframe_ evaluation order: VERBATIM, CONSTANT | FIXED, LPC; strict <)
+        if (tid == 0 || tid == 64) {
+            const int cand = tid == 0 ? 0 : 1;
+            const bool on = cand == 0 ? cand_fixed : (cand_lpc && !S.lpc_bad);
+            if (on) rice_search(S.psum[cand], mpo[cand], n, cand == 0 ? A.fixed_order : A.lpc_order, rice_limit, &S.rc[cand]);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t best = (uint32_t)(1 + 6 + 1 + w + n * sbps);
+            int type = 1;
+            if (n > 4) {
+                if (A.flags & kFlagConstant) {
+                    const uint32_t cb = (uint32_t)(1 + 6 + 1 + w + sbps);
+                    if (cb < best) {
+                        best = cb;
+                        type = 0;
+                    }
+                } else {
+                    if (cand_fixed) {
+                        uint32_t est = (uint32_t)(1 + 6 + 1 + w + A.fixed_order * sbps);
+                        est = (S.rc[0].bits < 0xFFFFFFFFu - est) ? est + S.rc[0].bits : 0xFFFFFFFFu;
+                        if (est < best) {
+                            best = est;
+                            type = 2;
+                        }
+                    }
+                    if (cand_lpc && !S.lpc_bad) {
+                        uint32_t est = (uint32_t)(1 + 6 + 1 + w + 4 + 5 + sbps * A.lpc_order + A.lpc_prec * A.lpc_order);
+                        est = (S.rc[1].bits < 0xFFFFFFFFu - est) ? est + S.rc[1].bits : 0xFFFFFFFFu;
+                        if (est != 0 && est < best) {
+                            best = est;
+                            type = 3;
+                        }
+                    }
+                }
+            }
+            S.choice = type;
+        }
+        __syncthreads();
+        const int type = S.choice;
+
+        // ---- emit the subframe bits at fb (relative to S.bits)
+        const uint64_t sb = fb;
+        uint64_t pos = sb;
+        const int typecode = type == 0 ? 0 : type == 1 ? 1 : type == 2 ? 8 + A.fixed_order : 32 + A.lpc_order - 1;
+        if (tid == 0) {
+            put_bits(S.bits, pos, (uint32_t)(typecode << 1) | (w ? 1u : 0u), 8);
+        }
+        pos += 8;
+        if (w) {
+            if (tid == 0) put_bits(S.bits, pos + (uint64_t)(w - 1), 1, 1);
+            pos += (uint64_t)w;
+        }
+        uint64_t sub_end;
+        if (type == 0) {
+            if (tid == 0) put_bits(S.bits, pos, mask_bits(S.xs[0], sbps), sbps);
+            sub_end = pos + (uint64_t)sbps;
+        } else if (type == 1) {
+            for (int i = tid; i < n; i += kEncThreads)
+                put_bits(S.bits, pos + (uint64_t)i * sbps, mask_bits(S.xs[i], sbps), sbps);
+            sub_end = pos + (uint64_t)n * sbps;
+        } else {
+            const int o = type == 2 ? A.fixed_order : A.lpc_order;
+            const RiceChoice &rc = S.rc[type == 2 ? 0 : 1];
+            for (int i = tid; i < o; i++) put_bits(S.bits, pos + (uint64_t)i * sbps, mask_bits(S.xs[i], sbps), sbps);
+            pos += (uint64_t)o * sbps;
+            if (type == 3) {
+                if (tid == 0) {
+                    put_bits(S.bits, pos, (uint32_t)(A.lpc_prec - 1), 4);
+                    put_bits(S.bits, pos + 4, mask_bits(A.lpc_shift, 5), 5);
+                }
+                pos += 9;
+                for (int j = tid; j < o; j += kEncThreads)
+                    put_bits(S.bits, pos + (uint64_t)j * A.lpc_prec, mask_bits(A.q[j], A.lpc_prec), A.lpc_prec);
+                pos += (uint64_t)o * A.lpc_prec;
+            }
+            if (tid == 0) {
+                put_bits(S.bits, pos, (uint32_t)rc.rice2, 2);
+                put_bits(S.bits, pos + 2, (uint32_t)rc.order, 4);
+            }
+            pos += 6;
+            const int pbits = rc.rice2 ? 5 : 4;
+            const int po = rc.order;
+            const int ps = n >> po;
+            // per-thread code lengths of its chunk, then block exclusive scan
+            uint64_t my = 0;
+            for (int i = max(i_beg, o); i < i_end; i++) {
+                int64_t r;
+                if (type == 2) {
+                    const int64_t x = S.xs[i];
+                    switch (o) {
+                    case 0: r = x; break;
+                    case 1: r = x - S.xs[i - 1]; break;
+                    case 2: r = x - 2 * (int64_t)S.xs[i - 1] + S.xs[i - 2]; break;
+                    case 3: r = x - 3 * (int64_t)S.xs[i - 1] + 3 * (int64_t)S.xs[i - 2] - S.xs[i - 3]; break;
+                    default: r = x - 4 * (int64_t)S.xs[i - 1] + 6 * (int64_t)S.xs[i - 2] - 4 * (int64_t)S.xs[i - 3] + S.xs[i - 4]; break;
+                    }
+                } else {
+                    int64_t s = 0;
+                    for (int j = 0; j < o; j++) s += (int64_t)A.q[j] * S.xs[i - 1 - j];
+                    r = (int64_t)S.xs[i] - (s >> A.lpc_shift);
+                }
+                const int32_t r32 = (int32_t)r;
+                const uint32_t u = ((uint32_t)r32 << 1) ^ (uint32_t)(r32 >> 31);
+                const int k = rc.k[i / ps];
+                my += 1 + (uint64_t)k + (u >> k);
+            }
+            // block scan of my (bit counts fit 32 bits per thread chunk for sane data; use 64-bit total)
+            // two-level: wave inclusive scan with shuffles, then wave totals in LDS.
+            uint64_t incl = my;
+            const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint64_t y = __shfl_up(incl, d);
+                if (lane >= d) incl += y;
+            }
+            __shared__ uint64_t wtot[kEncThreads / 64];
+            if (lane == 63) wtot[wv] = incl;
+            __syncthreads();
+            uint64_t wbase = 0;
+            for (int k = 0; k < wv; k++) wbase += wtot[k];
+            const uint64_t excl = wbase + incl - my;
+            uint64_t total = 0;
+            for (int k = 0; k < kEncThreads / 64; k++) total += wtot[k];
+            sub_end = pos + (uint64_t)pbits * (1 << po) + total;
+            if (sub_end > (uint64_t)kBitWords * 32 - 64) {  // exact code longer than the LDS window
+                if (tid == 0) atomicOr(error_flag, 2);
+                return;  // uniform: every thread sees the same sub_end
+            }
+            // bit position of sample i = pos + pbits*(p_i + 1) + (sum of code lengths before i);
+            // partition p's parameter field precedes its first code
+            uint64_t run = excl;
+            __shared__ uint64_t pstart[32];
+            for (int i = max(i_beg, o); i < i_end; i++) {
+                int64_t r;
+                if (type == 2) {
+                    const int64_t x = S.xs[i];
+                    switch (o) {
+                    case 0: r = x; break;
+                    case 1: r = x - S.xs[i - 1]; break;
+                    case 2: r = x - 2 * (int64_t)S.xs[i - 1] + S.xs[i - 2]; break;
+                    case 3: r = x - 3 * (int64_t)S.xs[i - 1] + 3 * (int64_t)S.xs[i - 2] - S.xs[i - 3]; break;
+                    default: r = x - 4 * (int64_t)S.xs[i - 1] + 6 * (int64_t)S.xs[i - 2] - 4 * (int64_t)S.xs[i - 3] + S.xs[i - 4]; break;
+                    }
+                } else {
+                    int64_t s = 0;
+                    for (int j = 0; j < o; j++) s += (int64_t)A.q[j] * S.xs[i - 1 - j];
+                    r = (int64_t)S.xs[i] - (s >> A.lpc_shift);
+                }
+                const int32_t r32 = (int32_t)r;
+                const uint32_t u = ((uint32_t)r32 << 1) ^ (uint32_t)(r32 >> 31);
+                const int p = i / ps;
+                const int k = rc.k[p];
+                const uint32_t q = u >> k;
+                const int first_of_p = p == 0 ? o : p * ps;
+                if (i == first_of_p) pstart[p] = run;  // codes before this partition
+                const uint64_t at = pos + (uint64_t)pbits * (p + 1) + run + q;
+                const uint32_t low = k ? (u & ((1u << k) - 1u)) : 0u;
+                put_bits(S.bits, at, (1u << k) | low, k + 1);
+                run += 1 + (uint64_t)k + q;
+            }
+            __syncthreads();
+            for (int p = tid; p < (1 << po); p += kEncThreads)
+                put_bits(S.bits, pos + (uint64_t)pbits * p + pstart[p], rc.k[p], pbits);
+        }
+        __syncthreads();
+        // ---- flush complete words of S.bits to the slot, keep the partial word
+        {
+            const uint64_t full = sub_end >> 5;
+            if ((int64_t)(w0 + full) + 2 > P.slot_words) {
+                if (tid == 0) atomicOr(error_flag, 1);
+                return;
+            }
+            for (uint64_t i = tid; i < full; i += kEncThreads) slot[w0 + i] = __builtin_bswap32(S.bits[i]);
+            __syncthreads();
+            const uint32_t keep = S.bits[full];
+            __syncthreads();
+            for (int i = tid; i < kBitWords; i += kEncThreads) S.bits[i] = 0;
+            __syncthreads();
+            if (tid == 0) S.bits[0] = keep;
+            __syncthreads();
+            w0 += (int64_t)full;
+            fb = sub_end - (full << 5);
+        }
+    }
+    // ---- byte-align; the final partial word goes out whole (zero tail)
+    const uint64_t bits_total = (uint64_t)w0 * 32 + fb;
+    const uint64_t bytes = (bits_total + 7) >> 3;
+    if (fb && tid == 0) slot[w0] = __builtin_bswap32(S.bits[0]);
+    if (tid == 0) frame_bytes[f] = (int64_t)bytes + 2;  // + CRC-16 footer
+}
+
+// ------------------------------------------------------------------------------------ k_compact
+__constant__ uint16_t c_crc16[256];
+__constant__ uint16_t c_xpow8[40];  // x^(8 * 2^j) mod P, j = 0..39
+
+__device__ inline uint32_t gf_mulmod(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 15; i >= 0; i--) {
+        r <<= 1;
+        if (r & 0x10000u) r ^= 0x18005u;
+        if ((b >> i) & 1u) r ^= a;
+    }
+    return r;
+}
+
+__device__ inline uint32_t xpow8(uint64_t m) {  // x^(8m) mod P
+    uint32_t r = 1;
+    int j = 0;
+    while (m) {
+        if (m & 1) r = gf_mulmod(r, c_xpow8[j]);
+        m >>= 1;
+        j++;
+    }
+    return r;
+}
+
+__global__ void __launch_bounds__(256) k_compact(const uint32_t *slots, int slot_words, const int64_t *frame_bytes,
+                                                const int64_t *frame_off, int64_t nframes, uint8_t *arena) {
+    const int64_t f = blockIdx.x;
+    if (f >= nframes) return;
+    const uint8_t *src = reinterpret_cast<const uint8_t *>(slots + (size_t)f * slot_words);
+    const int64_t S = frame_bytes[f];
+    const int64_t L = S - 2;  // CRC covers everything before the footer
+    const int64_t D = frame_off[f];
+    // CRC-16: chunked, each chunk's CRC shifted to the end of the frame, XOR-combined (linear, init 0)
+    const int64_t ch = (L + 255) / 256;
+    const int64_t b0 = min(L, (int64_t)threadIdx.x * ch), b1 = min(L, b0 + ch);
+    uint32_t c = 0;
+    for (int64_t i = b0; i < b1; i++) c = ((c << 8) & 0xFFFFu) ^ c_crc16[((c >> 8) ^ src[i]) & 0xFF];
+    if (b1 > b0 && b1 < L) c = gf_mulmod(c, xpow8((uint64_t)(L - b1)));
+    for (int o = 32; o > 0; o >>= 1) c ^= __shfl_xor(c, o);
+    __shared__ uint32_t wc[4];
+    if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
+    __syncthreads();
+    const uint32_t crc = wc[0] ^ wc[1] ^ wc[2] ^ wc[3];
+    for (int64_t i = threadIdx.x; i < L; i += 256) arena[D + i] = src[i];
+    if (threadIdx.x == 0) {
+        arena[D + L] = (uint8_t)(crc >> 8);
+        arena[D + L + 1] = (uint8_t)crc;
+    }
+}
+
+__global__ void k_gather_tile_off(const int64_t *frame_off, const TileGeom *tiles, int ntiles, int64_t total,
+                                  int64_t *tile_off) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < ntiles) tile_off[t] = frame_off[tiles[t].frame_base];
+    if (t == ntiles) tile_off[t] = total;
+}
+
+// ------------------------------------------------------------------------------------- host side
+static bool g_tables_ready[64];
+
+static int upload_tables(frs_ctx *ctx) {
+    if (g_tables_ready[ctx->device]) return FRS_OK;
+    uint8_t t8[256];
+    uint16_t t16[256];
+    for (int i = 0; i < 256; i++) {
+        uint8_t c = (uint8_t)i;
+        for (int k = 0; k < 8; k++) c = (c & 0x80) ? (uint8_t)((c << 1) ^ 0x07) : (uint8_t)(c << 1);
+        t8[i] = c;
+        uint16_t d = (uint16_t)(i << 8);
+        for (int k = 0; k < 8; k++) d = (d & 0x8000) ? (uint16_t)((d << 1) ^ 0x8005) : (uint16_t)(d << 1);
+        t16[i] = d;
+    }
+    // x^(8*2^j) mod P by repeated squaring of x^8
+    uint16_t xp[40];
+    auto mulmod = [](uint32_t a, uint32_t b) {
+        uint32_t r = 0;
+        for (int i = 15; i >= 0; i--) {
+            r <<= 1;
+            if (r & 0x10000u) r ^= 0x18005u;
+            if ((b >> i) & 1u) r ^= a;
+        }
+        return r;
+    };
+    uint32_t v = 0x100;  // x^8
+    for (int j = 0; j < 40; j++) {
+        xp[j] = (uint16_t)v;
+        v = mulmod(v, v);
+    }
+    FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_crc8), t8, sizeof(t8), 0, hipMemcpyHostToDevice, ctx->stream));
+    FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_crc16), t16, sizeof(t16), 0, hipMemcpyHostToDevice, ctx->stream));
+    FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_xpow8), xp, sizeof(xp), 0, hipMemcpyHostToDevice, ctx->stream));
+    FRS_HIP(hipStreamSynchronize(ctx->stream));
+    g_tables_ready[ctx->device] = true;
+    return FRS_OK;
+}
+
+int dtype_size(int dt) {
+    switch (dt) {
+    case FRS_DT_U8: return 1;
+    case FRS_DT_U16:
+    case FRS_DT_I16: return 2;
+    case FRS_DT_I32:
+    case FRS_DT_U32:
+    case FRS_DT_F32: return 4;
+    case FRS_DT_F64: return 8;
+    default: return 0;
+    }
+}
+
+static int stream_bps_of(const frs_encode_desc *d) { return d->bits_per_sample == 16 ? 16 : 32; }
+
+static int qlp_precision_for(int bps, int blocksize) {
+    // stream_encoder.c init: qlp_coeff_precision == 0 (level 5) -> chosen by bps and blocksize
+    if (bps < 16) return (2 + bps / 2) > 5 ? 2 + bps / 2 : 5;
+    if (bps == 16) {
+        if (blocksize <= 192) return 7;
+        if (blocksize <= 384) return 8;
+        if (blocksize <= 576) return 9;
+        if (blocksize <= 1152) return 10;
+        if (blocksize <= 2304) return 11;
+        if (blocksize <= 4608) return 12;
+        return 13;
+    }
+    if (blocksize <= 384) return 13;
+    if (blocksize <= 1152) return 14;
+    return 15;
+}
+
+static int64_t slot_words_for(const frs_encode_desc *d) {
+    // verbatim bound of a frame + header + slack (the exact coder can exceed the estimate a little)
+    const int64_t bps = stream_bps_of(d);
+    const int64_t bits = 16 * 8 + (int64_t)d->nbands * (16 + 32 + (int64_t)d->blocksize * bps) + 64;
+    return (bits + 31) / 32 + (int64_t)d->blocksize / 8 + 64;
+}
+
+static void build_tiles(const frs_encode_desc *d, std::vector<TileGeom> &tiles, int64_t &nframes) {
+    const int64_t tcols = (d->width + d->tile_w - 1) / d->tile_w;
+    nframes = 0;
+    tiles.clear();
+    for (int64_t ti = d->tile_begin; ti < d->tile_end; ti++) {
+        TileGeom g;
+        const int64_t tr = ti / tcols, tc = ti % tcols;
+        g.r0 = tr * d->tile_h;
+        g.c0 = tc * d->tile_w;
+        g.h = (int32_t)std::min<int64_t>(d->tile_h, d->height - g.r0);
+        g.w = (int32_t)std::min<int64_t>(d->tile_w, d->width - g.c0);
+        const int64_t px = (int64_t)g.h * g.w;
+        g.nframes = (int32_t)((px + d->blocksize - 1) / d->blocksize);
+        g.frame_base = nframes;
+        g.pad = 0;
+        nframes += g.nframes;
+        tiles.push_back(g);
+    }
+}
+
+int64_t arena_bound(const frs_encode_desc *d) {
+    std::vector<TileGeom> tiles;
+    int64_t nframes;
+    build_tiles(d, tiles, nframes);
+    return nframes * (slot_words_for(d) * 4) + 64;
+}
+
+template <int DT>
+static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster_dev, void *arena_dev,
+                      int64_t arena_cap, int64_t *tile_off, double *tile_min, double *tile_max) {
+    using T = typename Elem<DT>::T;
+    std::vector<TileGeom> tiles;
+    int64_t nframes;
+    build_tiles(d, tiles, nframes);
+    const int ntiles = (int)tiles.size();
+    if (ntiles == 0) {
+        tile_off[0] = 0;
+        return FRS_OK;
+    }
+    EncodeParams P;
+    P.row_stride = d->row_stride;
+    P.band_stride = d->band_stride;
+    P.band0 = d->band0;
+    P.nch = d->nbands;
+    P.blocksize = d->blocksize;
+    P.sample_rate = d->sample_rate;
+    P.bps = stream_bps_of(d);
+    P.scale_bits = d->bits_per_sample == 16 ? 16 : 24;
+    P.qlp_precision = qlp_precision_for(P.bps, d->blocksize);
+    P.slot_words = (int32_t)slot_words_for(d);
+    P.nframes = nframes;
+    P.ntiles = ntiles;
+    P.pad = 0;
+
+    int rc = upload_tables(ctx);
+    if (rc) return rc;
+    hipStream_t st = ctx->stream;
+    FRS_HIP(ctx->tiles.ensure(sizeof(TileGeom) * ntiles));
+    FRS_HIP(ctx->norms.ensure(sizeof(TileNorm) * ntiles));
+    FRS_HIP(ctx->analysis.ensure(sizeof(SubAnalysis) * nframes * P.nch));
+    FRS_HIP(ctx->slots.ensure((size_t)nframes * P.slot_words * 4));
+    FRS_HIP(ctx->frame_bytes.ensure(sizeof(int64_t) * (nframes + 1) + 64));
+    FRS_HIP(ctx->frame_off.ensure(sizeof(int64_t) * (nframes + 1)));
+    FRS_HIP(ctx->tile_sizes.ensure(sizeof(int64_t) * (ntiles + 1) + 64));
+    if (ctx->window_bs != d->blocksize) {
+        std::vector<float> win(d->blocksize, 1.0f);
+        // FLAC__window_tukey(0.5) computed in double with the host libm cos, stored as float (window.c)
+        const float p = 0.5f;
+        const int L = d->blocksize;
+        const int Np = (int)(p / 2.0f * (float)L) - 1;
+        if (Np > 0)
+            for (int k = 0; k <= Np; k++) {
+                win[k] = (float)(0.5f - 0.5f * cos(M_PI * k / Np));
+                win[L - Np - 1 + k] = (float)(0.5f - 0.5f * cos(M_PI * (k + Np) / Np));
+            }
+        FRS_HIP(ctx->window.ensure(sizeof(float) * L));
+        FRS_HIP(hipMemcpyAsync(ctx->window.ptr, win.data(), sizeof(float) * L, hipMemcpyHostToDevice, st));
+        FRS_HIP(hipStreamSynchronize(st));
+        ctx->window_bs = d->blocksize;
+    }
+    FRS_HIP(hipMemcpyAsync(ctx->tiles.ptr, tiles.data(), sizeof(TileGeom) * ntiles, hipMemcpyHostToDevice, st));
+    int *err_flag = reinterpret_cast<int *>(ctx->frame_bytes.as<int64_t>() + nframes + 1);
+    FRS_HIP(hipMemsetAsync(err_flag, 0, sizeof(int), st));
+
+    const T *raster = reinterpret_cast<const T *>(raster_dev);
+    TileGeom *dtiles = ctx->tiles.as<TileGeom>();
+    TileNorm *dnorms = ctx->norms.as<TileNorm>();
+    SubAnalysis *dana = ctx->analysis.as<SubAnalysis>();
+
+    hipEvent_t ev;
+    // 1. tile stats
+    prof_begin(ctx, "stats", &ev);
+    k_stats_init<<<(ntiles + 255) / 256, 256, 0, st>>>(dnorms, ntiles);
+    {
+        int64_t rows = (int64_t)d->tile_h * d->nbands;
+        int splits = (int)std::min<int64_t>(rows, std::max<int64_t>(1, (int64_t)4096 / ntiles));
+        if (splits < 1) splits = 1;
+        dim3 grid(splits, ntiles);
+        k_tile_stats<DT><<<grid, 256, 0, st>>>(raster, P, dtiles, dnorms, splits);
+    }
+    k_tile_finalize<DT><<<(ntiles + 255) / 256, 256, 0, st>>>(dnorms, ntiles);
+    prof_end(ctx, "stats", ev);
+    // 2. analysis
+    const int64_t nsub = nframes * P.nch;
+    prof_begin(ctx, "analyze", &ev);
+    if (P.bps > 16) {
+        k_analyze<DT, true><<<(unsigned)((nsub + 127) / 128), 128, 0, st>>>(raster, P, dtiles, dnorms,
+                                                                             ctx->window.as<float>(), dana);
+        k_analyze_fixed_wide<DT><<<(unsigned)((nsub + 127) / 128), 128, 0, st>>>(raster, P, dtiles, dnorms, dana);
+    } else {
+        k_analyze<DT, false><<<(unsigned)((nsub + 127) / 128), 128, 0, st>>>(raster, P, dtiles, dnorms,
+                                                                              ctx->window.as<float>(), dana);
+    }
+    prof_end(ctx, "analyze", ev);
+    // 3. encode frames into slots
+    prof_begin(ctx, "encode", &ev);
+    k_encode_frames<DT><<<(unsigned)nframes, kEncThreads, 0, st>>>(raster, P, dtiles, dnorms, dana,
+                                                                   ctx->slots.as<uint32_t>(),
+                                                                   ctx->frame_bytes.as<int64_t>(), err_flag);
+    prof_end(ctx, "encode", ev);
+    // 4. offsets
+    size_t tmp_bytes = 0;
+    FRS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ctx->frame_bytes.as<int64_t>(),
+                                             ctx->frame_off.as<int64_t>(), (int)(nframes + 1), st));
+    FRS_HIP(ctx->scan_tmp.ensure(tmp_bytes));
+    // frame_bytes[nframes] must be 0 for the total
+    FRS_HIP(hipMemsetAsync(ctx->frame_bytes.as<int64_t>() + nframes, 0, sizeof(int64_t), st));
+    FRS_HIP(hipcub::DeviceScan::ExclusiveSum(ctx->scan_tmp.ptr, tmp_bytes, ctx->frame_bytes.as<int64_t>(),
+                                             ctx->frame_off.as<int64_t>(), (int)(nframes + 1), st));
+    int64_t total = 0;
+    int errv = 0;
+    FRS_HIP(hipMemcpyAsync(&total, ctx->frame_off.as<int64_t>() + nframes, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    FRS_HIP(hipMemcpyAsync(&errv, err_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    FRS_HIP(hipStreamSynchronize(st));
+    if (errv) {
+        ctx->err = "frame exceeded its slot (pathological residuals), flag " + std::to_string(errv);
+        return FRS_E_UNSUPPORTED;
+    }
+    if (total > arena_cap) {
+        tile_off[ntiles] = total;
+        ctx->err = "arena too small";
+        return FRS_E_NOSPACE;
+    }
+    // 5. compact + CRC
+    prof_begin(ctx, "compact", &ev);
+    k_compact<<<(unsigned)nframes, 256, 0, st>>>(ctx->slots.as<uint32_t>(), P.slot_words, ctx->frame_bytes.as<int64_t>(),
+                                                 ctx->frame_off.as<int64_t>(), nframes,
+                                                 reinterpret_cast<uint8_t *>(arena_dev));
+    prof_end(ctx, "compact", ev);
+    k_gather_tile_off<<<(ntiles + 1 + 255) / 256, 256, 0, st>>>(ctx->frame_off.as<int64_t>(), dtiles, ntiles, total,
+                                                               ctx->tile_sizes.as<int64_t>());
+    std::vector<TileNorm> hn(ntiles);
+    FRS_HIP(hipMemcpyAsync(tile_off, ctx->tile_sizes.ptr, sizeof(int64_t) * (ntiles + 1), hipMemcpyDeviceToHost, st));
+    FRS_HIP(hipMemcpyAsync(hn.data(), dnorms, sizeof(TileNorm) * ntiles, hipMemcpyDeviceToHost, st));
+    FRS_HIP(hipStreamSynchronize(st));
+    prof_collect(ctx);
+    for (int t = 0; t < ntiles; t++) {
+        tile_min[t] = hn[t].dmin;
+        tile_max[t] = hn[t].dmax;
+    }
+    return FRS_OK;
+}
+
+int encode_job(frs_ctx *ctx, const frs_encode_desc *d, const void *raster_dev, void *arena_dev, int64_t arena_cap,
+               int64_t *tile_off, double *tile_min, double *tile_max, int32_t *stream_bps) {
+    if (stream_bps) *stream_bps = stream_bps_of(d);
+    switch (d->dtype) {
+    case FRS_DT_U8: return run_encode<FRS_DT_U8>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
+    case FRS_DT_U16: return run_encode<FRS_DT_U16>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
+    case FRS_DT_I16: return run_encode<FRS_DT_I16>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
+    case FRS_DT_I32: return run_encode<FRS_DT_I32>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
+    case FRS_DT_U32: return run_encode<FRS_DT_U32>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
+    case FRS_DT_F32: return run_encode<FRS_DT_F32>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
+    case FRS_DT_F64: return run_encode<FRS_DT_F64>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
+    default: ctx->err = "bad dtype"; return FRS_E_ARG;
+    }
+}
+
+}  // namespace frs

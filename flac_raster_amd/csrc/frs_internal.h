@@ -1,0 +1,86 @@
+// frs_internal.h -- host-side context, device buffers and launcher entry points.
+#pragma once
+#include <stdint.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#include "../../include/flac_raster_amd.h"
+#include "frs_common.h"
+
+// Grow-only device buffer owned by a context.
+struct DevBuf {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t need) {
+        if (need <= bytes) return hipSuccess;
+        if (ptr) hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+        size_t want = need + need / 8 + 4096;
+        hipError_t e = hipMalloc(&ptr, want);
+        if (e == hipSuccess) bytes = want;
+        return e;
+    }
+    void release() {
+        if (ptr) hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+    template <typename T> T *as() const { return reinterpret_cast<T *>(ptr); }
+};
+
+struct ProfEntry {
+    double total_ms = 0.0;
+    int count = 0;
+};
+
+struct frs_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // encode scratch
+    DevBuf tiles, norms, analysis, slots, frame_bytes, frame_off, scan_tmp, window, tile_sizes;
+    // host staging (pinned)
+    DevBuf raster_stage, arena_stage;  // device copies for the host-pointer entry points
+    // decode scratch
+    DevBuf dec_cand, dec_count, dec_blob, dec_pcm, dec_soff, dec_poff;
+    // profiling
+    bool prof = false;
+    std::map<std::string, ProfEntry> prof_tab;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> ev_pending;
+    // cached window (blocksize)
+    int window_bs = 0;
+};
+
+#define FRS_HIP(call)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (call);                                                        \
+        if (e_ != hipSuccess) {                                                        \
+            ctx->err = std::string(#call) + ": " + hipGetErrorString(e_);              \
+            return FRS_E_HIP;                                                          \
+        }                                                                              \
+    } while (0)
+
+namespace frs {
+// Kernel timing helpers (no-ops unless ctx->prof).
+void prof_begin(frs_ctx *ctx, const char *name, hipEvent_t *start);
+void prof_end(frs_ctx *ctx, const char *name, hipEvent_t start);
+void prof_collect(frs_ctx *ctx);
+
+int encode_job(frs_ctx *ctx, const frs_encode_desc *d, const void *raster_dev, void *arena_dev, int64_t arena_cap,
+               int64_t *tile_off, double *tile_min, double *tile_max, int32_t *stream_bps);
+int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const int64_t *stream_off,
+               int32_t nstreams, int32_t channels, int32_t bps, int32_t blocksize, int32_t *pcm_dev,
+               const int64_t *pcm_off);
+int denormalize_job(frs_ctx *ctx, const int32_t *pcm_dev, int64_t n, double dmin, double dmax, int32_t out_dtype,
+                    void *out_dev);
+int64_t arena_bound(const frs_encode_desc *d);
+int synth_job(frs_ctx *ctx, int16_t *dev, int bands, int64_t height, int64_t width, int64_t row0, int64_t full_height,
+              uint64_t seed);
+int dtype_size(int dt);
+}  // namespace frs

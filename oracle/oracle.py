@@ -1,0 +1,149 @@
+"""oracle.oracle -- TEST INFRASTRUCTURE ONLY: ctypes bindings to the CPU oracle (flac_oracle.c).
+
+The oracle restates the reference's hot path on the CPU (see flac_oracle.c header for the
+reference file:line each function follows).  Only tests/, __graft_entry__.smoke() and bench.py's
+``cpu_baseline`` leg may import this module; the product (flac_raster_amd) never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+_LIB_PATH = _HERE / "liborc_flac.so"
+_lib = None
+
+# dtype codes (shared numbering with include/flac_raster_amd.h FRS_DT_*)
+DTYPES = {np.dtype(np.uint8): 1, np.dtype(np.uint16): 2, np.dtype(np.int16): 3,
+          np.dtype(np.int32): 4, np.dtype(np.uint32): 5, np.dtype(np.float32): 6,
+          np.dtype(np.float64): 7}
+
+
+def build(force: bool = False) -> Path:
+    """Compile flac_oracle.c into liborc_flac.so with the committed Makefile."""
+    if force or not _LIB_PATH.exists() or _LIB_PATH.stat().st_mtime < (_HERE / "flac_oracle.c").stat().st_mtime:
+        subprocess.run(["make", "-C", str(_HERE), "-s"], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(str(_LIB_PATH))
+        i64, i32, vp, dp = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)
+        L.orc_encode_frames.restype = i64
+        L.orc_encode_frames.argtypes = [vp, i64, i32, i32, i32, i32, vp, i64]
+        L.orc_stream_header.restype = i64
+        L.orc_stream_header.argtypes = [i32, i32, i32, i32, vp, i64]
+        L.orc_normalize.restype = i32
+        L.orc_normalize.argtypes = [vp, i32, i64, i32, dp, dp, vp]
+        L.orc_denormalize_i16.restype = None
+        L.orc_denormalize_i16.argtypes = [vp, i64, ctypes.c_double, ctypes.c_double, i32, vp]
+        L.orc_decode_frames.restype = i64
+        L.orc_decode_frames.argtypes = [vp, i64, i32, i32, vp, i64]
+        L.orc_encode_tiles.restype = i64
+        L.orc_encode_tiles.argtypes = [vp, i32, i64, i64, i64, i32, i32, i32, vp, i64, vp, vp, vp, i32]
+        L.orc_window_tukey.restype = None
+        L.orc_window_tukey.argtypes = [vp, i32, ctypes.c_float]
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def bits_per_sample_for(dtype) -> int:
+    """converter.py:25-37 (_calculate_audio_params, bit depth part)."""
+    dt = np.dtype(dtype)
+    if dt in (np.uint8, np.uint16, np.int16):
+        return 16
+    return 24
+
+
+def sample_rate_for(shape0: int, shape1: int) -> int:
+    """converter.py:39-51 -- total_pixels = shape[0]*shape[1] of the (bands, h, w) array."""
+    total = shape0 * shape1
+    if total < 1000000:
+        return 44100
+    if total < 10000000:
+        return 48000
+    if total < 100000000:
+        return 96000
+    return 192000
+
+
+def normalize(arr: np.ndarray):
+    """converter.py:56-86 -> (pcm int32 array same shape, data_min, data_max, stream_bps)."""
+    a = np.ascontiguousarray(arr)
+    out = np.empty(a.shape, dtype=np.int32)
+    mn, mx = ctypes.c_double(), ctypes.c_double()
+    bps = lib().orc_normalize(_ptr(a), DTYPES[a.dtype], a.size, bits_per_sample_for(a.dtype),
+                              ctypes.byref(mn), ctypes.byref(mx), _ptr(out))
+    return out, mn.value, mx.value, bps
+
+
+def encode_frames(pcm: np.ndarray, bps: int, sample_rate: int, blocksize: int = 4096) -> bytes:
+    """libFLAC level-5 frames for interleaved pcm [N, C] (int32)."""
+    x = np.ascontiguousarray(pcm, dtype=np.int32)
+    if x.ndim == 1:
+        x = x[:, None]
+    n, c = x.shape
+    cap = n * c * (bps // 8 + 1) + (n // blocksize + 2) * (32 + 16 * c) + 1024
+    out = np.empty(cap, dtype=np.uint8)
+    r = lib().orc_encode_frames(_ptr(x), n, c, bps, sample_rate, blocksize, _ptr(out), cap)
+    if r < 0:
+        raise RuntimeError(f"oracle encode overflow {r}")
+    return out[:r].tobytes()
+
+
+def stream_header(channels: int, bps: int, sample_rate: int, blocksize: int = 4096) -> bytes:
+    out = np.empty(128, dtype=np.uint8)
+    r = lib().orc_stream_header(channels, bps, sample_rate, blocksize, _ptr(out), 128)
+    return out[:r].tobytes()
+
+
+def decode_frames(data: bytes, channels: int, bps: int, max_samples: int) -> np.ndarray:
+    buf = np.frombuffer(data, dtype=np.uint8)
+    out = np.empty((max_samples, channels), dtype=np.int32)
+    r = lib().orc_decode_frames(_ptr(buf), len(buf), channels, bps, _ptr(out), max_samples)
+    if r < 0:
+        raise RuntimeError(f"oracle decode error {r}")
+    return out[:r]
+
+
+def denormalize_i16(pcm: np.ndarray, dmin: float, dmax: float, dtype) -> np.ndarray:
+    """converter.py:88-110 after pyflac+soundfile's pcm/32768 scaling (sonos-pyflac.txt:1629)."""
+    p = np.ascontiguousarray(pcm, dtype=np.int32)
+    out = np.empty(p.shape, dtype=dtype)
+    lib().orc_denormalize_i16(_ptr(p), p.size, dmin, dmax, DTYPES[np.dtype(dtype)], _ptr(out))
+    return out
+
+
+def window_tukey(L: int, p: float = 0.5) -> np.ndarray:
+    w = np.empty(L, dtype=np.float32)
+    lib().orc_window_tukey(_ptr(w), L, p)
+    return w
+
+
+def encode_tiles(band: np.ndarray, tile: int, sample_rate: int = 44100, blocksize: int = 4096, threads: int = 1):
+    """Band-1 streaming tiles (cli.py:690-763): returns (arena bytes, tile_off, mins, maxs)."""
+    b = np.ascontiguousarray(band)
+    H, W = b.shape
+    nt = ((H + tile - 1) // tile) * ((W + tile - 1) // tile)
+    esz = b.dtype.itemsize
+    cap = H * W * (4 if esz <= 2 else 5) + nt * 4096 + 4096
+    arena = np.empty(cap, dtype=np.uint8)
+    off = np.zeros(nt + 1, dtype=np.int64)
+    mins = np.zeros(nt, dtype=np.float64)
+    maxs = np.zeros(nt, dtype=np.float64)
+    r = lib().orc_encode_tiles(_ptr(b), DTYPES[b.dtype], H, W, W, tile, sample_rate, blocksize,
+                               _ptr(arena), cap, _ptr(off), _ptr(mins), _ptr(maxs), threads)
+    if r < 0:
+        raise RuntimeError(f"oracle encode_tiles failed {r}")
+    return arena[:r], off, mins, maxs
