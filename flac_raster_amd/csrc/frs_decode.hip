@@ -211,7 +211,7 @@ struct BitReader {
                 const int z = __builtin_clzll(cache);
                 if (z < avail) {
                     q += z;
-                    cache <<= (z + 1);
+                    cache = (z + 1 >= 64) ? 0 : (cache << (z + 1));  // a 64-bit shift by 64 is a no-op on gfx950
                     avail -= z + 1;
                     pos_bits += z + 1;
                     return q;
