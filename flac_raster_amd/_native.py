@@ -55,6 +55,7 @@ class EncodeDesc(ctypes.Structure):
         ("tile_h", ctypes.c_int32), ("tile_w", ctypes.c_int32),
         ("blocksize", ctypes.c_int32), ("sample_rate", ctypes.c_int32),
         ("bits_per_sample", ctypes.c_int32), ("compression_level", ctypes.c_int32),
+        ("norm_mode", ctypes.c_int32),
         ("tile_begin", ctypes.c_int64), ("tile_end", ctypes.c_int64),
     ]
 
@@ -100,7 +101,7 @@ def load_library(path: Optional[os.PathLike] = None):
         L.frs_decode_frames_device.argtypes = dec_args
         L.frs_decode_frames.restype = i32
         L.frs_decode_frames.argtypes = dec_args
-        den_args = [ctxp, vp, i64, ctypes.c_double, ctypes.c_double, i32, vp]
+        den_args = [ctxp, vp, i64, i32, ctypes.c_double, ctypes.c_double, i32, vp]
         L.frs_denormalize_device.restype = i32
         L.frs_denormalize_device.argtypes = den_args
         L.frs_denormalize.restype = i32
@@ -224,7 +225,7 @@ class Context:
     @staticmethod
     def make_desc(height, width, dtype, *, row_stride=None, band_stride=None, band0=0, nbands=1,
                   tile_h=512, tile_w=512, sample_rate=44100, bits_per_sample=16, blocksize=4096,
-                  compression_level=5, tile_begin=0, tile_end=None) -> EncodeDesc:
+                  compression_level=5, tile_begin=0, tile_end=None, norm_mode=0) -> EncodeDesc:
         d = EncodeDesc()
         d.height, d.width = int(height), int(width)
         d.row_stride = int(row_stride if row_stride is not None else width)
@@ -234,6 +235,7 @@ class Context:
         d.tile_h, d.tile_w = int(tile_h), int(tile_w)
         d.blocksize, d.sample_rate = int(blocksize), int(sample_rate)
         d.bits_per_sample, d.compression_level = int(bits_per_sample), int(compression_level)
+        d.norm_mode = int(norm_mode)
         ntiles = ((d.height + d.tile_h - 1) // d.tile_h) * ((d.width + d.tile_w - 1) // d.tile_w)
         d.tile_begin = int(tile_begin)
         d.tile_end = int(ntiles if tile_end is None else tile_end)
@@ -297,16 +299,17 @@ class Context:
             poff.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
         return poff
 
-    def denormalize_host(self, pcm: np.ndarray, data_min: float, data_max: float, dtype) -> np.ndarray:
+    def denormalize_host(self, pcm: np.ndarray, data_min: float, data_max: float, dtype, pcm_bps: int = 16) -> np.ndarray:
         p = np.ascontiguousarray(pcm, dtype=np.int32)
         out = np.empty(p.shape, dtype=dtype)
-        self._check(self.lib.frs_denormalize(self.handle, _p(p), p.size, float(data_min), float(data_max),
+        self._check(self.lib.frs_denormalize(self.handle, _p(p), p.size, int(pcm_bps), float(data_min), float(data_max),
                                              DTYPE_CODES[np.dtype(dtype)], _p(out)))
         return out
 
-    def denormalize_device(self, pcm_ptr: int, n: int, data_min: float, data_max: float, dtype, out_ptr: int):
-        self._check(self.lib.frs_denormalize_device(self.handle, ctypes.c_void_p(pcm_ptr), int(n), float(data_min),
-                                                    float(data_max), DTYPE_CODES[np.dtype(dtype)],
+    def denormalize_device(self, pcm_ptr: int, n: int, data_min: float, data_max: float, dtype, out_ptr: int,
+                           pcm_bps: int = 16):
+        self._check(self.lib.frs_denormalize_device(self.handle, ctypes.c_void_p(pcm_ptr), int(n), int(pcm_bps),
+                                                    float(data_min), float(data_max), DTYPE_CODES[np.dtype(dtype)],
                                                     ctypes.c_void_p(out_ptr)))
 
     # ---- bench helpers

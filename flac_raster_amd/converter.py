@@ -1,0 +1,182 @@
+"""RasterFLACConverter -- drop-in for reference src/flac_raster/converter.py:18-437 on the MI355X codec.
+
+Same class, method names, arguments and output bytes.  Sample arithmetic (normalisation, FLAC frame
+coding, decoding, de-normalisation) runs in libflac_raster_amd.so; this module does file I/O and the
+metadata/container bytes.  Metadata embedding follows the reference's pinned environment (mutagen
+1.47.0 present, pixi.lock:77): tags + padding inside the FLAC file.  ``embed_metadata=False``
+reproduces the mutagen-missing fallback (bare libFLAC header + ``<flac>.json`` sidecar) that produced
+test_data/sample_rgb.flac and sample_rgb.json.
+"""
+from __future__ import annotations
+
+import json
+import logging
+from pathlib import Path
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+
+from . import container, geotiff
+from ._native import Context, default_context
+
+log = logging.getLogger("flac_raster.converter")
+
+FLOAT_DTYPES = (np.dtype(np.float32), np.dtype(np.float64))
+
+
+def audio_params(shape0: int, shape1: int, dtype) -> Tuple[int, int]:
+    """converter.py:25-54: (sample_rate, bits_per_sample).  total_pixels = shape[0]*shape[1] of the
+    (bands, h, w) array, i.e. bands*h."""
+    dt = np.dtype(dtype)
+    if dt in (np.uint8, np.uint16, np.int16):
+        bps = 16
+    else:
+        bps = 24
+    total = shape0 * shape1
+    if total < 1000000:
+        sr = 44100
+    elif total < 10000000:
+        sr = 48000
+    elif total < 100000000:
+        sr = 96000
+    else:
+        sr = 192000
+    return sr, bps
+
+
+def raster_metadata(r: geotiff.GeoRaster, data_min: float, data_max: float) -> Dict:
+    """converter.py:157-174 (key order matters for the JSON sidecar)."""
+    t = r.transform or geotiff.Affine(1.0, 0.0, 0.0, 0.0, 1.0, 0.0)
+    left, bottom, right, top = geotiff.GeoRaster(r.data[:1], t).bounds
+    return {
+        "width": r.width,
+        "height": r.height,
+        "count": r.count,
+        "dtype": str(r.dtype),
+        "crs": r.crs_string,
+        "transform": list(t),
+        "bounds": {"left": left, "bottom": bottom, "right": right, "top": top},
+        "data_min": data_min,
+        "data_max": data_max,
+        "nodata": r.nodata,
+        "driver": "GTiff",
+    }
+
+
+class RasterFLACConverter:
+    """Handles conversion between TIFF and FLAC formats for raster data (converter.py:18)."""
+
+    def __init__(self, ctx: Optional[Context] = None, embed_metadata: bool = True):
+        self.metadata_key = "RASTER_METADATA"
+        self.logger = log
+        self._ctx = ctx
+        self.embed_metadata = embed_metadata
+
+    @property
+    def ctx(self) -> Context:
+        if self._ctx is None:
+            self._ctx = default_context()
+        return self._ctx
+
+    # ------------------------------------------------------------------ reference helpers
+    def _calculate_audio_params(self, raster_data: np.ndarray, dtype) -> Tuple[int, int]:
+        return audio_params(raster_data.shape[0], raster_data.shape[1], dtype)
+
+    # ------------------------------------------------------------------ encode
+    def encode_array(self, data: np.ndarray) -> Tuple[bytes, float, float, int, int]:
+        """Encode a (bands, h, w) raster as one interleaved-channel FLAC stream's frames.
+        Returns (frames, data_min, data_max, stream_bps, sample_rate)."""
+        if data.ndim == 2:
+            data = data[None]
+        B, H, W = data.shape
+        if B > 8:
+            raise ValueError("FLAC supports at most 8 channels (bands)")
+        sr, bps = audio_params(B, H, data.dtype)
+        d = self.ctx.make_desc(H, W, data.dtype, nbands=B, tile_h=H, tile_w=W, sample_rate=sr, bits_per_sample=bps)
+        arena, off, mn, mx, sbps = self.ctx.encode_tiles_host(np.ascontiguousarray(data), d)
+        return arena.tobytes(), float(mn[0]), float(mx[0]), sbps, sr
+
+    def tiff_to_flac(self, tiff_path: Path, flac_path: Path, compression_level: int = 5,
+                     spatial_tiling: bool = False, tile_size: int = 512):
+        """converter.py:112-232."""
+        if compression_level != 5:
+            raise NotImplementedError("only compression level 5 (the reference's default and create-streaming's) "
+                                      "is implemented on the GPU encoder")
+        tiff_path, flac_path = Path(tiff_path), Path(flac_path)
+        if spatial_tiling:
+            from .spatial_encoder import SpatialFLACEncoder
+            return SpatialFLACEncoder(tile_size=tile_size, ctx=self.ctx).encode_spatial_flac(
+                tiff_path, flac_path, compression_level)
+        r = geotiff.read(tiff_path)
+        frames, dmin, dmax, sbps, sr = self.encode_array(r.data)
+        meta = raster_metadata(r, dmin, dmax)
+        self.write_flac(flac_path, frames, meta, r.count, sbps, sr)
+        return None
+
+    def write_flac(self, flac_path: Path, frames: bytes, meta: Dict, channels: int, sbps: int, sr: int) -> None:
+        if self.embed_metadata:
+            hdr = container.mutagen_header(channels, sbps, sr, container.raster_tags(meta), len(frames))
+            Path(flac_path).write_bytes(hdr + frames)
+        else:
+            Path(flac_path).write_bytes(container.bare_header(channels, sbps, sr) + frames)
+            Path(flac_path).with_suffix(".json").write_text(json.dumps(meta, indent=2))
+
+    # ------------------------------------------------------------------ decode
+    def _read_embedded_metadata(self, flac_path: Path, meta: Optional[container.StreamMeta] = None) -> Optional[Dict]:
+        """converter.py:375-427: embedded GEOSPATIAL_* tags, else the JSON sidecar."""
+        flac_path = Path(flac_path)
+        try:
+            if meta is None:
+                meta = container.parse_metadata(flac_path.read_bytes())
+            m = container.read_raster_tags(meta)
+            if m is not None:
+                return m
+        except (ValueError, OSError) as e:
+            self.logger.warning(f"Failed to read embedded metadata: {e}")
+        side = flac_path.with_suffix(".json")
+        if side.exists():
+            return json.loads(side.read_text())
+        return None
+
+    def decode_bytes(self, buf: bytes, metadata: Optional[Dict] = None) -> Tuple[np.ndarray, Dict]:
+        """Decode one FLAC stream (bytes) to a (count, h, w) raster of the original dtype."""
+        sm = container.parse_metadata(buf)
+        md = metadata if metadata is not None else container.read_raster_tags(sm)
+        if md is None:
+            raise ValueError("No metadata found in FLAC file or sidecar file")
+        return self._decode_with_meta(buf, sm, md), md
+
+    def _decode_with_meta(self, buf: bytes, sm: container.StreamMeta, md: Dict) -> np.ndarray:
+        W, H, count = int(md["width"]), int(md["height"]), int(md["count"])
+        if sm.bps not in (16, 32):
+            raise ValueError("Only int16/int32 data type is supported")  # pyflac decoder.py check
+        frames = np.frombuffer(buf, dtype=np.uint8)[sm.audio_offset:]
+        pcm = self.ctx.decode_frames_host(frames, [0, len(frames)], [W * H], channels=sm.channels, bps=sm.bps,
+                                          blocksize=sm.blocksize)
+        dtype = np.dtype(md["dtype"])
+        out = self.ctx.denormalize_host(pcm, md["data_min"], md["data_max"], dtype, pcm_bps=sm.bps)
+        if count > 1:
+            return np.ascontiguousarray(out.reshape(H, W, count).transpose(2, 0, 1))
+        return out.reshape(1, H, W)
+
+    def flac_to_tiff(self, flac_path: Path, tiff_path: Path):
+        """converter.py:234-313."""
+        flac_path, tiff_path = Path(flac_path), Path(tiff_path)
+        buf = flac_path.read_bytes()
+        sm = container.parse_metadata(buf)
+        md = self._read_embedded_metadata(flac_path, sm)
+        if not md:
+            raise ValueError("No metadata found in FLAC file or sidecar file")
+        raster = self._decode_with_meta(buf, sm, md)
+        write_tiff_from_meta(tiff_path, raster, md)
+
+
+def write_tiff_from_meta(tiff_path: Path, raster: np.ndarray, md: Dict) -> None:
+    """converter.py:284-309: GTiff with the metadata's CRS, transform and nodata."""
+    t = md.get("transform")
+    transform = geotiff.Affine(*t[:6]) if t else None
+    epsg = None
+    crs = md.get("crs")
+    if crs and str(crs).upper().startswith("EPSG:"):
+        epsg = int(str(crs).split(":")[1])
+    geotiff.write(tiff_path, raster, transform=transform, epsg=epsg, nodata=md.get("nodata"))

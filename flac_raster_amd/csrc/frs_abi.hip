@@ -60,6 +60,12 @@ static int check_desc(frs_ctx *ctx, const frs_encode_desc *d) {
     if (d->compression_level != 5) { ctx->err = "only compression level 5 is implemented"; return FRS_E_UNSUPPORTED; }
     if (d->bits_per_sample != 16 && d->bits_per_sample != 24) { ctx->err = "bits_per_sample must be 16 or 24"; return FRS_E_ARG; }
     if (d->sample_rate <= 0 || d->sample_rate > 655350) { ctx->err = "bad sample rate"; return FRS_E_ARG; }
+    if (d->norm_mode != 0 && d->norm_mode != 1) { ctx->err = "bad norm_mode"; return FRS_E_ARG; }
+    if (d->norm_mode == 1 && !(d->dtype == FRS_DT_U8 || d->dtype == FRS_DT_U16 || d->dtype == FRS_DT_I16 ||
+                               d->dtype == FRS_DT_I32 || d->dtype == FRS_DT_F32)) {
+        ctx->err = "spatial (raw-frames) normalisation gives a 64-bit sample array for this dtype; pyflac rejects it";
+        return FRS_E_UNSUPPORTED;
+    }
     const int64_t tiles = ((d->height + d->tile_h - 1) / d->tile_h) * ((d->width + d->tile_w - 1) / d->tile_w);
     if (d->tile_begin < 0 || d->tile_end > tiles || d->tile_begin > d->tile_end) { ctx->err = "bad tile range"; return FRS_E_ARG; }
     if (d->nbands > 1 && d->band_stride < d->row_stride * d->height) { ctx->err = "band_stride too small"; return FRS_E_ARG; }
@@ -207,16 +213,16 @@ int frs_decode_frames(frs_ctx *ctx, const uint8_t *blob_host, const int64_t *str
     return FRS_OK;
 }
 
-int frs_denormalize_device(frs_ctx *ctx, const int32_t *pcm_dev, int64_t n, double data_min, double data_max,
-                           int32_t out_dtype, void *out_dev) {
+int frs_denormalize_device(frs_ctx *ctx, const int32_t *pcm_dev, int64_t n, int32_t pcm_bps, double data_min,
+                           double data_max, int32_t out_dtype, void *out_dev) {
     if (!ctx) return FRS_E_ARG;
     if (!pcm_dev || !out_dev || n < 0) { ctx->err = "bad denormalize arguments"; return FRS_E_ARG; }
     FRS_HIP(hipSetDevice(ctx->device));
-    return frs::denormalize_job(ctx, pcm_dev, n, data_min, data_max, out_dtype, out_dev);
+    return frs::denormalize_job(ctx, pcm_dev, n, pcm_bps, data_min, data_max, out_dtype, out_dev);
 }
 
-int frs_denormalize(frs_ctx *ctx, const int32_t *pcm_host, int64_t n, double data_min, double data_max,
-                    int32_t out_dtype, void *out_host) {
+int frs_denormalize(frs_ctx *ctx, const int32_t *pcm_host, int64_t n, int32_t pcm_bps, double data_min,
+                    double data_max, int32_t out_dtype, void *out_host) {
     if (!ctx) return FRS_E_ARG;
     const int es = frs::dtype_size(out_dtype);
     if (!pcm_host || !out_host || n < 0 || es == 0) { ctx->err = "bad denormalize arguments"; return FRS_E_ARG; }
@@ -224,7 +230,8 @@ int frs_denormalize(frs_ctx *ctx, const int32_t *pcm_host, int64_t n, double dat
     FRS_HIP(ctx->dec_pcm.ensure((size_t)n * 4 + 16));
     FRS_HIP(ctx->raster_stage.ensure((size_t)n * es + 16));
     FRS_HIP(hipMemcpyAsync(ctx->dec_pcm.ptr, pcm_host, (size_t)n * 4, hipMemcpyHostToDevice, ctx->stream));
-    int rc = frs::denormalize_job(ctx, ctx->dec_pcm.as<int32_t>(), n, data_min, data_max, out_dtype, ctx->raster_stage.ptr);
+    int rc = frs::denormalize_job(ctx, ctx->dec_pcm.as<int32_t>(), n, pcm_bps, data_min, data_max, out_dtype,
+                                  ctx->raster_stage.ptr);
     if (rc) return rc;
     FRS_HIP(hipMemcpyAsync(out_host, ctx->raster_stage.ptr, (size_t)n * es, hipMemcpyDeviceToHost, ctx->stream));
     FRS_HIP(hipStreamSynchronize(ctx->stream));

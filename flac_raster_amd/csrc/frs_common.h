@@ -60,7 +60,7 @@ struct EncodeParams {
     int32_t slot_words;   // capacity of one frame slot in 32-bit words
     int64_t nframes;
     int32_t ntiles;
-    int32_t pad;
+    int32_t norm_mode;    // 0 converter.py:56-86, 1 spatial_encoder.py:229-248
 };
 
 __host__ __device__ inline int ilog2_u32(uint32_t v) { return 31 - __builtin_clz(v); }

@@ -343,12 +343,13 @@ __global__ void __launch_bounds__(64) k_decode_frames(const uint8_t *blob, const
     atomicAdd(nvalid, 1);
 }
 
-// converter.py:88-110 (fp32, round half to even) after soundfile's pcm/32768 scaling.
+// converter.py:88-110 (fp32, round half to even) after the pyflac/soundfile WAV round trip.
 template <typename O>
-__global__ void k_denormalize(const int32_t *pcm, int64_t n, float rng, float fmn, int is_float, O *out) {
+__global__ void k_denormalize(const int32_t *pcm, int64_t n, int shift, float rng, float fmn, int is_float, O *out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const float v = (float)((double)pcm[i] / 32768.0);
+    const int32_t p16 = pcm[i] >> shift;  // 32-bit streams: libsndfile int -> short keeps the high half
+    const float v = (float)((double)p16 / 32768.0);
     if (is_float) {
         out[i] = (O)v;
         return;
@@ -445,20 +446,22 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     return FRS_OK;
 }
 
-int denormalize_job(frs_ctx *ctx, const int32_t *pcm_dev, int64_t n, double dmin, double dmax, int32_t out_dtype,
-                    void *out_dev) {
+int denormalize_job(frs_ctx *ctx, const int32_t *pcm_dev, int64_t n, int pcm_bps, double dmin, double dmax,
+                    int32_t out_dtype, void *out_dev) {
     hipStream_t st = ctx->stream;
+    // python-float arithmetic first (data_max - data_min in double), then NEP 50 casts to float32
     const float rng = (float)(dmax - dmin), fmn = (float)dmin;
+    const int sh = pcm_bps > 16 ? 16 : 0;
     const unsigned grid = (unsigned)((n + 255) / 256);
     if (n == 0) return FRS_OK;
     switch (out_dtype) {
-    case FRS_DT_U8: k_denormalize<uint8_t><<<grid, 256, 0, st>>>(pcm_dev, n, rng, fmn, 0, (uint8_t *)out_dev); break;
-    case FRS_DT_U16: k_denormalize<uint16_t><<<grid, 256, 0, st>>>(pcm_dev, n, rng, fmn, 0, (uint16_t *)out_dev); break;
-    case FRS_DT_I16: k_denormalize<int16_t><<<grid, 256, 0, st>>>(pcm_dev, n, rng, fmn, 0, (int16_t *)out_dev); break;
-    case FRS_DT_I32: k_denormalize<int32_t><<<grid, 256, 0, st>>>(pcm_dev, n, rng, fmn, 0, (int32_t *)out_dev); break;
-    case FRS_DT_U32: k_denormalize<uint32_t><<<grid, 256, 0, st>>>(pcm_dev, n, rng, fmn, 0, (uint32_t *)out_dev); break;
-    case FRS_DT_F32: k_denormalize<float><<<grid, 256, 0, st>>>(pcm_dev, n, rng, fmn, 1, (float *)out_dev); break;
-    case FRS_DT_F64: k_denormalize<double><<<grid, 256, 0, st>>>(pcm_dev, n, rng, fmn, 1, (double *)out_dev); break;
+    case FRS_DT_U8: k_denormalize<uint8_t><<<grid, 256, 0, st>>>(pcm_dev, n, sh, rng, fmn, 0, (uint8_t *)out_dev); break;
+    case FRS_DT_U16: k_denormalize<uint16_t><<<grid, 256, 0, st>>>(pcm_dev, n, sh, rng, fmn, 0, (uint16_t *)out_dev); break;
+    case FRS_DT_I16: k_denormalize<int16_t><<<grid, 256, 0, st>>>(pcm_dev, n, sh, rng, fmn, 0, (int16_t *)out_dev); break;
+    case FRS_DT_I32: k_denormalize<int32_t><<<grid, 256, 0, st>>>(pcm_dev, n, sh, rng, fmn, 0, (int32_t *)out_dev); break;
+    case FRS_DT_U32: k_denormalize<uint32_t><<<grid, 256, 0, st>>>(pcm_dev, n, sh, rng, fmn, 0, (uint32_t *)out_dev); break;
+    case FRS_DT_F32: k_denormalize<float><<<grid, 256, 0, st>>>(pcm_dev, n, sh, rng, fmn, 1, (float *)out_dev); break;
+    case FRS_DT_F64: k_denormalize<double><<<grid, 256, 0, st>>>(pcm_dev, n, sh, rng, fmn, 1, (double *)out_dev); break;
     default: ctx->err = "bad dtype"; return FRS_E_ARG;
     }
     FRS_HIP(hipGetLastError());

@@ -48,6 +48,16 @@ template <int DT> __device__ inline int64_t elem_key(typename Elem<DT>::T v) {
 
 // converter.py:56-86 for one element.  numpy 2 (NEP 50): x - min and max - min are evaluated in the
 // raster dtype (wrapping), promoted to float64 by 2.0*(...); the cast to int16/int32 truncates.
+// spatial_encoder.py:229-248 then pyflac's astype(int32): float32 arithmetic, truncation to int32.
+template <int DT> __device__ inline int32_t spatial_norm(typename Elem<DT>::T x) {
+    if constexpr (DT == FRS_DT_U8) return cast_f64_i32_x86((double)__fdiv_rn(__fsub_rn((float)x, 127.5f), 127.5f));
+    else if constexpr (DT == FRS_DT_U16) return cast_f64_i32_x86((double)__fdiv_rn(__fsub_rn((float)x, 32767.5f), 32767.5f));
+    else if constexpr (DT == FRS_DT_I16) return cast_f64_i32_x86((double)__fdiv_rn((float)x, 32767.0f));
+    else if constexpr (DT == FRS_DT_I32) return cast_f64_i32_x86((double)__fdiv_rn((float)x, 2147483647.0f));
+    else if constexpr (DT == FRS_DT_F32) return cast_f64_i32_x86((double)fminf(fmaxf(x, -1.0f), 1.0f));
+    else return 0;  // other dtypes are rejected by the host (pyflac would see a 64-bit itemsize)
+}
+
 template <int DT> struct Normalizer {
     using T = typename Elem<DT>::T;
     T mn;
@@ -55,7 +65,9 @@ template <int DT> struct Normalizer {
     double scale;
     int has_range;
     int bps16;
+    int spatial;
     __device__ inline int32_t operator()(T x) const {
+        if (spatial) return spatial_norm<DT>(x);
         if constexpr (DT == FRS_DT_F32) {
             float v = x * 8388607.0f;  // float data used as-is, float32 product (converter.py:61-64, 81)
             return cast_f64_i32_x86((double)v);
@@ -72,8 +84,9 @@ template <int DT> struct Normalizer {
     }
 };
 
-template <int DT> __device__ inline Normalizer<DT> make_norm(const TileNorm &tn, int scale_bits) {
+template <int DT> __device__ inline Normalizer<DT> make_norm(const TileNorm &tn, int scale_bits, int norm_mode) {
     Normalizer<DT> nz;
+    nz.spatial = norm_mode == 1;
     using T = typename Elem<DT>::T;
     if constexpr (!Elem<DT>::is_float) nz.mn = (T)tn.imin;
     else nz.mn = (T)0;
@@ -243,7 +256,7 @@ __global__ void __launch_bounds__(128) k_analyze(const typename Elem<DT>::T *ras
     const int64_t s0 = (f - g.frame_base) * P.blocksize;
     const int64_t tile_px = (int64_t)g.h * g.w;
     const int n = live ? (int)((tile_px - s0) < P.blocksize ? (tile_px - s0) : P.blocksize) : 0;
-    const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits);
+    const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits, P.norm_mode);
 
     int64_t row = s0 / g.w;
     int col = (int)(s0 - row * g.w);
@@ -469,7 +482,7 @@ __global__ void __launch_bounds__(128) k_analyze_fixed_wide(const typename Elem<
     const int64_t s0 = (f - g.frame_base) * P.blocksize;
     const int64_t tile_px = (int64_t)g.h * g.w;
     const int n = (int)((tile_px - s0) < P.blocksize ? (tile_px - s0) : P.blocksize);
-    const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits);
+    const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits, P.norm_mode);
     SubAnalysis A = out[sub];
     if (n <= 4) return;
     const int w = A.wasted;
@@ -667,7 +680,7 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
     const int64_t s0 = fk * P.blocksize;
     const int64_t tile_px = (int64_t)g.h * g.w;
     const int n = (int)((tile_px - s0) < P.blocksize ? (tile_px - s0) : P.blocksize);
-    const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits);
+    const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits, P.norm_mode);
     uint32_t *slot = slots + (size_t)f * P.slot_words;
     const int rice_limit = P.bps > 16 ? 31 : 15;
     const int max_po_block = min(kMaxPartOrder, __builtin_ctz((unsigned)n));
@@ -1122,7 +1135,11 @@ int dtype_size(int dt) {
     }
 }
 
-static int stream_bps_of(const frs_encode_desc *d) { return d->bits_per_sample == 16 ? 16 : 32; }
+static int stream_bps_of(const frs_encode_desc *d) {
+    // pyflac: bits_per_sample = itemsize * 8 of the sample array (sonos-pyflac.txt:1986-1992): int16 for
+    // bps 16, int32 for bps 24 and float32 for the spatial encoder's normalisation
+    return (d->norm_mode == 0 && d->bits_per_sample == 16) ? 16 : 32;
+}
 
 static int qlp_precision_for(int bps, int blocksize) {
     // stream_encoder.c init: qlp_coeff_precision == 0 (level 5) -> chosen by bps and blocksize
@@ -1200,7 +1217,7 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     P.slot_words = (int32_t)slot_words_for(d);
     P.nframes = nframes;
     P.ntiles = ntiles;
-    P.pad = 0;
+    P.norm_mode = d->norm_mode;
 
     int rc = upload_tables(ctx);
     if (rc) return rc;

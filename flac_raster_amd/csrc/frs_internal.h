@@ -77,8 +77,8 @@ int encode_job(frs_ctx *ctx, const frs_encode_desc *d, const void *raster_dev, v
 int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const int64_t *stream_off,
                int32_t nstreams, int32_t channels, int32_t bps, int32_t blocksize, int32_t *pcm_dev,
                const int64_t *pcm_off);
-int denormalize_job(frs_ctx *ctx, const int32_t *pcm_dev, int64_t n, double dmin, double dmax, int32_t out_dtype,
-                    void *out_dev);
+int denormalize_job(frs_ctx *ctx, const int32_t *pcm_dev, int64_t n, int pcm_bps, double dmin, double dmax,
+                    int32_t out_dtype, void *out_dev);
 int64_t arena_bound(const frs_encode_desc *d);
 int synth_job(frs_ctx *ctx, int16_t *dev, int bands, int64_t height, int64_t width, int64_t row0, int64_t full_height,
               uint64_t seed);

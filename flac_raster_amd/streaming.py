@@ -1,0 +1,285 @@
+"""Streaming FLAC format (create-streaming / extract-streaming) on the MI355X codec.
+
+Reference: cli.py:620-804 (create_streaming) and cli.py:875-1039 (extract_streaming).
+File layout: ``[u32 BE index_len][compact JSON index][tile FLAC 0]...[tile FLAC N-1]``; every tile is a
+complete FLAC stream of band 1 (cli.py:699) with the mutagen-embedded geospatial tags of its temporary
+GeoTIFF (converter.py:315-349).
+
+Differences from the reference are only in *how*: all tiles are encoded in one GPU call (the reference
+loops tiles serially through two temporary files each), and extraction decodes any number of tiles in
+one batched GPU call.  ``extract_bbox_mosaic`` is an extension: the reference returns
+only the first intersecting tile.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import struct
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+from . import container, geotiff
+from ._native import Context, default_context
+from .converter import audio_params, write_tiff_from_meta
+
+log = logging.getLogger("flac_raster.streaming")
+
+
+# ----------------------------------------------------------------------------- encode
+def tile_grid(height: int, width: int, tile: int) -> List[Tuple[int, int, int, int]]:
+    """cli.py:691-696: row-major (col_off, row_off, w, h) windows, edge tiles truncated."""
+    out = []
+    for row in range(0, height, tile):
+        for col in range(0, width, tile):
+            out.append((col, row, min(tile, width - col), min(tile, height - row)))
+    return out
+
+
+def tile_transform_and_bbox(transform: geotiff.Affine, col: int, row: int, w: int, h: int):
+    """cli.py:702-706 with rasterio's window_transform."""
+    tt = geotiff.window_transform(transform, col, row)
+    xmin = tt.c
+    ymax = tt.f
+    xmax = xmin + (w * tt.a)
+    ymin = ymax + (h * tt.e)
+    return tt, [xmin, ymin, xmax, ymax]
+
+
+def tile_tags(crs: Optional[str], tt: geotiff.Affine, w: int, h: int, dtype, tmin: float, tmax: float):
+    """Tags of the per-tile FLAC (tiff_to_flac on the temporary 1-band GeoTIFF, cli.py:719-733)."""
+    bounds = geotiff.GeoRaster(np.empty((1, h, w), dtype=np.uint8), tt).bounds
+    md = {
+        "width": w, "height": h, "count": 1, "dtype": str(np.dtype(dtype)), "crs": crs,
+        "transform": list(tt),
+        "bounds": {"left": bounds[0], "bottom": bounds[1], "right": bounds[2], "top": bounds[3]},
+        "data_min": tmin, "data_max": tmax, "nodata": None, "driver": "GTiff",
+    }
+    return container.raster_tags(md)
+
+
+@dataclass
+class EncodedTiles:
+    """Output of one GPU encode of all band-1 tiles."""
+    windows: List[Tuple[int, int, int, int]]
+    frames: np.ndarray          # arena: all tiles' frames back to back
+    tile_off: np.ndarray        # int64[n+1]
+    tile_min: np.ndarray
+    tile_max: np.ndarray
+    stream_bps: int
+
+
+def encode_band_tiles(band: np.ndarray, tile_size: int, ctx: Optional[Context] = None) -> EncodedTiles:
+    """All band-1 tiles in one GPU launch sequence (the reference's tile loop, cli.py:690-763)."""
+    ctx = ctx or default_context()
+    H, W = band.shape
+    _, bps = audio_params(1, min(tile_size, H), band.dtype)
+    d = ctx.make_desc(H, W, band.dtype, nbands=1, tile_h=tile_size, tile_w=tile_size, sample_rate=44100,
+                      bits_per_sample=bps)
+    arena, off, mn, mx, sbps = ctx.encode_tiles_host(np.ascontiguousarray(band), d)
+    return EncodedTiles(tile_grid(H, W, tile_size), arena, off, mn, mx, sbps)
+
+
+def assemble_streaming(enc: EncodedTiles, transform: geotiff.Affine, crs: Optional[str], width: int, height: int,
+                       tile_size: int, dtype) -> Tuple[bytes, List[bytes], Dict]:
+    """Index JSON + per-tile FLAC streams (header bytes + frames) -> (head, tile_streams, index)."""
+    index = {"crs": str(crs), "transform": list(transform), "width": width, "height": height,
+             "tile_size": tile_size, "frames": []}
+    streams: List[bytes] = []
+    total = 0
+    frames = enc.frames
+    for i, (col, row, w, h) in enumerate(enc.windows):
+        tt, bbox = tile_transform_and_bbox(transform, col, row, w, h)
+        # sample rate of the tile: _calculate_audio_params on the (1, h, w) array -> shape0*shape1 = h
+        sr, _ = audio_params(1, h, dtype)
+        body = frames[enc.tile_off[i]:enc.tile_off[i + 1]].tobytes()
+        if sr != 44100:
+            raise NotImplementedError("tile heights >= 1e6 rows change the sample rate; re-encode needed")
+        hdr = container.mutagen_header(1, enc.stream_bps, sr,
+                                       tile_tags(crs, tt, w, h, dtype, float(enc.tile_min[i]), float(enc.tile_max[i])),
+                                       len(body))
+        s = hdr + body
+        index["frames"].append({"frame_id": i, "bbox": bbox,
+                                "window": {"col_off": col, "row_off": row, "width": w, "height": h},
+                                "byte_offset": total, "byte_size": len(s)})
+        streams.append(s)
+        total += len(s)
+    js = container.index_json(index)
+    return struct.pack(">I", len(js)) + js, streams, index
+
+
+def create_streaming(input_file: Path, output_file: Path, tile_size: int = 1024,
+                     ctx: Optional[Context] = None) -> Dict:
+    """cli.py:620-804 without the console output: writes the streaming file, returns the index."""
+    r = geotiff.read(input_file)
+    transform = r.transform or geotiff.Affine(1.0, 0.0, 0.0, 0.0, 1.0, 0.0)
+    band = np.ascontiguousarray(r.data[0])
+    enc = encode_band_tiles(band, tile_size, ctx)
+    head, streams, index = assemble_streaming(enc, transform, r.crs_string, r.width, r.height, tile_size, band.dtype)
+    with open(output_file, "wb") as fh:
+        fh.write(head)
+        for s in streams:
+            fh.write(s)
+    return index
+
+
+# ----------------------------------------------------------------------------- read / select
+class Source:
+    """Local file or HTTP(S) URL with byte-range reads (cli.py:898-919, 1001-1011)."""
+
+    def __init__(self, path_or_url: Union[str, Path]):
+        self.src = str(path_or_url)
+        self.is_url = self.src.startswith(("http://", "https://"))
+
+    def read(self, start: int, length: int) -> bytes:
+        if length <= 0:
+            return b""
+        if self.is_url:
+            import requests
+            r = requests.get(self.src, headers={"Range": f"bytes={start}-{start + length - 1}"})
+            if r.status_code != 206:
+                raise ValueError(f"Server doesn't support range requests: {r.status_code}")
+            return r.content
+        with open(self.src, "rb") as fh:
+            fh.seek(start)
+            return fh.read(length)
+
+    def read_ranges(self, ranges: Sequence[Tuple[int, int]]) -> List[bytes]:
+        if not self.is_url:
+            out = []
+            with open(self.src, "rb") as fh:
+                for s, n in ranges:
+                    fh.seek(s)
+                    out.append(fh.read(n))
+            return out
+        return [self.read(s, n) for s, n in ranges]
+
+
+def read_index(src: Union[str, Path, Source]) -> Tuple[int, Dict]:
+    """Index size and JSON index (cli.py:898-919)."""
+    s = src if isinstance(src, Source) else Source(src)
+    n = struct.unpack(">I", s.read(0, 4))[0]
+    return n, json.loads(s.read(4, n).decode("utf-8"))
+
+
+def select_frame(index: Dict, tile_id: Optional[int] = None, last: bool = False, center: bool = False,
+                 bbox: Optional[Sequence[float]] = None) -> Dict:
+    """cli.py:926-990: precedence tile_id > last > center > bbox; bbox = first strict intersection."""
+    frames = index["frames"]
+    if tile_id is not None:
+        for f in frames:
+            if f["frame_id"] == tile_id:
+                return f
+        raise KeyError(f"Tile ID {tile_id} not found")
+    if last:
+        return max(frames, key=lambda f: f["frame_id"])
+    if center:
+        bbs = [f["bbox"] for f in frames]
+        cx = (min(b[0] for b in bbs) + max(b[2] for b in bbs)) / 2
+        cy = (min(b[1] for b in bbs) + max(b[3] for b in bbs)) / 2
+        best, dmin = None, float("inf")
+        for f in frames:
+            fx = (f["bbox"][0] + f["bbox"][2]) / 2
+            fy = (f["bbox"][1] + f["bbox"][3]) / 2
+            d = ((fx - cx) ** 2 + (fy - cy) ** 2) ** 0.5
+            if d < dmin:
+                dmin, best = d, f
+        return best
+    if bbox is not None:
+        hits = intersecting(index, bbox)
+        if not hits:
+            raise LookupError(f"No tiles intersect with bbox {bbox}")
+        return hits[0]
+    raise ValueError("Must specify --tile-id, --bbox, --center, or --last")
+
+
+def intersecting(index: Dict, bbox: Sequence[float]) -> List[Dict]:
+    """cli.py:976-979 strict-inequality intersection, index order."""
+    x0, y0, x1, y1 = bbox
+    return [f for f in index["frames"]
+            if x0 < f["bbox"][2] and x1 > f["bbox"][0] and y0 < f["bbox"][3] and y1 > f["bbox"][1]]
+
+
+# ----------------------------------------------------------------------------- decode
+class TileDecoder:
+    """Batched GPU decode of streaming tiles: one frs_decode_frames call for any number of tiles."""
+
+    def __init__(self, ctx: Optional[Context] = None):
+        self.ctx = ctx or default_context()
+
+    def decode_streams(self, streams: Sequence[bytes]) -> List[Tuple[np.ndarray, Dict]]:
+        metas = [container.parse_metadata(s) for s in streams]
+        mds = [container.read_raster_tags(m) for m in metas]
+        for m, md in zip(metas, mds):
+            if md is None:
+                raise ValueError("No metadata found in FLAC file or sidecar file")
+            if m.bps not in (16, 32):
+                raise ValueError("Only int16/int32 data type is supported")
+        out: List[Tuple[np.ndarray, Dict]] = [None] * len(streams)
+        # group by (channels, bps, blocksize) so each group is one GPU call
+        groups: Dict[Tuple[int, int, int], List[int]] = {}
+        for i, m in enumerate(metas):
+            groups.setdefault((m.channels, m.bps, m.blocksize), []).append(i)
+        for (ch, bps, bs), idx in groups.items():
+            blobs = [np.frombuffer(streams[i], dtype=np.uint8)[metas[i].audio_offset:] for i in idx]
+            soff = np.zeros(len(idx) + 1, dtype=np.int64)
+            soff[1:] = np.cumsum([len(b) for b in blobs])
+            blob = np.concatenate(blobs) if blobs else np.zeros(0, np.uint8)
+            counts = [int(mds[i]["width"]) * int(mds[i]["height"]) for i in idx]
+            pcm = self.ctx.decode_frames_host(blob, soff, counts, channels=ch, bps=bps, blocksize=bs)
+            p0 = 0
+            for j, i in enumerate(idx):
+                md = mds[i]
+                n = counts[j]
+                seg = pcm[p0:p0 + n]
+                p0 += n
+                dt = np.dtype(md["dtype"])
+                vals = self.ctx.denormalize_host(seg, md["data_min"], md["data_max"], dt, pcm_bps=bps)
+                H, W, C = int(md["height"]), int(md["width"]), int(md["count"])
+                arr = vals.reshape(H, W, C).transpose(2, 0, 1) if C > 1 else vals.reshape(1, H, W)
+                out[i] = (np.ascontiguousarray(arr), md)
+        return out
+
+
+def fetch_tiles(src: Union[str, Path, Source], frames: Sequence[Dict], index_size: int) -> List[bytes]:
+    s = src if isinstance(src, Source) else Source(src)
+    return s.read_ranges([(4 + index_size + f["byte_offset"], f["byte_size"]) for f in frames])
+
+
+def extract_streaming(flac_url: Union[str, Path], output: Path, bbox: Optional[Sequence[float]] = None,
+                      tile_id: Optional[int] = None, center: bool = False, last: bool = False,
+                      ctx: Optional[Context] = None) -> Dict:
+    """cli.py:875-1039: pick one tile, range-read it, decode it and write it as a GeoTIFF."""
+    src = Source(flac_url)
+    n, index = read_index(src)
+    f = select_frame(index, tile_id=tile_id, last=last, center=center, bbox=bbox)
+    data = fetch_tiles(src, [f], n)[0]
+    (arr, md), = TileDecoder(ctx).decode_streams([data])
+    write_tiff_from_meta(Path(output), arr, md)
+    return f
+
+
+def extract_bbox_mosaic(flac_url: Union[str, Path], bbox: Sequence[float], ctx: Optional[Context] = None):
+    """Extension: decode every tile intersecting bbox in one GPU batch and mosaic them into
+    the raster window they cover.  Returns (array (1, h, w), window dict, transform list)."""
+    src = Source(flac_url)
+    n, index = read_index(src)
+    hits = intersecting(index, bbox)
+    if not hits:
+        raise LookupError(f"No tiles intersect with bbox {bbox}")
+    datas = fetch_tiles(src, hits, n)
+    dec = TileDecoder(ctx).decode_streams(datas)
+    c0 = min(f["window"]["col_off"] for f in hits)
+    r0 = min(f["window"]["row_off"] for f in hits)
+    c1 = max(f["window"]["col_off"] + f["window"]["width"] for f in hits)
+    r1 = max(f["window"]["row_off"] + f["window"]["height"] for f in hits)
+    dtype = dec[0][0].dtype
+    out = np.zeros((1, r1 - r0, c1 - c0), dtype=dtype)
+    for f, (arr, _) in zip(hits, dec):
+        w = f["window"]
+        out[0, w["row_off"] - r0:w["row_off"] - r0 + w["height"], w["col_off"] - c0:w["col_off"] - c0 + w["width"]] = arr[0]
+    t = geotiff.Affine(*index["transform"][:6])
+    wt = geotiff.window_transform(t, c0, r0)
+    return out, {"col_off": c0, "row_off": r0, "width": c1 - c0, "height": r1 - r0}, list(wt)

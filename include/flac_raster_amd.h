@@ -79,8 +79,16 @@ typedef struct {
     int32_t sample_rate;        /* STREAMINFO / frame header sample rate (converter.py:25-54) */
     int32_t bits_per_sample;    /* 16 or 24 from _calculate_audio_params (converter.py:29-37) */
     int32_t compression_level;  /* must be 5 (cli.py:733, converter.py default) */
+    int32_t norm_mode;          /* FRS_NORM_CONVERTER or FRS_NORM_SPATIAL */
     int64_t tile_begin, tile_end;
 } frs_encode_desc;
+
+/* sample normalisation of an encode job */
+enum frs_norm_mode {
+    FRS_NORM_CONVERTER = 0, /* converter.py:56-86: min/max -> int16 (bps 16) or int32 x 8388607 (bps 24) */
+    FRS_NORM_SPATIAL = 1    /* spatial_encoder.py:229-248: dtype-fixed float32 scaling, pyflac casts to int32
+                               (32-bit stream, samples in {-1, 0, 1}: the lossy raw-frames format) */
+};
 
 int frs_abi_version(void);
 /* number of usable gfx950 devices (0 when none) */
@@ -120,13 +128,15 @@ int frs_decode_frames_device(frs_ctx *ctx, const uint8_t *blob_dev, const int64_
 int frs_decode_frames(frs_ctx *ctx, const uint8_t *blob_host, const int64_t *stream_off, int32_t nstreams,
                       int32_t channels, int32_t bps, int32_t blocksize, int32_t *pcm_host, const int64_t *pcm_off);
 
-/* converter.py:88-110 after pyflac+soundfile's PCM_16 -> float64 = pcm/32768 (sonos-pyflac.txt:1629):
- * out = round_half_even(((float32(pcm/32768) + 1)/2) * float32(max-min) + float32(min)), fp32 ops,
- * cast to out_dtype.  For float out_dtype the scaled value float32(pcm/32768) is written as-is. */
-int frs_denormalize_device(frs_ctx *ctx, const int32_t *pcm_dev, int64_t n, double data_min, double data_max,
-                           int32_t out_dtype, void *out_dev);
-int frs_denormalize(frs_ctx *ctx, const int32_t *pcm_host, int64_t n, double data_min, double data_max,
-                    int32_t out_dtype, void *out_host);
+/* converter.py:88-110 after pyflac+soundfile's WAV round trip (sonos-pyflac.txt:1629, 1827-1852): the
+ * decoder's int32 samples go into a PCM_16 WAV (16-bit streams unchanged; 32-bit streams keep x >> 16,
+ * libsndfile's int->short conversion) and are read back as float64 = pcm16/32768.  Then
+ * out = round_half_even(((float32(v) + 1)/2) * float32(max-min) + float32(min)), all fp32 ops, cast to
+ * out_dtype; for a float out_dtype float32(v) is written as-is.  pcm_bps = STREAMINFO bits per sample. */
+int frs_denormalize_device(frs_ctx *ctx, const int32_t *pcm_dev, int64_t n, int32_t pcm_bps, double data_min,
+                           double data_max, int32_t out_dtype, void *out_dev);
+int frs_denormalize(frs_ctx *ctx, const int32_t *pcm_host, int64_t n, int32_t pcm_bps, double data_min,
+                    double data_max, int32_t out_dtype, void *out_host);
 
 /* Device memory helpers so hosts need no other GPU runtime binding (no PyTorch in the codec path). */
 void *frs_dev_malloc(frs_ctx *ctx, int64_t bytes);

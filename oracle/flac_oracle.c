@@ -744,13 +744,39 @@ int orc_normalize(const void *src, int dtype, int64_t n, int bits_per_sample, do
     return bits_per_sample == 16 ? 16 : 32;
 }
 
+/* spatial_encoder.py:229-248 then pyflac's samples.astype(np.int32) (sonos-pyflac.txt:1994): float32 maths,
+ * truncation.  Returns 0, or -1 for dtypes whose normalised array is float64 (pyflac then asks libFLAC for
+ * 64-bit samples and fails). */
+int orc_normalize_spatial(const void *src, int dtype, int64_t n, int32_t *dst) {
+    for (int64_t i = 0; i < n; i++) {
+        volatile float v;
+        switch (dtype) {
+        case 1: v = ((float)((const uint8_t *)src)[i] - 127.5f) / 127.5f; break;
+        case 2: v = ((float)((const uint16_t *)src)[i] - 32767.5f) / 32767.5f; break;
+        case 3: v = (float)((const int16_t *)src)[i] / 32767.0f; break;
+        case 4: v = (float)((const int32_t *)src)[i] / 2147483647.0f; break;
+        case 6: {
+            float x = ((const float *)src)[i];
+            v = x < -1.0f ? -1.0f : (x > 1.0f ? 1.0f : x);
+            if (x != x) v = x;
+            break;
+        }
+        default: return -1;
+        }
+        dst[i] = cast_f64_i32((double)v);
+    }
+    return 0;
+}
+
 /* converter.py:88-110 with the decode scaling of pyflac+soundfile (pcm/32768, docs/sonos-pyflac.txt:1629):
  * v = float32(pcm/32768); out = round_half_even(((v + 1)/2) * f32(max-min) + f32(min)), all fp32. */
 static double rint_even(double v) { return nearbyint(v); }
-void orc_denormalize_i16(const int32_t *pcm, int64_t n, double dmin, double dmax, int out_dtype, void *out) {
+void orc_denormalize_i16(const int32_t *pcm, int64_t n, int pcm_bps, double dmin, double dmax, int out_dtype,
+                         void *out) {
     float rng = (float)(dmax - dmin), fmn = (float)dmin;
     for (int64_t i = 0; i < n; i++) {
-        float v = (float)((double)pcm[i] / 32768.0);
+        int32_t p16 = pcm_bps > 16 ? (pcm[i] >> 16) : pcm[i]; /* libsndfile int -> short for 32-bit streams */
+        float v = (float)((double)p16 / 32768.0);
         volatile float a = v + 1.0f;
         volatile float b = a / 2.0f;
         volatile float c = b * rng;

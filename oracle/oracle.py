@@ -43,11 +43,13 @@ def lib():
         L.orc_normalize.restype = i32
         L.orc_normalize.argtypes = [vp, i32, i64, i32, dp, dp, vp]
         L.orc_denormalize_i16.restype = None
-        L.orc_denormalize_i16.argtypes = [vp, i64, ctypes.c_double, ctypes.c_double, i32, vp]
+        L.orc_denormalize_i16.argtypes = [vp, i64, i32, ctypes.c_double, ctypes.c_double, i32, vp]
         L.orc_decode_frames.restype = i64
         L.orc_decode_frames.argtypes = [vp, i64, i32, i32, vp, i64]
         L.orc_encode_tiles.restype = i64
         L.orc_encode_tiles.argtypes = [vp, i32, i64, i64, i64, i32, i32, i32, vp, i64, vp, vp, vp, i32]
+        L.orc_normalize_spatial.restype = i32
+        L.orc_normalize_spatial.argtypes = [vp, i32, i64, vp]
         L.orc_window_tukey.restype = None
         L.orc_window_tukey.argtypes = [vp, i32, ctypes.c_float]
         _lib = L
@@ -88,6 +90,15 @@ def normalize(arr: np.ndarray):
     return out, mn.value, mx.value, bps
 
 
+def normalize_spatial(arr: np.ndarray) -> np.ndarray:
+    """spatial_encoder.py:229-248 + pyflac's astype(int32): samples in {-1, 0, 1}."""
+    a = np.ascontiguousarray(arr)
+    out = np.empty(a.shape, dtype=np.int32)
+    if lib().orc_normalize_spatial(_ptr(a), DTYPES[a.dtype], a.size, _ptr(out)) != 0:
+        raise ValueError("pyflac rejects the 64-bit sample array of this dtype")
+    return out
+
+
 def encode_frames(pcm: np.ndarray, bps: int, sample_rate: int, blocksize: int = 4096) -> bytes:
     """libFLAC level-5 frames for interleaved pcm [N, C] (int32)."""
     x = np.ascontiguousarray(pcm, dtype=np.int32)
@@ -117,11 +128,11 @@ def decode_frames(data: bytes, channels: int, bps: int, max_samples: int) -> np.
     return out[:r]
 
 
-def denormalize_i16(pcm: np.ndarray, dmin: float, dmax: float, dtype) -> np.ndarray:
-    """converter.py:88-110 after pyflac+soundfile's pcm/32768 scaling (sonos-pyflac.txt:1629)."""
+def denormalize_i16(pcm: np.ndarray, dmin: float, dmax: float, dtype, pcm_bps: int = 16) -> np.ndarray:
+    """converter.py:88-110 after pyflac+soundfile's PCM_16 WAV round trip (sonos-pyflac.txt:1629)."""
     p = np.ascontiguousarray(pcm, dtype=np.int32)
     out = np.empty(p.shape, dtype=dtype)
-    lib().orc_denormalize_i16(_ptr(p), p.size, dmin, dmax, DTYPES[np.dtype(dtype)], _ptr(out))
+    lib().orc_denormalize_i16(_ptr(p), p.size, pcm_bps, dmin, dmax, DTYPES[np.dtype(dtype)], _ptr(out))
     return out
 
 

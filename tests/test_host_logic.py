@@ -1,0 +1,85 @@
+"""CPU tests of the product's host-side logic (containers, GeoTIFF, tile selection) -- no GPU calls."""
+import json
+import struct
+
+import numpy as np
+import pytest
+
+from flac_raster_amd import container, geotiff, streaming
+from flac_raster_amd.converter import audio_params, raster_metadata
+from oracle import pipeline as P
+
+
+def test_bare_header_matches_fixture(golden):
+    assert container.bare_header(3, 16, 44100) == (golden / "sample_rgb.flac").read_bytes()[:86]
+
+
+def test_mutagen_header_matches_fixture(golden):
+    fx = (golden / "sample_dem.flac").read_bytes()
+    m = container.parse_metadata(fx)
+    content = len(fx) - m.audio_offset
+    hdr = container.mutagen_header(1, 32, 44100, m.tags, content)
+    assert hdr == fx[:m.audio_offset]
+
+
+def test_product_container_equals_oracle_restatement(golden):
+    r = geotiff.read(golden / "sample_rgb.tif")
+    md = raster_metadata(r, 1.0, 255.0)
+    tags = container.raster_tags(md)
+    assert tags == P.tags_converter(md)
+    bare = container.bare_header(3, 16, 44100) + bytes(5000)
+    assert container.mutagen_header(3, 16, 44100, tags, 5000) + bytes(5000) == P.mutagen_save(bare, tags)
+
+
+def test_sidecar_json_matches_fixture(golden):
+    r = geotiff.read(golden / "sample_rgb.tif")
+    md = raster_metadata(r, 1.0, 255.0)
+    assert json.dumps(md, indent=2) == (golden / "sample_rgb.json").read_text()
+
+
+def test_audio_params_quirk_q3():
+    assert audio_params(3, 256, np.uint8) == (44100, 16)
+    assert audio_params(4, 300000, np.int16) == (48000, 16)   # bands*height, not pixels
+    assert audio_params(1, 512, np.int32) == (44100, 24)
+
+
+def test_window_transform_and_bbox_match_oracle():
+    t = geotiff.Affine(0.0001, 0.0, -120.0, 0.0, -0.0001, 37.0)
+    for col, row in [(0, 0), (512, 0), (512, 1024), (37, 91)]:
+        tt = geotiff.window_transform(t, col, row)
+        assert tt.to_tuple() == P._window_transform(list(t), col, row)
+
+
+def test_select_frame_semantics():
+    idx = {"frames": [
+        {"frame_id": 0, "bbox": [0, 10, 10, 20]}, {"frame_id": 1, "bbox": [10, 10, 20, 20]},
+        {"frame_id": 2, "bbox": [0, 0, 10, 10]}, {"frame_id": 3, "bbox": [10, 0, 20, 10]}]}
+    assert streaming.select_frame(idx, tile_id=2)["frame_id"] == 2
+    assert streaming.select_frame(idx, tile_id=2, last=True)["frame_id"] == 2   # tile_id wins
+    assert streaming.select_frame(idx, last=True, center=True)["frame_id"] == 3
+    assert streaming.select_frame(idx, center=True)["frame_id"] == 0            # first minimum
+    assert streaming.select_frame(idx, bbox=[9, 9, 11, 11])["frame_id"] == 0    # first intersecting
+    assert streaming.select_frame(idx, bbox=[10, 10, 15, 15])["frame_id"] == 1  # strict: edge-touch excluded
+    with pytest.raises(LookupError):
+        streaming.select_frame(idx, bbox=[30, 30, 40, 40])
+    with pytest.raises(KeyError):
+        streaming.select_frame(idx, tile_id=9)
+
+
+def test_geotiff_roundtrip(tmp_path):
+    rng = np.random.default_rng(1)
+    for dt, count in [(np.uint8, 3), (np.int16, 1), (np.uint16, 4), (np.float32, 2)]:
+        a = (rng.random((count, 37, 53)) * 1000).astype(dt)
+        t = geotiff.Affine(10.0, 0.0, 500000.0, 0.0, -10.0, 4000000.0)
+        p = tmp_path / f"x_{np.dtype(dt).name}.tif"
+        geotiff.write(p, a, transform=t, epsg=32636, nodata=0)
+        r = geotiff.read(p)
+        assert np.array_equal(r.data, a) and r.data.dtype == a.dtype
+        assert r.transform.to_tuple() == t.to_tuple() and r.epsg == 32636 and r.nodata == 0.0
+
+
+def test_streaming_header_parse():
+    idx = {"crs": "EPSG:4326", "frames": []}
+    js = container.index_json(idx)
+    n, back = container.parse_streaming_header(struct.pack(">I", len(js)) + js)
+    assert n == len(js) and back == idx
