@@ -1,6 +1,7 @@
 // frs_abi.hip -- exported C-ABI (include/flac_raster_amd.h): contexts, argument checks, host staging,
 // profiling.  The product has no CPU fallback: without a gfx950 device every entry point fails with
 // FRS_E_NODEV and the Python host raises.
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -93,6 +94,8 @@ int frs_ctx_create(int device, frs_ctx **out) {
     if (!is_gfx950(device)) return FRS_E_NODEV;
     frs_ctx *ctx = new frs_ctx();
     ctx->device = device;
+    const char *fg = getenv("FRS_FORCE_GENERIC");
+    ctx->force_generic = fg && fg[0] == '1';
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return FRS_E_HIP;
@@ -107,7 +110,7 @@ void frs_ctx_destroy(frs_ctx *ctx) {
     hipStreamSynchronize(ctx->stream);
     frs::prof_collect(ctx);
     DevBuf *bufs[] = {&ctx->tiles, &ctx->norms, &ctx->analysis, &ctx->slots, &ctx->frame_bytes, &ctx->frame_off,
-                      &ctx->scan_tmp, &ctx->window, &ctx->tile_sizes, &ctx->raster_stage, &ctx->arena_stage,
+                      &ctx->scan_tmp, &ctx->window, &ctx->tile_sizes, &ctx->luts, &ctx->status, &ctx->raster_stage, &ctx->arena_stage,
                       &ctx->dec_cand, &ctx->dec_count, &ctx->dec_blob, &ctx->dec_pcm, &ctx->dec_soff, &ctx->dec_poff};
     for (DevBuf *b : bufs) b->release();
     hipStreamDestroy(ctx->stream);

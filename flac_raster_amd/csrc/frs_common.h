@@ -31,9 +31,15 @@ struct TileNorm {
     int64_t imin, imax;  // integer min / max, or order-preserving bits of float min / max
     double dmin, dmax;   // float(np.min(tile)), float(np.max(tile))
     double den;          // (double)(dtype)(max - min)  -- numpy same-kind (wrapping) subtraction
+    double rinv;         // RN(1/den) for the exact reciprocal division (fastdiv)
     int32_t has_range;   // max > min
-    int32_t pad;
+    int32_t mode;        // kNorm*: how the fast kernels normalise this tile
 };
+constexpr int kNormLut = 0;      // pcm = lut[x - min] (R + 1 <= kLutCap entries, built once per tile)
+constexpr int kNormFastDiv = 1;  // no wrap, den <= 65535: RN(2d/den) by reciprocal + 2 FMA (exhaustively exact)
+constexpr int kNormSlow = 2;     // anything else (wrapping int16, 32-bit dtypes, floats): IEEE division
+constexpr int kNormZero = 3;     // max == min: zeros
+constexpr int kLutCap = 4096;    // LUT entries per tile
 
 // Per-subframe decision inputs produced by the analysis kernel (lane = subframe).
 struct SubAnalysis {
@@ -61,6 +67,8 @@ struct EncodeParams {
     int64_t nframes;
     int32_t ntiles;
     int32_t norm_mode;    // 0 converter.py:56-86, 1 spatial_encoder.py:229-248
+    int32_t vec_ok;       // rows 16-B aligned and tile widths multiples of 64 (fast loads)
+    int32_t pad2;
 };
 
 __host__ __device__ inline int ilog2_u32(uint32_t v) { return 31 - __builtin_clz(v); }

@@ -15,6 +15,8 @@
 //   k_compact        workgroup = frame: CRC-16 (parallel GF(2) combine) + copy slot -> arena offset
 #include <hipcub/hipcub.hpp>
 
+#include <type_traits>
+
 #include "frs_internal.h"
 
 namespace frs {
@@ -147,11 +149,13 @@ __global__ void __launch_bounds__(256) k_tile_stats(const typename Elem<DT>::T *
     }
 }
 
-template <int DT> __global__ void k_tile_finalize(TileNorm *norms, int ntiles) {
+template <int DT> __global__ void k_tile_finalize(TileNorm *norms, int ntiles, int norm_mode, int scale_bits) {
     int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntiles) return;
     TileNorm n = norms[t];
     using T = typename Elem<DT>::T;
+    n.mode = kNormSlow;
+    n.rinv = 0.0;
     if constexpr (Elem<DT>::is_float) {
         n.dmin = key2f(n.imin);
         n.dmax = key2f(n.imax);
@@ -162,6 +166,14 @@ template <int DT> __global__ void k_tile_finalize(TileNorm *norms, int ntiles) {
         n.dmax = (double)n.imax;
         n.has_range = n.imax > n.imin;
         n.den = (double)(T)(n.imax - n.imin);  // data_max - data_min in the dtype (wraps for int16)
+        const int64_t R = n.imax - n.imin;
+        const bool nowrap = (int64_t)(T)R == R;  // x - min and max - min never wrap in the dtype
+        if (norm_mode == 0 && scale_bits == 16) {
+            if (!n.has_range) n.mode = kNormZero;
+            else if (nowrap && R + 1 <= kLutCap) n.mode = kNormLut;
+            else if (nowrap && R <= 65535) n.mode = kNormFastDiv;
+            n.rinv = 1.0 / n.den;
+        }
     }
     norms[t] = n;
 }
@@ -1083,6 +1095,789 @@ __global__ void k_gather_tile_off(const int64_t *frame_off, const TileGeom *tile
     if (t == ntiles) tile_off[t] = total;
 }
 
+// =================================================================================================
+// FAST PATH (16-bit mono streams: create-streaming band-1 tiles, converter bps 16)
+//   k_build_lut     per tile: pcm = lut[x - min] for x - min in [0, R] (exact double path, once per value)
+//   k_analyze_v2    lane = frame; 64-sample chunks loaded as 8 x 16 B per lane (no L1 reuse needed),
+//                   LUT normalisation, wave-uniform window from LDS, 9 fp64 FMA chains per lane
+//   k_encode_v2     wave = frame, 64 consecutive samples per lane held in registers: fixed totals,
+//                   v_dot2 residuals, partition sums by lane-pair shuffles, Rice search, exact bit
+//                   positions by one wave scan, LDS bit packing, CRC-16, single-pass decoupled
+//                   look-back for the frame's arena offset, byte-exact store at that offset
+// =================================================================================================
+
+// exact converter.py normalisation of one element for the fast kernels (mode per tile)
+template <int DT>
+__device__ inline int32_t norm_fast(typename Elem<DT>::T x, const TileNorm &tn, const int16_t *lut) {
+    if constexpr (Elem<DT>::is_float) {
+        (void)tn; (void)lut;
+        return 0;  // float rasters never take the fast path (32-bit streams)
+    } else {
+        const int64_t d = (int64_t)x - tn.imin;
+        switch (tn.mode) {
+        case kNormLut: return lut[d];
+        case kNormZero: return 0;
+        case kNormFastDiv: {
+            const double a = (double)(2 * d);
+            const double q0 = a * tn.rinv;
+            const double r = fma(-q0, tn.den, a);
+            const double q1 = fma(r, tn.rinv, q0);  // == RN(a / den): verified for every d <= den <= 65535
+            const double v = (q1 - 1.0) * 32767.0;
+            return (int32_t)(int16_t)cast_f64_i32_x86(v);
+        }
+        default: {
+            using T = typename Elem<DT>::T;
+            const T dd = (T)((int64_t)x - tn.imin);
+            const double v = ((2.0 * (double)dd) / tn.den - 1.0) * 32767.0;
+            return (int32_t)(int16_t)cast_f64_i32_x86(v);
+        }
+        }
+    }
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) k_build_lut(const TileNorm *norms, int16_t *luts) {
+    const int t = blockIdx.x;
+    const TileNorm tn = norms[t];
+    if (tn.mode != kNormLut) return;
+    using T = typename Elem<DT>::T;
+    const int64_t R = tn.imax - tn.imin;
+    for (int64_t d = threadIdx.x; d <= R; d += blockDim.x) {
+        const T dd = (T)d;
+        const double v = ((2.0 * (double)dd) / tn.den - 1.0) * 32767.0;  // numpy: 2.0*(x-min)/(max-min)-1.0, *32767
+        luts[(int64_t)t * kLutCap + d] = (int16_t)cast_f64_i32_x86(v);
+    }
+}
+
+// 64 consecutive elements of a frame, kept packed in 32-bit words (int16: 32 words; uint8: 16 words).
+// vec: 16-byte loads of one row segment; otherwise an element gather with a row cursor.
+template <int DT> struct Chunk64 {
+    using T = typename Elem<DT>::T;
+    static constexpr int kWords = (int)(64 * sizeof(T) / 4);
+    uint32_t w[kWords];
+    __device__ inline T get(int j) const {  // j must be a compile-time constant after unrolling
+        if constexpr (sizeof(T) == 1) return (T)((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+        else if constexpr (sizeof(T) == 2) return (T)((w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
+        else return __builtin_bit_cast(T, w[j]);
+    }
+    __device__ inline void load(const T *base, int64_t row_stride, int width, int64_t s, bool vec, int nvalid) {
+        if (vec) {
+            const int64_t row = s / width;
+            const int col = (int)(s - row * width);
+            const uint4 *p = reinterpret_cast<const uint4 *>(base + row * row_stride + col);
+#pragma unroll
+            for (int k = 0; k < kWords / 4; k++) {
+                const uint4 v = p[k];
+                w[4 * k] = v.x;
+                w[4 * k + 1] = v.y;
+                w[4 * k + 2] = v.z;
+                w[4 * k + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kWords; k++) w[k] = 0;
+            int64_t row = s / width;
+            int col = (int)(s - row * width);
+            const T *rp = base + row * row_stride;
+            for (int j = 0; j < nvalid; j++) {
+                uint32_t v;
+                if constexpr (sizeof(T) == 4) v = __builtin_bit_cast(uint32_t, rp[col]);
+                else v = (uint32_t)(std::make_unsigned_t<T>)rp[col];
+                // dynamic insert (rare path): rebuild through a small switch-free loop
+#pragma unroll
+                for (int k = 0; k < kWords; k++) {
+                    constexpr int per = 4 / (int)sizeof(T);
+                    if (k == j / per) {
+                        const int sh = (int)(8 * sizeof(T)) * (j % per);
+                        w[k] |= (sizeof(T) == 4) ? v : (v << sh);
+                    }
+                }
+                if (++col == width) {
+                    col = 0;
+                    rp += row_stride;
+                }
+            }
+        }
+    }
+};
+
+template <int DT>
+__global__ void __launch_bounds__(256) k_analyze_v2(const typename Elem<DT>::T *raster, EncodeParams P,
+                                                   const TileGeom *tiles, const TileNorm *norms,
+                                                   const int16_t *luts, const float *__restrict__ window,
+                                                   SubAnalysis *out) {
+    using T = typename Elem<DT>::T;
+    __shared__ float swin[kMaxBlock];
+    __shared__ int16_t slut[4][kLutCap];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int i = threadIdx.x; i < P.blocksize; i += blockDim.x) swin[i] = window[i];
+    const int64_t f = ((int64_t)blockIdx.x * 4 + wave) * 64 + lane;
+    const bool live = f < P.nframes;
+    const int t = tile_of_frame(tiles, P.ntiles, live ? f : P.nframes - 1);
+    const TileGeom g = tiles[t];
+    const int64_t s0 = (f - g.frame_base) * P.blocksize;
+    const int64_t tile_px = (int64_t)g.h * g.w;
+    const int n = live ? (int)min((int64_t)P.blocksize, tile_px - s0) : 0;
+    TileNorm tn = norms[t];
+    // LUT: one per wave when the wave's frames share a tile
+    const int t0 = __shfl(t, 0);
+    const bool uni = __all(t == t0);
+    const bool wave_lut = uni && tn.mode == kNormLut;
+    if (wave_lut) {
+        const int64_t R = tn.imax - tn.imin;
+        const int16_t *src = luts + (int64_t)t0 * kLutCap;
+        for (int64_t d = lane; d <= R; d += 64) slut[wave][d] = src[d];
+    }
+    __syncthreads();
+    const int16_t *lut = wave_lut ? slut[wave] : luts + (int64_t)t * kLutCap;
+    const T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
+    const bool vec = P.vec_ok && (g.w % 64) == 0;
+
+    uint32_t or_acc = 0;
+    double acc[kMaxLpc + 1];
+#pragma unroll
+    for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
+    double prev[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) prev[j] = 0.0;
+
+    for (int c = 0; c < P.blocksize / 64; c++) {
+        const int i0 = c * 64;
+        Chunk64<DT> ch;
+        const int nv = min(64, n - i0);
+        if (nv > 0) ch.load(base, P.row_stride, g.w, s0 + i0, vec && nv == 64, nv);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            double cur[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int jj = b * 8 + j;
+                int32_t x = 0;
+                if (jj < nv) x = norm_fast<DT>(ch.get(jj), tn, lut);
+                or_acc |= (uint32_t)x;
+                cur[j] = (double)((float)x * swin[i0 + jj]);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+#pragma unroll
+                for (int l = 0; l <= kMaxLpc; l++) {
+                    const double other = (j - l >= 0) ? cur[j - l] : prev[8 + j - l];
+                    acc[l] = fma(cur[j], other, acc[l]);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) prev[j] = cur[j];
+        }
+    }
+    if (!live) return;
+    SubAnalysis A;
+    A.n = n;
+    int w = or_acc ? __builtin_ctz(or_acc) : 0;
+    if (w > P.bps) w = P.bps;
+    const int sbps = P.bps - w;
+    A.wasted = w;
+    A.flags = 0;
+    A.fixed_order = 0;
+    A.lpc_order = 0;
+    A.lpc_prec = 0;
+    A.lpc_shift = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxLpc; j++) A.q[j] = 0;
+    int max_order = kMaxLpc < n ? kMaxLpc : n - 1;
+    double autoc[kMaxLpc + 1];
+    const double sc = ldexp(1.0, -2 * w);
+#pragma unroll
+    for (int l = 0; l <= kMaxLpc; l++) autoc[l] = acc[l] * sc;
+    if (n > 4 && max_order > 0 && autoc[0] != 0.0) {
+        double err[kMaxLpc];
+        const int mo = levinson_errors(autoc, max_order, err);
+        const double es = 0.5 / (double)n;
+        const int ovh = sbps + P.qlp_precision;
+        int best = 0;
+        double best_bits = (double)(unsigned)(-1);
+#pragma unroll
+        for (int i = 0; i < kMaxLpc; i++) {
+            if (i < mo) {
+                const int o = i + 1;
+                const double b = expected_bits(err[i], es) * (double)(n - o) + (double)(o * ovh);
+                if (b < best_bits) {
+                    best = i;
+                    best_bits = b;
+                }
+            }
+        }
+        const int o = best + 1;
+        double eo = err[0];
+#pragma unroll
+        for (int i = 1; i < kMaxLpc; i++)
+            if (i == best) eo = err[i];
+        const double lbits = expected_bits(eo, 0.5 / (double)(n - o));
+        if (!(lbits >= (double)sbps)) {
+            int prec = P.qlp_precision;
+            if (sbps <= 17) {
+                const int lim = 32 - sbps - ilog2_u32((uint32_t)o);
+                prec = lim < prec ? lim : prec;
+            }
+            float lp[kMaxLpc];
+            levinson_coefs(autoc, o, lp);
+            const int pm1 = prec - 1;
+            const int32_t qmax = (1 << pm1) - 1, qmin = -(1 << pm1);
+            double cmax = 0.0;
+#pragma unroll
+            for (int j = 0; j < kMaxLpc; j++)
+                if (j < o) {
+                    const double dd = fabs((double)lp[j]);
+                    if (dd > cmax) cmax = dd;
+                }
+            if (cmax > 0.0) {
+                int shift = pm1 - ilogb(cmax) - 1;
+                bool ok = true;
+                if (shift > 15) shift = 15;
+                else if (shift < -16) ok = false;
+                if (ok) {
+                    double error = 0.0;
+                    if (shift >= 0) {
+                        const float m = (float)(1 << shift);
+#pragma unroll
+                        for (int j = 0; j < kMaxLpc; j++)
+                            if (j < o) {
+                                error += (double)(lp[j] * m);
+                                int64_t qi = lround_exact(error);
+                                qi = qi > qmax ? qmax : (qi < qmin ? qmin : qi);
+                                error -= (double)qi;
+                                A.q[j] = (int32_t)qi;
+                            }
+                    } else {
+                        const float m = (float)(1 << (-shift));
+#pragma unroll
+                        for (int j = 0; j < kMaxLpc; j++)
+                            if (j < o) {
+                                error += (double)(lp[j] / m);
+                                int64_t qi = lround_exact(error);
+                                qi = qi > qmax ? qmax : (qi < qmin ? qmin : qi);
+                                error -= (double)qi;
+                                A.q[j] = (int32_t)qi;
+                            }
+                        shift = 0;
+                    }
+                    A.lpc_order = o;
+                    A.lpc_prec = prec;
+                    A.lpc_shift = shift;
+                    A.flags |= kFlagLpcOk;
+                }
+            }
+        }
+    }
+    out[f] = A;
+}
+
+// ---- wave helpers (64 lanes)
+__device__ inline uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ inline uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ inline uint32_t wave_or_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o);
+    return v;
+}
+// exclusive scan of a 64-bit per-lane value
+__device__ inline uint64_t wave_excl_scan_u64(uint64_t v, int lane) {
+    uint64_t incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(incl, d);
+        if (lane >= d) incl += y;
+    }
+    return incl - v;
+}
+
+typedef short v2s16 __attribute__((ext_vector_type(2)));
+__device__ inline int32_t dot2(uint32_t a, uint32_t b, int32_t c) {
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(v2s16, a), __builtin_bit_cast(v2s16, b), c, false);
+}
+__device__ inline uint32_t pack2(int32_t lo, int32_t hi) { return ((uint32_t)lo & 0xFFFFu) | ((uint32_t)hi << 16); }
+
+// residual of local sample index j (0..63) of this lane given even pairs E[] (E[m] = x[2m], x[2m+1]) and
+// odd pairs O[] (O[m] = x[2m-1], x[2m]), each array holding 4 history pairs from the previous lane
+// first (indices 0..3) then this lane's 32 pairs (4..35).  C[] = coefficient pairs (q1,q0),(q3,q2),...
+__device__ inline int32_t residual_at(const uint32_t *E, const uint32_t *O, const uint32_t *C, int shift, int j,
+                                      int32_t x) {
+    int32_t s = 0;
+    if ((j & 1) == 0) {
+        const int m = 4 + (j >> 1);  // E[m-1] = (x[j-2], x[j-1])
+        s = dot2(E[m - 1], C[0], s);
+        s = dot2(E[m - 2], C[1], s);
+        s = dot2(E[m - 3], C[2], s);
+        s = dot2(E[m - 4], C[3], s);
+    } else {
+        const int m = 4 + (j >> 1);  // O[m] = (x[j-2], x[j-1]) for odd j = 2m'+1
+        s = dot2(O[m], C[0], s);
+        s = dot2(O[m - 1], C[1], s);
+        s = dot2(O[m - 2], C[2], s);
+        s = dot2(O[m - 3], C[3], s);
+    }
+    return x - (s >> shift);
+}
+
+__device__ inline void lds_put_bits(uint32_t *buf, uint32_t pos, uint32_t val, int nbits) {
+    const uint32_t wi = pos >> 5;
+    const int off = (int)(pos & 31);
+    const uint64_t v = (uint64_t)val << (64 - off - nbits);
+    atomicOr(&buf[wi], (uint32_t)(v >> 32));
+    const uint32_t lo = (uint32_t)v;
+    if (lo) atomicOr(&buf[wi + 1], lo);
+}
+
+constexpr int kFrameWords = 2688;  // 86016 bits: > 4096 * 20 + headers (bound on exact Rice size)
+constexpr uint64_t kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62, kValMask = (1ull << 62) - 1;
+
+struct EncFastShared {
+    uint32_t bits[4][kFrameWords];
+    int16_t lut[kLutCap];
+    uint16_t crc[256];
+    uint8_t crc8[256];
+    int ticket;
+    int lut_tile;
+};
+
+template <int DT>
+__global__ void __launch_bounds__(256) k_encode_v2(const typename Elem<DT>::T *raster, EncodeParams P,
+                                                  const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
+                                                  const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap,
+                                                  int64_t *frame_off, uint64_t *status, int *ticket_ctr, int *err) {
+    using T = typename Elem<DT>::T;
+    __shared__ EncFastShared S;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+        S.crc[i] = c_crc16[i];
+        S.crc8[i] = c_crc8[i];
+    }
+    if (threadIdx.x == 0) S.ticket = atomicAdd(ticket_ctr, 1);
+    __syncthreads();
+    const int64_t f = (int64_t)S.ticket * 4 + wave;
+    const bool live = f < P.nframes;
+    const int64_t fq = live ? f : P.nframes - 1;
+    const int t = tile_of_frame(tiles, P.ntiles, fq);
+    const TileGeom g = tiles[t];
+    const TileNorm tn = norms[t];
+    // shared LUT when the WG's four frames share a tile
+    if (threadIdx.x == 0) {
+        const int64_t fl = min((int64_t)S.ticket * 4 + 3, P.nframes - 1);
+        const int tl = tile_of_frame(tiles, P.ntiles, fl);
+        S.lut_tile = (tl == t && tn.mode == kNormLut) ? t : -1;
+    }
+    __syncthreads();
+    if (S.lut_tile >= 0) {
+        const int64_t R = tn.imax - tn.imin;
+        const int16_t *src = luts + (int64_t)S.lut_tile * kLutCap;
+        for (int64_t d = threadIdx.x; d <= R; d += blockDim.x) S.lut[d] = src[d];
+    }
+    uint32_t *fbuf = S.bits[wave];
+    for (int i = lane; i < kFrameWords; i += 64) fbuf[i] = 0;
+    __syncthreads();
+    if (!live) return;
+    const int16_t *lut = (S.lut_tile == t) ? S.lut : luts + (int64_t)t * kLutCap;
+
+    const int64_t fk = f - g.frame_base;
+    const int64_t s0 = fk * P.blocksize;
+    const int n = (int)min((int64_t)P.blocksize, (int64_t)g.h * g.w - s0);
+    const SubAnalysis A = ana[f];
+    const int w = A.wasted;
+    const int sbps = 16 - w;
+    const T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
+
+    // ---- samples of this lane: frame indices [64*lane, 64*lane + 64), normalised, shifted, packed as
+    //      int16 pairs E[4 + m] = (x[2m], x[2m+1]); E[0..3] = the previous lane's last 8 samples
+    const int j0 = 64 * lane;
+    const int nv = max(0, min(64, n - j0));
+    uint32_t E[36], O[36];
+    {
+        Chunk64<DT> ch;
+        if (nv > 0) ch.load(base, P.row_stride, g.w, s0 + j0, P.vec_ok && (g.w % 64) == 0 && nv == 64, nv);
+#pragma unroll
+        for (int m = 0; m < 32; m++) {
+            const int32_t a = (2 * m < nv) ? (norm_fast<DT>(ch.get(2 * m), tn, lut) >> w) : 0;
+            const int32_t b = (2 * m + 1 < nv) ? (norm_fast<DT>(ch.get(2 * m + 1), tn, lut) >> w) : 0;
+            E[4 + m] = pack2(a, b);
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+        E[m] = __shfl_up(E[32 + m], 1);
+        if (lane == 0) E[m] = 0;
+    }
+    // O[m] = (x[2m-9+... ]): odd-aligned pairs, O[k] = (hi(E[k-1]), lo(E[k]))
+    O[0] = 0;
+#pragma unroll
+    for (int m = 1; m < 36; m++) O[m] = __builtin_amdgcn_perm(E[m], E[m - 1], 0x05040302u);
+    auto X = [&](int j) -> int32_t {  // sample j of this lane (compile-time j)
+        const uint32_t v = E[4 + (j >> 1)];
+        return (j & 1) ? ((int32_t)v >> 16) : (int32_t)(int16_t)(v & 0xFFFFu);
+    };
+
+    // ---- fixed predictor totals over samples 4..n-1 (FLAC__fixed_compute_best_predictor) + constant test
+    uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0, diff = 0;
+    const int32_t x0 = __shfl((int)(int16_t)(E[4] & 0xFFFFu), 0);
+    {
+        const int32_t h1 = (int32_t)E[3] >> 16, h2 = (int16_t)(E[3] & 0xFFFFu);
+        const int32_t h3 = (int32_t)E[2] >> 16, h4 = (int16_t)(E[2] & 0xFFFFu);
+        int32_t a1 = h1, d1 = h1 - h2, d2 = (h1 - h2) - (h2 - h3), d3 = ((h1 - h2) - (h2 - h3)) - ((h2 - h3) - (h3 - h4));
+#pragma unroll
+        for (int j = 0; j < 64; j++) {
+            const int32_t xi = X(j);
+            const int32_t e1 = xi - a1, e2 = e1 - d1, e3 = e2 - d2, e4 = e3 - d3;
+            if ((j0 + j >= 4) && (j < nv)) {
+                t0 += (uint32_t)abs(xi);
+                t1 += (uint32_t)abs(e1);
+                t2 += (uint32_t)abs(e2);
+                t3 += (uint32_t)abs(e3);
+                t4 += (uint32_t)abs(e4);
+            }
+            if (j < nv) diff |= (uint32_t)(xi ^ x0);
+            a1 = xi;
+            d1 = e1;
+            d2 = e2;
+            d3 = e3;
+        }
+    }
+    t0 = wave_sum_u32(t0);
+    t1 = wave_sum_u32(t1);
+    t2 = wave_sum_u32(t2);
+    t3 = wave_sum_u32(t3);
+    t4 = wave_sum_u32(t4);
+    diff = wave_or_u32(diff);
+    int guess;
+    {
+        uint32_t m = min(min(t1, t2), min(t3, t4));
+        if (t0 <= m) guess = 0;
+        else if (t1 <= min(min(t2, t3), t4)) guess = 1;
+        else if (t2 <= min(t3, t4)) guess = 2;
+        else if (t3 <= t4) guess = 3;
+        else guess = 4;
+    }
+    const double dn = (double)(n - 4);
+    const uint32_t tg = guess == 0 ? t0 : guess == 1 ? t1 : guess == 2 ? t2 : guess == 3 ? t3 : t4;
+    const float fb1 = (float)(t1 > 0 ? log(M_LN2 * (double)t1 / dn) / M_LN2 : 0.0);
+    const float fbg = (float)(tg > 0 ? log(M_LN2 * (double)tg / dn) / M_LN2 : 0.0);
+    const bool constant = n > 4 && fb1 == 0.0f && diff == 0;
+    const bool cand_fixed = n > 4 && !constant && !(fbg >= (float)sbps);
+    const bool cand_lpc = n > 4 && !constant && (A.flags & kFlagLpcOk);
+
+    // coefficient pairs
+    uint32_t CF[4], CL[4];
+    {
+        int32_t qf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (guess == 1) qf[0] = 1;
+        else if (guess == 2) { qf[0] = 2; qf[1] = -1; }
+        else if (guess == 3) { qf[0] = 3; qf[1] = -3; qf[2] = 1; }
+        else if (guess == 4) { qf[0] = 4; qf[1] = -6; qf[2] = 4; qf[3] = -1; }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            CF[k] = pack2(qf[2 * k + 1], qf[2 * k]);
+            CL[k] = pack2(A.q[2 * k + 1], A.q[2 * k]);
+        }
+    }
+    const int of = guess, ol = A.lpc_order, lshift = A.lpc_shift;
+    // ---- per-lane residual magnitude sums for both candidates (partition = 2 lanes at order 5)
+    uint64_t sf = 0, sl = 0;
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+        const int i = j0 + j;
+        if (j < nv) {
+            if (cand_fixed && i >= of) sf += (uint32_t)abs(residual_at(E, O, CF, 0, j, X(j)));
+            if (cand_lpc && i >= ol) sl += (uint32_t)abs(residual_at(E, O, CL, lshift, j, X(j)));
+        }
+    }
+    // ---- partition search (set_partitioned_rice_) for one candidate: returns bits, order, lane's k
+    const int max_po_blk = min(kMaxPartOrder, __builtin_ctz((unsigned)n));
+    const bool aligned = n == 4096;  // partitions at orders <= 5 cover whole lanes
+    auto rice = [&](uint64_t lane_sum, int order, uint32_t &best_bits, int &best_po, int &my_k) {
+        int mpo = max_po_blk;
+        while (mpo > 0 && (n >> mpo) <= order) mpo--;
+        // group sums at each order: groups of 64 >> po lanes (aligned frames)
+        uint64_t gs[6];
+        gs[5] = lane_sum + __shfl_xor(lane_sum, 1);
+        gs[4] = gs[5] + __shfl_xor(gs[5], 2);
+        gs[3] = gs[4] + __shfl_xor(gs[4], 4);
+        gs[2] = gs[3] + __shfl_xor(gs[3], 8);
+        gs[1] = gs[2] + __shfl_xor(gs[2], 16);
+        gs[0] = gs[1] + __shfl_xor(gs[1], 32);
+        best_bits = 0;
+        best_po = 0;
+        my_k = 0;
+        for (int po = mpo; po >= 0; po--) {
+            const int lanes_per = 64 >> po;
+            const int p = lane / lanes_per;
+            const uint32_t pbase = (uint32_t)(n >> po);
+            uint32_t ns = pbase, div = 0x40000u / pbase;
+            if (p == 0) {
+                ns -= (uint32_t)order;
+                div = 0x40000u / ns;
+            }
+            const uint64_t mean = gs[po];
+            uint32_t k;
+            if (mean < 2 || (((mean - 1) * div) >> 18) == 0) k = 0;
+            else k = (uint32_t)ilog2_u64(((mean - 1) * div) >> 18) + 1;
+            if (k >= 15) k = 14;
+            uint64_t pb = 4 + (uint64_t)(1 + k) * ns + (k ? (mean >> (k - 1)) : (mean << 1)) - (ns >> 1);
+            if (pb > 0xFFFFFFFFull) pb = 0xFFFFFFFFull;
+            const uint32_t contrib = (lane % lanes_per == 0) ? (uint32_t)pb : 0u;
+            const uint32_t bits = 6 + wave_sum_u32(contrib);
+            if (best_bits == 0 || bits < best_bits) {
+                best_bits = bits;
+                best_po = po;
+                my_k = (int)k;
+            }
+        }
+    };
+    uint32_t rb_f = 0, rb_l = 0;
+    int po_f = 0, po_l = 0, k_f = 0, k_l = 0;
+    if (aligned) {
+        if (cand_fixed) rice(sf, of, rb_f, po_f, k_f);
+        if (cand_lpc) rice(sl, ol, rb_l, po_l, k_l);
+    } else if (cand_fixed || cand_lpc) {
+        atomicOr(err, 4);  // partial frames go through the generic kernels (host routes them)
+    }
+    // ---- choose (process_subframe_: VERBATIM, then CONSTANT | FIXED, LPC; strict <)
+    uint32_t best = (uint32_t)(1 + 6 + 1 + w + n * sbps);
+    int type = 1;
+    if (n > 4) {
+        if (constant) {
+            const uint32_t cb = (uint32_t)(1 + 6 + 1 + w + sbps);
+            if (cb < best) { best = cb; type = 0; }
+        } else {
+            if (cand_fixed) {
+                uint32_t est = (uint32_t)(1 + 6 + 1 + w + of * sbps);
+                est = (rb_f < 0xFFFFFFFFu - est) ? est + rb_f : 0xFFFFFFFFu;
+                if (est < best) { best = est; type = 2; }
+            }
+            if (cand_lpc) {
+                uint32_t est = (uint32_t)(1 + 6 + 1 + w + 4 + 5 + sbps * ol + A.lpc_prec * ol);
+                est = (rb_l < 0xFFFFFFFFu - est) ? est + rb_l : 0xFFFFFFFFu;
+                if (est != 0 && est < best) { best = est; type = 3; }
+            }
+        }
+    }
+    // ---- frame header (lane 0)
+    uint32_t hdr_bits = 0;
+    if (lane == 0) {
+        uint8_t h[16];
+        int hb = 0;
+        int bsc = 0, bsx = 0;
+        switch (n) {
+        case 192: bsc = 1; break;
+        case 576: bsc = 2; break;
+        case 1152: bsc = 3; break;
+        case 2304: bsc = 4; break;
+        case 4608: bsc = 5; break;
+        case 256: bsc = 8; break;
+        case 512: bsc = 9; break;
+        case 1024: bsc = 10; break;
+        case 2048: bsc = 11; break;
+        case 4096: bsc = 12; break;
+        default: bsc = bsx = (n <= 256 ? 6 : 7); break;
+        }
+        const int sr = P.sample_rate;
+        int src, srx = 0;
+        switch (sr) {
+        case 88200: src = 1; break;
+        case 176400: src = 2; break;
+        case 192000: src = 3; break;
+        case 8000: src = 4; break;
+        case 16000: src = 5; break;
+        case 22050: src = 6; break;
+        case 24000: src = 7; break;
+        case 32000: src = 8; break;
+        case 44100: src = 9; break;
+        case 48000: src = 10; break;
+        case 96000: src = 11; break;
+        default:
+            if (sr <= 255000 && sr % 1000 == 0) src = srx = 12;
+            else if (sr % 10 == 0 && sr / 10 <= 65535) src = srx = 14;
+            else src = srx = 13;
+        }
+        h[hb++] = 0xFF;
+        h[hb++] = 0xF8;
+        h[hb++] = (uint8_t)((bsc << 4) | src);
+        h[hb++] = (uint8_t)((0 << 4) | (4 << 1));  // mono, 16 bits
+        const uint32_t v = (uint32_t)fk;
+        if (v < 0x80) h[hb++] = (uint8_t)v;
+        else if (v < 0x800) { h[hb++] = (uint8_t)(0xC0 | (v >> 6)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+        else if (v < 0x10000) { h[hb++] = (uint8_t)(0xE0 | (v >> 12)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+        else { h[hb++] = (uint8_t)(0xF0 | (v >> 18)); h[hb++] = (uint8_t)(0x80 | ((v >> 12) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+        if (bsx == 6) h[hb++] = (uint8_t)(n - 1);
+        else if (bsx == 7) { h[hb++] = (uint8_t)((n - 1) >> 8); h[hb++] = (uint8_t)(n - 1); }
+        if (srx == 12) h[hb++] = (uint8_t)(sr / 1000);
+        else if (srx == 13) { h[hb++] = (uint8_t)(sr >> 8); h[hb++] = (uint8_t)sr; }
+        else if (srx == 14) { h[hb++] = (uint8_t)((sr / 10) >> 8); h[hb++] = (uint8_t)(sr / 10); }
+        uint8_t c = 0;
+        for (int i = 0; i < hb; i++) c = S.crc8[c ^ h[i]];
+        h[hb++] = c;
+        for (int i = 0; i < hb; i++) lds_put_bits(fbuf, (uint32_t)(i * 8), h[i], 8);
+        hdr_bits = (uint32_t)(hb * 8);
+        // subframe header: 0, type(6), wasted flag, unary wasted
+        const int typecode = type == 0 ? 0 : type == 1 ? 1 : type == 2 ? 8 + of : 32 + ol - 1;
+        lds_put_bits(fbuf, hdr_bits, (uint32_t)(typecode << 1) | (w ? 1u : 0u), 8);
+        if (w) lds_put_bits(fbuf, hdr_bits + 8 + (uint32_t)(w - 1), 1, 1);
+    }
+    hdr_bits = (uint32_t)__shfl((int)hdr_bits, 0);
+    uint32_t pos = hdr_bits + 8 + (uint32_t)w;  // after the subframe header
+    uint32_t end_bits;
+    if (type == 0) {
+        if (lane == 0) lds_put_bits(fbuf, pos, (uint32_t)X(0) & ((1u << sbps) - 1u), sbps);
+        end_bits = pos + (uint32_t)sbps;
+    } else if (type == 1) {
+#pragma unroll
+        for (int j = 0; j < 64; j++)
+            if (j < nv) lds_put_bits(fbuf, pos + (uint32_t)(j0 + j) * sbps, (uint32_t)X(j) & ((1u << sbps) - 1u), sbps);
+        end_bits = pos + (uint32_t)n * sbps;
+    } else {
+        const int o = type == 2 ? of : ol;
+        const uint32_t *C = type == 2 ? CF : CL;
+        const int shift = type == 2 ? 0 : lshift;
+        const int po = type == 2 ? po_f : po_l;
+        const int k = type == 2 ? k_f : k_l;
+        const int lanes_per = 64 >> po;
+        const int p = lane / lanes_per;
+        // warm-up samples (lane 0 holds samples 0..63, o <= 8)
+        if (lane == 0) {
+#pragma unroll
+            for (int i = 0; i < kMaxLpc; i++)
+                if (i < o) lds_put_bits(fbuf, pos + (uint32_t)i * sbps, (uint32_t)X(i) & ((1u << sbps) - 1u), sbps);
+        }
+        pos += (uint32_t)o * sbps;
+        if (type == 3) {
+            if (lane == 0) {
+                lds_put_bits(fbuf, pos, (uint32_t)(A.lpc_prec - 1), 4);
+                lds_put_bits(fbuf, pos + 4, (uint32_t)lshift & 31u, 5);
+                for (int i = 0; i < o; i++)
+                    lds_put_bits(fbuf, pos + 9 + (uint32_t)i * A.lpc_prec, (uint32_t)A.q[i] & ((1u << A.lpc_prec) - 1u), A.lpc_prec);
+            }
+            pos += 9 + (uint32_t)o * A.lpc_prec;
+        }
+        if (lane == 0) lds_put_bits(fbuf, pos, (uint32_t)po, 6);  // method RICE (00) + order (4 bits)
+        pos += 6;
+        // exact code lengths
+        uint32_t lens = 0;
+#pragma unroll
+        for (int j = 0; j < 64; j++) {
+            const int i = j0 + j;
+            if (j < nv && i >= o) {
+                const int32_t r = residual_at(E, O, C, shift, j, X(j));
+                const uint32_t u = ((uint32_t)r << 1) ^ (uint32_t)(r >> 31);
+                lens += 1u + (uint32_t)k + (u >> k);
+            }
+        }
+        const uint64_t excl = wave_excl_scan_u64(lens, lane);
+        const uint64_t total = (uint64_t)__shfl((long long)(excl + lens), 63);
+        const uint64_t fin = (uint64_t)pos + 4ull * (uint64_t)(1 << po) + total;
+        if (fin + 64 > (uint64_t)kFrameWords * 32) {
+            if (lane == 0) atomicOr(err, 2);
+            return;
+        }
+        // parameter field of the partition starting at this lane
+        if (lane % lanes_per == 0) lds_put_bits(fbuf, pos + 4u * (uint32_t)p + (uint32_t)excl, (uint32_t)k, 4);
+        uint32_t run = pos + 4u * (uint32_t)(p + 1) + (uint32_t)excl;
+#pragma unroll
+        for (int j = 0; j < 64; j++) {
+            const int i = j0 + j;
+            if (j < nv && i >= o) {
+                const int32_t r = residual_at(E, O, C, shift, j, X(j));
+                const uint32_t u = ((uint32_t)r << 1) ^ (uint32_t)(r >> 31);
+                const uint32_t q = u >> k;
+                lds_put_bits(fbuf, run + q, (1u << k) | (u & ((1u << k) - 1u)), k + 1);
+                run += q + 1 + (uint32_t)k;
+            }
+        }
+        end_bits = (uint32_t)fin;
+    }
+    const uint32_t body = (end_bits + 7) >> 3;  // bytes before the CRC-16 footer
+    const uint64_t fbytes = (uint64_t)body + 2;
+    // ---- publish our aggregate, compute CRC-16 while predecessors resolve
+    if (lane == 0) {
+        const uint64_t v = (f == 0 ? kFlagIncl : kFlagAgg) | fbytes;
+        __hip_atomic_store(&status[f], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // wave-level LDS visibility of the atomics above: all lanes' ds ops complete in order per wave
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    uint32_t crc = 0;
+    {
+        const uint32_t ch = (body + 63) / 64;
+        const uint32_t b0 = min(body, (uint32_t)lane * ch), b1 = min(body, b0 + ch);
+        for (uint32_t b = b0; b < b1; b++) {
+            const uint8_t byte = (uint8_t)(fbuf[b >> 2] >> (24 - 8 * (b & 3)));
+            crc = ((crc << 8) & 0xFFFFu) ^ S.crc[((crc >> 8) ^ byte) & 0xFF];
+        }
+        if (b1 > b0 && b1 < body) crc = gf_mulmod(crc, xpow8((uint64_t)(body - b1)));
+#pragma unroll
+        for (int o2 = 32; o2 > 0; o2 >>= 1) crc ^= __shfl_xor(crc, o2);
+    }
+    // ---- decoupled look-back for the exclusive prefix
+    uint64_t prefix = 0;
+    if (lane == 0 && f > 0) {
+        int64_t j = f - 1;
+        uint64_t accum = 0;
+        long spins = 0;
+        while (true) {
+            uint64_t sv = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((sv >> 62) == 0) {
+                if (++spins > (1l << 26)) {  // bounded: never hang the device
+                    atomicOr(err, 8);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            accum += sv & kValMask;
+            if ((sv >> 62) == 2) break;
+            j--;
+        }
+        prefix = accum;
+        __hip_atomic_store(&status[f], kFlagIncl | (prefix + fbytes), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        frame_off[f] = (int64_t)prefix;
+    } else if (lane == 0) {
+        frame_off[f] = 0;
+    }
+    prefix = (uint64_t)__shfl((long long)prefix, 0);
+    // ---- store: body bytes from LDS then the CRC, at arena[prefix ..)
+    if ((int64_t)(prefix + fbytes) > arena_cap) {
+        if (lane == 0) atomicOr(err, 16);
+        return;
+    }
+    uint8_t *dst = arena + prefix;
+    const uint64_t total_b = fbytes;
+    auto byte_at = [&](uint64_t b) -> uint32_t {
+        if (b < body) return (fbuf[b >> 2] >> (24 - 8 * (b & 3))) & 0xFFu;
+        return b == body ? (crc >> 8) & 0xFFu : crc & 0xFFu;
+    };
+    // aligned 4-byte words of the destination fully inside the frame
+    const uint64_t a0 = (4 - (prefix & 3)) & 3;  // leading unaligned bytes
+    for (uint64_t b = (uint64_t)lane; b < min(a0, total_b); b += 64) dst[b] = (uint8_t)byte_at(b);
+    const uint64_t nwords = (total_b > a0) ? (total_b - a0) / 4 : 0;
+    uint32_t *dw = reinterpret_cast<uint32_t *>(dst + a0);
+    for (uint64_t wi = (uint64_t)lane; wi < nwords; wi += 64) {
+        const uint64_t b = a0 + wi * 4;
+        const uint32_t v = byte_at(b) | (byte_at(b + 1) << 8) | (byte_at(b + 2) << 16) | (byte_at(b + 3) << 24);
+        dw[wi] = v;
+    }
+    for (uint64_t b = a0 + nwords * 4 + (uint64_t)lane; b < total_b; b += 64) dst[b] = (uint8_t)byte_at(b);
+}
+
+__global__ void k_fast_finish(const int64_t *frame_off, const uint64_t *status, const TileGeom *tiles, int ntiles,
+                              int64_t nframes, int64_t *tile_off) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < ntiles) tile_off[t] = frame_off[tiles[t].frame_base];
+    if (t == ntiles) tile_off[t] = (int64_t)(status[nframes - 1] & kValMask);
+}
+
 // ------------------------------------------------------------------------------------- host side
 static bool g_tables_ready[64];
 
@@ -1218,6 +2013,8 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     P.nframes = nframes;
     P.ntiles = ntiles;
     P.norm_mode = d->norm_mode;
+    P.vec_ok = 0;
+    P.pad2 = 0;
 
     int rc = upload_tables(ctx);
     if (rc) return rc;
@@ -1225,7 +2022,6 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     FRS_HIP(ctx->tiles.ensure(sizeof(TileGeom) * ntiles));
     FRS_HIP(ctx->norms.ensure(sizeof(TileNorm) * ntiles));
     FRS_HIP(ctx->analysis.ensure(sizeof(SubAnalysis) * nframes * P.nch));
-    FRS_HIP(ctx->slots.ensure((size_t)nframes * P.slot_words * 4));
     FRS_HIP(ctx->frame_bytes.ensure(sizeof(int64_t) * (nframes + 1) + 64));
     FRS_HIP(ctx->frame_off.ensure(sizeof(int64_t) * (nframes + 1)));
     FRS_HIP(ctx->tile_sizes.ensure(sizeof(int64_t) * (ntiles + 1) + 64));
@@ -1265,8 +2061,57 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         dim3 grid(splits, ntiles);
         k_tile_stats<DT><<<grid, 256, 0, st>>>(raster, P, dtiles, dnorms, splits);
     }
-    k_tile_finalize<DT><<<(ntiles + 255) / 256, 256, 0, st>>>(dnorms, ntiles);
+    k_tile_finalize<DT><<<(ntiles + 255) / 256, 256, 0, st>>>(dnorms, ntiles, P.norm_mode, P.scale_bits);
     prof_end(ctx, "stats", ev);
+    // fast path: mono 16-bit streams whose frames are all full 4096-sample blocks
+    bool all_full = true;
+    for (const TileGeom &tg : tiles) all_full = all_full && (((int64_t)tg.h * tg.w) % d->blocksize == 0);
+    const bool fast = !ctx->force_generic && P.bps == 16 && P.nch == 1 && P.norm_mode == 0 && d->blocksize == 4096 &&
+                      all_full && !Elem<DT>::is_float;
+    if constexpr (!Elem<DT>::is_float) if (fast) {
+        const int es = (int)sizeof(T);
+        P.vec_ok = ((d->row_stride * es) % 16 == 0) && (d->tile_w % 64 == 0) &&
+                   ((reinterpret_cast<uintptr_t>(raster_dev) + (size_t)d->band0 * d->band_stride * es) % 16 == 0);
+        FRS_HIP(ctx->luts.ensure(sizeof(int16_t) * (size_t)kLutCap * ntiles));
+        FRS_HIP(ctx->status.ensure(sizeof(uint64_t) * (nframes + 1) + 64));
+        k_build_lut<DT><<<ntiles, 256, 0, st>>>(dnorms, ctx->luts.as<int16_t>());
+        prof_begin(ctx, "analyze", &ev);
+        k_analyze_v2<DT><<<(unsigned)((nframes + 255) / 256), 256, 0, st>>>(raster, P, dtiles, dnorms,
+                                                                             ctx->luts.as<int16_t>(),
+                                                                             ctx->window.as<float>(), dana);
+        prof_end(ctx, "analyze", ev);
+        uint64_t *dstatus = ctx->status.as<uint64_t>();
+        int *ticket = reinterpret_cast<int *>(dstatus + nframes);
+        FRS_HIP(hipMemsetAsync(dstatus, 0, sizeof(uint64_t) * (nframes + 1), st));
+        prof_begin(ctx, "encode", &ev);
+        k_encode_v2<DT><<<(unsigned)((nframes + 3) / 4), 256, 0, st>>>(
+            raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(), dana, reinterpret_cast<uint8_t *>(arena_dev), arena_cap,
+            ctx->frame_off.as<int64_t>(), dstatus, ticket, err_flag);
+        prof_end(ctx, "encode", ev);
+        k_fast_finish<<<(ntiles + 1 + 255) / 256, 256, 0, st>>>(ctx->frame_off.as<int64_t>(), dstatus, dtiles, ntiles,
+                                                               nframes, ctx->tile_sizes.as<int64_t>());
+        std::vector<TileNorm> hn(ntiles);
+        int errv = 0;
+        FRS_HIP(hipMemcpyAsync(tile_off, ctx->tile_sizes.ptr, sizeof(int64_t) * (ntiles + 1), hipMemcpyDeviceToHost, st));
+        FRS_HIP(hipMemcpyAsync(hn.data(), dnorms, sizeof(TileNorm) * ntiles, hipMemcpyDeviceToHost, st));
+        FRS_HIP(hipMemcpyAsync(&errv, err_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+        FRS_HIP(hipStreamSynchronize(st));
+        prof_collect(ctx);
+        for (int t = 0; t < ntiles; t++) {
+            tile_min[t] = hn[t].dmin;
+            tile_max[t] = hn[t].dmax;
+        }
+        if (errv & 16) {
+            ctx->err = "arena too small";
+            return FRS_E_NOSPACE;
+        }
+        if (errv) {
+            ctx->err = "fast encode failed, flags " + std::to_string(errv);
+            return FRS_E_UNSUPPORTED;
+        }
+        return FRS_OK;
+    }
+    FRS_HIP(ctx->slots.ensure((size_t)nframes * P.slot_words * 4));
     // 2. analysis
     const int64_t nsub = nframes * P.nch;
     prof_begin(ctx, "analyze", &ev);

@@ -43,7 +43,8 @@ struct frs_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     // encode scratch
-    DevBuf tiles, norms, analysis, slots, frame_bytes, frame_off, scan_tmp, window, tile_sizes;
+    DevBuf tiles, norms, analysis, slots, frame_bytes, frame_off, scan_tmp, window, tile_sizes, luts, status;
+    bool force_generic = false;  // testing: route every job through the generic kernels
     // host staging (pinned)
     DevBuf raster_stage, arena_stage;  // device copies for the host-pointer entry points
     // decode scratch

@@ -109,3 +109,24 @@ def test_decode_roundtrip_and_denormalize(gpu_ctx, golden):
     assert np.array_equal(out, O.denormalize_i16(pcm, 1.0, 255.0, np.uint8))
     # lossless for uint8: back to the TIFF pixels
     assert np.array_equal(out.reshape(256, 256, 3).transpose(2, 0, 1), r.data)
+
+
+@pytest.mark.parametrize("dtype,lo,hi,shape,tile", [
+    (np.int16, 900, 1800, (1024, 1536), 512),     # LUT normalisation (range < 4096)
+    (np.uint16, 0, 40000, (512, 512), 256),       # exact reciprocal division (range 4096..65535)
+    (np.int16, -30000, 30000, (512, 512), 512),   # wrapping int16 range (slow exact path)
+    (np.uint8, 0, 255, (384, 640), 128),
+    (np.uint16, 5, 6, (256, 256), 64),            # near-constant tiles: wasted bits / constant subframes
+])
+def test_fast_path_matches_oracle(gpu_ctx, dtype, lo, hi, shape, tile):
+    rng = np.random.default_rng(hash((lo, hi)) % 1000)
+    H, W = shape
+    y, x = np.meshgrid(np.linspace(0, 1, H), np.linspace(0, 1, W), indexing="ij")
+    smooth = lo + (hi - lo) * (0.5 + 0.45 * np.sin(6 * x) * np.cos(4 * y))
+    band = np.clip(smooth + rng.normal(0, (hi - lo) * 0.01 + 0.3, (H, W)), lo, hi).astype(dtype)
+    band[:tile // 2, :tile // 2] = band[0, 0]        # a constant quarter tile
+    arena, off, mn, mx, bps = _gpu_tiles(gpu_ctx, band, tile)
+    o_arena, o_off, o_mn, o_mx = O.encode_tiles(band, tile)
+    assert list(off) == list(o_off)
+    assert arena.tobytes() == o_arena.tobytes()
+    assert list(mn) == list(o_mn) and list(mx) == list(o_mx)
