@@ -96,10 +96,15 @@ int frs_ctx_create(int device, frs_ctx **out) {
     ctx->device = device;
     const char *fg = getenv("FRS_FORCE_GENERIC");
     ctx->force_generic = fg && fg[0] == '1';
+    const char *ab = getenv("FRS_ABLATE");
+    ctx->ablate = ab ? atoi(ab) : 0;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return FRS_E_HIP;
     }
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+        ctx->num_cus = cus;
     *out = ctx;
     return FRS_OK;
 }

@@ -149,6 +149,76 @@ __global__ void __launch_bounds__(256) k_tile_stats(const typename Elem<DT>::T *
     }
 }
 
+// vectorised min/max for 8/16-bit integer rasters whose tile rows are 16-byte aligned runs: 16-B loads,
+// packed 16-bit min/max (v_pk_min_i16 / v_pk_min_u16), 4 loads in flight per thread
+typedef short v2i16 __attribute__((ext_vector_type(2)));
+typedef unsigned short v2u16 __attribute__((ext_vector_type(2)));
+template <int DT>
+__global__ void __launch_bounds__(256) k_tile_stats_vec(const typename Elem<DT>::T *raster, EncodeParams P,
+                                                       const TileGeom *tiles, TileNorm *norms, int splits) {
+    using T = typename Elem<DT>::T;
+    static_assert(sizeof(T) <= 2, "16-bit or narrower");
+    const int t = blockIdx.y;
+    const TileGeom g = tiles[t];
+    const int nvec = (int)((int64_t)g.w * sizeof(T) / 16);  // 16-B vectors per row
+    const int64_t rows = (int64_t)g.h * P.nch;
+    const int64_t r0 = rows * blockIdx.x / splits, r1 = rows * (blockIdx.x + 1) / splits;
+    const int64_t total = (r1 - r0) * nvec;
+    // packed accumulators: (lo, hi) halves; u8 values are widened into u16 lanes
+    using V = std::conditional_t<std::is_signed_v<T>, v2i16, v2u16>;
+    using E16 = std::conditional_t<std::is_signed_v<T>, short, unsigned short>;
+    V vmin = (V)(std::is_signed_v<T> ? (E16)32767 : (E16)65535), vmax = (V)(std::is_signed_v<T> ? (E16)-32768 : (E16)0);
+    auto fold = [&](uint32_t w) {
+        if constexpr (sizeof(T) == 2) {
+            const V v = __builtin_bit_cast(V, w);
+            vmin = __builtin_elementwise_min(vmin, v);
+            vmax = __builtin_elementwise_max(vmax, v);
+        } else {
+            const V a = __builtin_bit_cast(V, w & 0x00FF00FFu), b = __builtin_bit_cast(V, (w >> 8) & 0x00FF00FFu);
+            vmin = __builtin_elementwise_min(vmin, __builtin_elementwise_min(a, b));
+            vmax = __builtin_elementwise_max(vmax, __builtin_elementwise_max(a, b));
+        }
+    };
+    auto addr = [&](int64_t idx) -> const uint4 * {
+        const int64_t rr = r0 + idx / nvec;
+        const int v = (int)(idx - (idx / nvec) * nvec);
+        const int ch = (int)(rr / g.h);
+        const int64_t r = rr - (int64_t)ch * g.h;
+        return reinterpret_cast<const uint4 *>(raster + (int64_t)(P.band0 + ch) * P.band_stride +
+                                               (g.r0 + r) * P.row_stride + g.c0) + v;
+    };
+    int64_t idx = threadIdx.x;
+    for (; idx + 3 * 256 < total; idx += 4 * 256) {
+        uint4 q[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) q[u] = *addr(idx + u * 256);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            fold(q[u].x);
+            fold(q[u].y);
+            fold(q[u].z);
+            fold(q[u].w);
+        }
+    }
+    for (; idx < total; idx += 256) {
+        const uint4 q = *addr(idx);
+        fold(q.x);
+        fold(q.y);
+        fold(q.z);
+        fold(q.w);
+    }
+    int32_t lo = min((int32_t)vmin.x, (int32_t)vmin.y), hi = max((int32_t)vmax.x, (int32_t)vmax.y);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, __shfl_xor(lo, o));
+        hi = max(hi, __shfl_xor(hi, o));
+    }
+    if ((threadIdx.x & 63) == 0 && total > 0) {
+        atomicMin((long long *)&norms[t].imin, (long long)lo);
+        atomicMax((long long *)&norms[t].imax, (long long)hi);
+    }
+}
+
 template <int DT> __global__ void k_tile_finalize(TileNorm *norms, int ntiles, int norm_mode, int scale_bits) {
     int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntiles) return;
@@ -1100,10 +1170,10 @@ __global__ void k_gather_tile_off(const int64_t *frame_off, const TileGeom *tile
 //   k_build_lut     per tile: pcm = lut[x - min] for x - min in [0, R] (exact double path, once per value)
 //   k_analyze_v2    lane = frame; 64-sample chunks loaded as 8 x 16 B per lane (no L1 reuse needed),
 //                   LUT normalisation, wave-uniform window from LDS, 9 fp64 FMA chains per lane
-//   k_encode_v2     wave = frame, 64 consecutive samples per lane held in registers: fixed totals,
-//                   v_dot2 residuals, partition sums by lane-pair shuffles, Rice search, exact bit
-//                   positions by one wave scan, LDS bit packing, CRC-16, single-pass decoupled
-//                   look-back for the frame's arena offset, byte-exact store at that offset
+//   k_encode_v3     persistent WGs, wave = frame, 64 consecutive samples per lane held as packed int16
+//                   pairs: fixed totals, v_dot2 residuals, partition sums by lane shuffles, Rice search,
+//                   exact bit positions by one wave scan, size published before LDS bit packing,
+//                   slice-by-4 CRC-16, decoupled look-back for the arena offset, 16-B aligned stores
 // =================================================================================================
 
 // exact converter.py normalisation of one element for the fast kernels (mode per tile)
@@ -1135,6 +1205,45 @@ __device__ inline int32_t norm_fast(typename Elem<DT>::T x, const TileNorm &tn, 
     }
 }
 
+// normalise 64 elements of a chunk into int32 (mode is wave-uniform in the callers' common case; the
+// switch sits outside the unrolled element loop so the loop body is branch-free)
+template <int DT> struct Chunk64;
+
+// normalise the 64 elements of a chunk (mode is wave-uniform in the encode kernel; the switch sits
+// outside the unrolled element loop so the loop body is branch-free).  emit(j, x) in order j = 0..63.
+template <int DT, typename Fn>
+__device__ inline void norm_chunk(const Chunk64<DT> &ch, const TileNorm &tn, const int16_t *lut, Fn &&emit) {
+    switch (tn.mode) {
+    case kNormLut: {
+        const int32_t mn = (int32_t)tn.imin;
+#pragma unroll
+        for (int j = 0; j < 64; j++) emit(j, (int32_t)lut[(int32_t)ch.get(j) - mn]);
+        break;
+    }
+    case kNormZero:
+#pragma unroll
+        for (int j = 0; j < 64; j++) emit(j, 0);
+        break;
+    case kNormFastDiv: {
+        const int32_t mn = (int32_t)tn.imin;
+        const double rinv = tn.rinv, den = tn.den;
+#pragma unroll
+        for (int j = 0; j < 64; j++) {
+            const double a = (double)(2 * ((int32_t)ch.get(j) - mn));
+            const double q0 = a * rinv;
+            const double r = fma(-q0, den, a);
+            const double q1 = fma(r, rinv, q0);
+            emit(j, (int32_t)(int16_t)(int32_t)((q1 - 1.0) * 32767.0));
+        }
+        break;
+    }
+    default:
+#pragma unroll
+        for (int j = 0; j < 64; j++) emit(j, norm_fast<DT>(ch.get(j), tn, lut));
+        break;
+    }
+}
+
 template <int DT>
 __global__ void __launch_bounds__(256) k_build_lut(const TileNorm *norms, int16_t *luts) {
     const int t = blockIdx.x;
@@ -1155,6 +1264,10 @@ template <int DT> struct Chunk64 {
     using T = typename Elem<DT>::T;
     static constexpr int kWords = (int)(64 * sizeof(T) / 4);
     uint32_t w[kWords];
+    __device__ inline void unpack(T *out) const {
+#pragma unroll
+        for (int j = 0; j < 64; j++) out[j] = get(j);
+    }
     __device__ inline T get(int j) const {  // j must be a compile-time constant after unrolling
         if constexpr (sizeof(T) == 1) return (T)((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
         else if constexpr (sizeof(T) == 2) return (T)((w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
@@ -1213,9 +1326,10 @@ __global__ void __launch_bounds__(256) k_analyze_v2(const typename Elem<DT>::T *
     for (int i = threadIdx.x; i < P.blocksize; i += blockDim.x) swin[i] = window[i];
     const int64_t f = ((int64_t)blockIdx.x * 4 + wave) * 64 + lane;
     const bool live = f < P.nframes;
-    const int t = tile_of_frame(tiles, P.ntiles, live ? f : P.nframes - 1);
+    const int64_t fq = live ? f : P.nframes - 1;  // dead lanes re-read the last frame (no out-of-tile loads)
+    const int t = tile_of_frame(tiles, P.ntiles, fq);
     const TileGeom g = tiles[t];
-    const int64_t s0 = (f - g.frame_base) * P.blocksize;
+    const int64_t s0 = (fq - g.frame_base) * P.blocksize;
     const int64_t tile_px = (int64_t)g.h * g.w;
     const int n = live ? (int)min((int64_t)P.blocksize, tile_px - s0) : 0;
     TileNorm tn = norms[t];
@@ -1241,22 +1355,23 @@ __global__ void __launch_bounds__(256) k_analyze_v2(const typename Elem<DT>::T *
 #pragma unroll
     for (int j = 0; j < 8; j++) prev[j] = 0.0;
 
-    for (int c = 0; c < P.blocksize / 64; c++) {
+    // fast path: every frame is a full block (host guarantees), 64 chunks of 64 samples per lane
+    for (int c = 0; c < kMaxBlock / 64; c++) {
         const int i0 = c * 64;
-        Chunk64<DT> ch;
-        const int nv = min(64, n - i0);
-        if (nv > 0) ch.load(base, P.row_stride, g.w, s0 + i0, vec && nv == 64, nv);
+        float xf[64];
+        {
+            Chunk64<DT> ch;
+            ch.load(base, P.row_stride, g.w, s0 + i0, vec, 64);
+            norm_chunk<DT>(ch, tn, lut, [&](int j, int32_t x) {
+                or_acc |= (uint32_t)x;
+                xf[j] = (float)x;
+            });
+        }
 #pragma unroll
         for (int b = 0; b < 8; b++) {
             double cur[8];
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
-                const int jj = b * 8 + j;
-                int32_t x = 0;
-                if (jj < nv) x = norm_fast<DT>(ch.get(jj), tn, lut);
-                or_acc |= (uint32_t)x;
-                cur[j] = (double)((float)x * swin[i0 + jj]);
-            }
+            for (int j = 0; j < 8; j++) cur[j] = (double)(xf[b * 8 + j] * swin[i0 + b * 8 + j]);
 #pragma unroll
             for (int j = 0; j < 8; j++) {
 #pragma unroll
@@ -1407,21 +1522,22 @@ __device__ inline uint32_t pack2(int32_t lo, int32_t hi) { return ((uint32_t)lo 
 // residual of local sample index j (0..63) of this lane given even pairs E[] (E[m] = x[2m], x[2m+1]) and
 // odd pairs O[] (O[m] = x[2m-1], x[2m]), each array holding 4 history pairs from the previous lane
 // first (indices 0..3) then this lane's 32 pairs (4..35).  C[] = coefficient pairs (q1,q0),(q3,q2),...
-__device__ inline int32_t residual_at(const uint32_t *E, const uint32_t *O, const uint32_t *C, int shift, int j,
-                                      int32_t x) {
+// residual of local sample index j (0..63, compile-time) of this lane given the even pairs E[] (E[0..3]:
+// the previous lane's last 8 samples, E[4 + m] = (x[2m], x[2m+1])).  C[] = (q1,q0),(q3,q2),(q5,q4),(q7,q6).
+// Odd j uses odd-aligned pairs (x[j-2], x[j-1]) = perm(E[m], E[m-1]).
+__device__ inline int32_t residual_at(const uint32_t *E, const uint32_t *C, int shift, int j, int32_t x) {
     int32_t s = 0;
+    const int m = 4 + (j >> 1);
     if ((j & 1) == 0) {
-        const int m = 4 + (j >> 1);  // E[m-1] = (x[j-2], x[j-1])
         s = dot2(E[m - 1], C[0], s);
         s = dot2(E[m - 2], C[1], s);
         s = dot2(E[m - 3], C[2], s);
         s = dot2(E[m - 4], C[3], s);
     } else {
-        const int m = 4 + (j >> 1);  // O[m] = (x[j-2], x[j-1]) for odd j = 2m'+1
-        s = dot2(O[m], C[0], s);
-        s = dot2(O[m - 1], C[1], s);
-        s = dot2(O[m - 2], C[2], s);
-        s = dot2(O[m - 3], C[3], s);
+        s = dot2(__builtin_amdgcn_perm(E[m], E[m - 1], 0x05040302u), C[0], s);
+        s = dot2(__builtin_amdgcn_perm(E[m - 1], E[m - 2], 0x05040302u), C[1], s);
+        s = dot2(__builtin_amdgcn_perm(E[m - 2], E[m - 3], 0x05040302u), C[2], s);
+        s = dot2(__builtin_amdgcn_perm(E[m - 3], E[m - 4], 0x05040302u), C[3], s);
     }
     return x - (s >> shift);
 }
@@ -1435,95 +1551,93 @@ __device__ inline void lds_put_bits(uint32_t *buf, uint32_t pos, uint32_t val, i
     if (lo) atomicOr(&buf[wi + 1], lo);
 }
 
-constexpr int kFrameWords = 2688;  // 86016 bits: > 4096 * 20 + headers (bound on exact Rice size)
 constexpr uint64_t kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62, kValMask = (1ull << 62) - 1;
 
-struct EncFastShared {
-    uint32_t bits[4][kFrameWords];
+// ------------------------------------------------------------------------------ k_encode_v3
+// Persistent work-groups of 4 waves; a WG takes a ticket of 4 consecutive frames (wave = frame), so
+// tickets are handed out in frame order and every look-back waits only on frames already owned by
+// resident waves.  Frames on this path are always full 4096-sample blocks (host guarantees), so no
+// per-sample validity predicates exist: only lane 0's first `order` (<= 8) samples are masked, by
+// selects.  LPC residuals stay in registers between the partition-sum, code-length and packing passes;
+// the fixed candidate's partition sums fall out of the fixed-predictor totals pass.
+constexpr int kFrameWordsV3 = 2176;  // 69632 bits >= worst exact frame (estimate < verbatim)
+constexpr int kXpowBytes = kFrameWordsV3 * 4 + 16;
+__constant__ uint16_t c_crc16x4[4][256];           // T_k[v] = CRC-16 of byte v followed by k zero bytes
+__device__ uint16_t g_xpow_bytes[kXpowBytes];      // x^(8m) mod P for m bytes
+
+struct EncV3Shared {
+    uint32_t bits[4][kFrameWordsV3];
     int16_t lut[kLutCap];
-    uint16_t crc[256];
+    uint16_t crc4[4][256];
     uint8_t crc8[256];
     int ticket;
+    int want;
     int lut_tile;
 };
 
+// bit writer without branches: the (up to 32-bit) code at [pos, pos + nbits) straddles at most 2 words
+__device__ inline void lds_put_bits2(uint32_t *buf, uint32_t pos, uint32_t val, int nbits) {
+    const uint32_t wi = pos >> 5;
+    const uint64_t v = (uint64_t)val << (64 - (int)(pos & 31) - nbits);
+    atomicOr(&buf[wi], (uint32_t)(v >> 32));
+    atomicOr(&buf[wi + 1], (uint32_t)v);
+}
+
+// opaque register barrier: stops the compiler from carrying 64 residuals across passes (CSE) and
+// instead recomputes them from the 36 packed pairs
+__device__ inline void reg_fence(uint32_t *E) {
+#pragma unroll
+    for (int m = 0; m < 36; m++) asm volatile("" : "+v"(E[m]));
+}
+
+__device__ inline uint32_t zigzag(int32_t r) { return ((uint32_t)r << 1) ^ (uint32_t)(r >> 31); }
+
 template <int DT>
-__global__ void __launch_bounds__(256) k_encode_v2(const typename Elem<DT>::T *raster, EncodeParams P,
-                                                  const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
-                                                  const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap,
-                                                  int64_t *frame_off, uint64_t *status, int *ticket_ctr, int *err) {
+__device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const EncodeParams &P,
+                                       const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
+                                       const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap, int64_t *frame_off,
+                                       uint64_t *status, int *err, EncV3Shared &S, int want, int64_t f, int lane) {
     using T = typename Elem<DT>::T;
-    __shared__ EncFastShared S;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-        S.crc[i] = c_crc16[i];
-        S.crc8[i] = c_crc8[i];
-    }
-    if (threadIdx.x == 0) S.ticket = atomicAdd(ticket_ctr, 1);
-    __syncthreads();
-    const int64_t f = (int64_t)S.ticket * 4 + wave;
-    const bool live = f < P.nframes;
-    const int64_t fq = live ? f : P.nframes - 1;
-    const int t = tile_of_frame(tiles, P.ntiles, fq);
+    uint32_t *fbuf = S.bits[threadIdx.x >> 6];
+    const int t = tile_of_frame(tiles, P.ntiles, f);
     const TileGeom g = tiles[t];
     const TileNorm tn = norms[t];
-    // shared LUT when the WG's four frames share a tile
-    if (threadIdx.x == 0) {
-        const int64_t fl = min((int64_t)S.ticket * 4 + 3, P.nframes - 1);
-        const int tl = tile_of_frame(tiles, P.ntiles, fl);
-        S.lut_tile = (tl == t && tn.mode == kNormLut) ? t : -1;
-    }
-    __syncthreads();
-    if (S.lut_tile >= 0) {
-        const int64_t R = tn.imax - tn.imin;
-        const int16_t *src = luts + (int64_t)S.lut_tile * kLutCap;
-        for (int64_t d = threadIdx.x; d <= R; d += blockDim.x) S.lut[d] = src[d];
-    }
-    uint32_t *fbuf = S.bits[wave];
-    for (int i = lane; i < kFrameWords; i += 64) fbuf[i] = 0;
-    __syncthreads();
-    if (!live) return;
-    const int16_t *lut = (S.lut_tile == t) ? S.lut : luts + (int64_t)t * kLutCap;
-
+    const int16_t *lut = (t == want) ? S.lut : luts + (int64_t)t * kLutCap;
     const int64_t fk = f - g.frame_base;
-    const int64_t s0 = fk * P.blocksize;
-    const int n = (int)min((int64_t)P.blocksize, (int64_t)g.h * g.w - s0);
+    const int64_t s0 = fk * kMaxBlock;
+    constexpr int n = kMaxBlock;
     const SubAnalysis A = ana[f];
     const int w = A.wasted;
     const int sbps = 16 - w;
     const T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
 
-    // ---- samples of this lane: frame indices [64*lane, 64*lane + 64), normalised, shifted, packed as
-    //      int16 pairs E[4 + m] = (x[2m], x[2m+1]); E[0..3] = the previous lane's last 8 samples
-    const int j0 = 64 * lane;
-    const int nv = max(0, min(64, n - j0));
-    uint32_t E[36], O[36];
+    // ---- this lane's 64 samples, normalised and shifted, packed as int16 pairs E[4 + m] = (x[2m], x[2m+1]);
+    //      E[0..3] = the previous lane's last 8 samples (zeros on lane 0)
+    uint32_t E[36];
     {
         Chunk64<DT> ch;
-        if (nv > 0) ch.load(base, P.row_stride, g.w, s0 + j0, P.vec_ok && (g.w % 64) == 0 && nv == 64, nv);
-#pragma unroll
-        for (int m = 0; m < 32; m++) {
-            const int32_t a = (2 * m < nv) ? (norm_fast<DT>(ch.get(2 * m), tn, lut) >> w) : 0;
-            const int32_t b = (2 * m + 1 < nv) ? (norm_fast<DT>(ch.get(2 * m + 1), tn, lut) >> w) : 0;
-            E[4 + m] = pack2(a, b);
-        }
+        ch.load(base, P.row_stride, g.w, s0 + 64 * lane, P.vec_ok && (g.w % 64) == 0, 64);
+        int32_t lo = 0;
+        norm_chunk<DT>(ch, tn, lut, [&](int j, int32_t x) {
+            if (j & 1) E[4 + (j >> 1)] = pack2(lo, x >> w);
+            else lo = x >> w;
+        });
     }
 #pragma unroll
     for (int m = 0; m < 4; m++) {
-        E[m] = __shfl_up(E[32 + m], 1);
-        if (lane == 0) E[m] = 0;
+        const uint32_t h = __shfl_up(E[32 + m], 1);
+        E[m] = lane == 0 ? 0u : h;
     }
-    // O[m] = (x[2m-9+... ]): odd-aligned pairs, O[k] = (hi(E[k-1]), lo(E[k]))
-    O[0] = 0;
-#pragma unroll
-    for (int m = 1; m < 36; m++) O[m] = __builtin_amdgcn_perm(E[m], E[m - 1], 0x05040302u);
-    auto X = [&](int j) -> int32_t {  // sample j of this lane (compile-time j)
+    auto X = [&](int j) -> int32_t {
         const uint32_t v = E[4 + (j >> 1)];
         return (j & 1) ? ((int32_t)v >> 16) : (int32_t)(int16_t)(v & 0xFFFFu);
     };
+    const bool l0 = lane == 0;
 
-    // ---- fixed predictor totals over samples 4..n-1 (FLAC__fixed_compute_best_predictor) + constant test
-    uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0, diff = 0;
+    // ---- fixed predictor totals over samples 4..n-1 (fixed.c FLAC__fixed_compute_best_predictor), the
+    //      constant test, and lane 0's warm-up extras wk = sum_{i=k}^{3} |e_k(i)| for the fixed partition sums
+    uint32_t lt[5] = {0, 0, 0, 0, 0}, wx[5] = {0, 0, 0, 0, 0};
+    uint32_t diff = 0;
     const int32_t x0 = __shfl((int)(int16_t)(E[4] & 0xFFFFu), 0);
     {
         const int32_t h1 = (int32_t)E[3] >> 16, h2 = (int16_t)(E[3] & 0xFFFFu);
@@ -1532,103 +1646,86 @@ __global__ void __launch_bounds__(256) k_encode_v2(const typename Elem<DT>::T *r
 #pragma unroll
         for (int j = 0; j < 64; j++) {
             const int32_t xi = X(j);
-            const int32_t e1 = xi - a1, e2 = e1 - d1, e3 = e2 - d2, e4 = e3 - d3;
-            if ((j0 + j >= 4) && (j < nv)) {
-                t0 += (uint32_t)abs(xi);
-                t1 += (uint32_t)abs(e1);
-                t2 += (uint32_t)abs(e2);
-                t3 += (uint32_t)abs(e3);
-                t4 += (uint32_t)abs(e4);
+            const int32_t e[5] = {xi, xi - a1, xi - a1 - d1, xi - a1 - d1 - d2, xi - a1 - d1 - d2 - d3};
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                const uint32_t ae = (uint32_t)abs(e[k]);
+                if (j >= 4) lt[k] += ae;
+                else {
+                    lt[k] += l0 ? 0u : ae;
+                    if (j >= k) wx[k] += l0 ? ae : 0u;
+                }
             }
-            if (j < nv) diff |= (uint32_t)(xi ^ x0);
+            diff |= (uint32_t)(xi ^ x0);
             a1 = xi;
-            d1 = e1;
-            d2 = e2;
-            d3 = e3;
+            d1 = e[1];
+            d2 = e[2];
+            d3 = e[3];
         }
     }
-    t0 = wave_sum_u32(t0);
-    t1 = wave_sum_u32(t1);
-    t2 = wave_sum_u32(t2);
-    t3 = wave_sum_u32(t3);
-    t4 = wave_sum_u32(t4);
+    reg_fence(E);
+    uint32_t tt[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) tt[k] = wave_sum_u32(lt[k]);
     diff = wave_or_u32(diff);
     int guess;
     {
-        uint32_t m = min(min(t1, t2), min(t3, t4));
-        if (t0 <= m) guess = 0;
-        else if (t1 <= min(min(t2, t3), t4)) guess = 1;
-        else if (t2 <= min(t3, t4)) guess = 2;
-        else if (t3 <= t4) guess = 3;
+        const uint32_t m = min(min(tt[1], tt[2]), min(tt[3], tt[4]));
+        if (tt[0] <= m) guess = 0;
+        else if (tt[1] <= min(min(tt[2], tt[3]), tt[4])) guess = 1;
+        else if (tt[2] <= min(tt[3], tt[4])) guess = 2;
+        else if (tt[3] <= tt[4]) guess = 3;
         else guess = 4;
     }
     const double dn = (double)(n - 4);
-    const uint32_t tg = guess == 0 ? t0 : guess == 1 ? t1 : guess == 2 ? t2 : guess == 3 ? t3 : t4;
-    const float fb1 = (float)(t1 > 0 ? log(M_LN2 * (double)t1 / dn) / M_LN2 : 0.0);
+    uint32_t tg = tt[0], sf = lt[0] + wx[0];
+#pragma unroll
+    for (int k = 1; k < 5; k++)
+        if (guess == k) {
+            tg = tt[k];
+            sf = lt[k] + wx[k];
+        }
+    const float fb1 = (float)(tt[1] > 0 ? log(M_LN2 * (double)tt[1] / dn) / M_LN2 : 0.0);
     const float fbg = (float)(tg > 0 ? log(M_LN2 * (double)tg / dn) / M_LN2 : 0.0);
-    const bool constant = n > 4 && fb1 == 0.0f && diff == 0;
-    const bool cand_fixed = n > 4 && !constant && !(fbg >= (float)sbps);
-    const bool cand_lpc = n > 4 && !constant && (A.flags & kFlagLpcOk);
-
-    // coefficient pairs
-    uint32_t CF[4], CL[4];
-    {
-        int32_t qf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (guess == 1) qf[0] = 1;
-        else if (guess == 2) { qf[0] = 2; qf[1] = -1; }
-        else if (guess == 3) { qf[0] = 3; qf[1] = -3; qf[2] = 1; }
-        else if (guess == 4) { qf[0] = 4; qf[1] = -6; qf[2] = 4; qf[3] = -1; }
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            CF[k] = pack2(qf[2 * k + 1], qf[2 * k]);
-            CL[k] = pack2(A.q[2 * k + 1], A.q[2 * k]);
-        }
-    }
+    const bool constant = fb1 == 0.0f && diff == 0;
+    const bool cand_fixed = !constant && !(fbg >= (float)sbps);
+    const bool cand_lpc = !constant && (A.flags & kFlagLpcOk);
     const int of = guess, ol = A.lpc_order, lshift = A.lpc_shift;
-    // ---- per-lane residual magnitude sums for both candidates (partition = 2 lanes at order 5)
-    uint64_t sf = 0, sl = 0;
+
+    uint32_t CL[4];
 #pragma unroll
-    for (int j = 0; j < 64; j++) {
-        const int i = j0 + j;
-        if (j < nv) {
-            if (cand_fixed && i >= of) sf += (uint32_t)abs(residual_at(E, O, CF, 0, j, X(j)));
-            if (cand_lpc && i >= ol) sl += (uint32_t)abs(residual_at(E, O, CL, lshift, j, X(j)));
+    for (int k = 0; k < 4; k++) CL[k] = pack2(A.q[2 * k + 1], A.q[2 * k]);
+    // ---- this lane's LPC |r| sum (residuals are recomputed by the later passes: cheaper than 64 live VGPRs)
+    uint32_t sl = 0;
+    if (cand_lpc) {
+#pragma unroll
+        for (int j = 0; j < 64; j++) {
+            const uint32_t a = (uint32_t)abs(residual_at(E, CL, lshift, j, X(j)));
+            if (j < kMaxLpc) sl += (l0 && j < ol) ? 0u : a;
+            else sl += a;
         }
     }
-    // ---- partition search (set_partitioned_rice_) for one candidate: returns bits, order, lane's k
-    const int max_po_blk = min(kMaxPartOrder, __builtin_ctz((unsigned)n));
-    const bool aligned = n == 4096;  // partitions at orders <= 5 cover whole lanes
-    auto rice = [&](uint64_t lane_sum, int order, uint32_t &best_bits, int &best_po, int &my_k) {
-        int mpo = max_po_blk;
-        while (mpo > 0 && (n >> mpo) <= order) mpo--;
-        // group sums at each order: groups of 64 >> po lanes (aligned frames)
-        uint64_t gs[6];
-        gs[5] = lane_sum + __shfl_xor(lane_sum, 1);
-        gs[4] = gs[5] + __shfl_xor(gs[5], 2);
-        gs[3] = gs[4] + __shfl_xor(gs[4], 4);
-        gs[2] = gs[3] + __shfl_xor(gs[3], 8);
-        gs[1] = gs[2] + __shfl_xor(gs[2], 16);
-        gs[0] = gs[1] + __shfl_xor(gs[1], 32);
+    reg_fence(E);
+    // ---- set_partitioned_rice_ (stream_encoder.c): orders 5..0, group sums merged by lane shuffles;
+    //      n = 4096 so max order is 5 for every predictor order <= 8
+    auto rice = [&](uint32_t lane_sum, int order, uint32_t &best_bits, int &best_po, int &my_k) {
         best_bits = 0;
         best_po = 0;
         my_k = 0;
-        for (int po = mpo; po >= 0; po--) {
+        uint64_t gsum = (uint64_t)lane_sum + (uint64_t)__shfl_xor(lane_sum, 1);
+#pragma unroll
+        for (int po = 5; po >= 0; po--) {
+            if (po < 5) gsum += __shfl_xor(gsum, 1 << (5 - po));
             const int lanes_per = 64 >> po;
-            const int p = lane / lanes_per;
             const uint32_t pbase = (uint32_t)(n >> po);
-            uint32_t ns = pbase, div = 0x40000u / pbase;
-            if (p == 0) {
-                ns -= (uint32_t)order;
-                div = 0x40000u / ns;
-            }
-            const uint64_t mean = gs[po];
-            uint32_t k;
-            if (mean < 2 || (((mean - 1) * div) >> 18) == 0) k = 0;
-            else k = (uint32_t)ilog2_u64(((mean - 1) * div) >> 18) + 1;
+            const uint32_t ns = lane < lanes_per ? pbase - (uint32_t)order : pbase;
+            const uint32_t div = 0x40000u / ns;
+            const uint64_t prod = gsum >= 1 ? ((gsum - 1) * div) >> 18 : 0;
+            uint32_t k = (gsum < 2 || prod == 0) ? 0u : (uint32_t)ilog2_u64(prod) + 1;
             if (k >= 15) k = 14;
-            uint64_t pb = 4 + (uint64_t)(1 + k) * ns + (k ? (mean >> (k - 1)) : (mean << 1)) - (ns >> 1);
+            uint64_t pb = 4 + (uint64_t)(1 + k) * ns + (k ? (gsum >> (k - 1)) : (gsum << 1)) - (ns >> 1);
             if (pb > 0xFFFFFFFFull) pb = 0xFFFFFFFFull;
-            const uint32_t contrib = (lane % lanes_per == 0) ? (uint32_t)pb : 0u;
+            const uint32_t contrib = ((lane & (lanes_per - 1)) == 0) ? (uint32_t)pb : 0u;
             const uint32_t bits = 6 + wave_sum_u32(contrib);
             if (best_bits == 0 || bits < best_bits) {
                 best_bits = bits;
@@ -1639,51 +1736,35 @@ __global__ void __launch_bounds__(256) k_encode_v2(const typename Elem<DT>::T *r
     };
     uint32_t rb_f = 0, rb_l = 0;
     int po_f = 0, po_l = 0, k_f = 0, k_l = 0;
-    if (aligned) {
-        if (cand_fixed) rice(sf, of, rb_f, po_f, k_f);
-        if (cand_lpc) rice(sl, ol, rb_l, po_l, k_l);
-    } else if (cand_fixed || cand_lpc) {
-        atomicOr(err, 4);  // partial frames go through the generic kernels (host routes them)
-    }
+    if (cand_fixed) rice(sf, of, rb_f, po_f, k_f);
+    if (cand_lpc) rice(sl, ol, rb_l, po_l, k_l);
     // ---- choose (process_subframe_: VERBATIM, then CONSTANT | FIXED, LPC; strict <)
     uint32_t best = (uint32_t)(1 + 6 + 1 + w + n * sbps);
     int type = 1;
-    if (n > 4) {
-        if (constant) {
-            const uint32_t cb = (uint32_t)(1 + 6 + 1 + w + sbps);
-            if (cb < best) { best = cb; type = 0; }
-        } else {
-            if (cand_fixed) {
-                uint32_t est = (uint32_t)(1 + 6 + 1 + w + of * sbps);
-                est = (rb_f < 0xFFFFFFFFu - est) ? est + rb_f : 0xFFFFFFFFu;
-                if (est < best) { best = est; type = 2; }
-            }
-            if (cand_lpc) {
-                uint32_t est = (uint32_t)(1 + 6 + 1 + w + 4 + 5 + sbps * ol + A.lpc_prec * ol);
-                est = (rb_l < 0xFFFFFFFFu - est) ? est + rb_l : 0xFFFFFFFFu;
-                if (est != 0 && est < best) { best = est; type = 3; }
-            }
+    if (constant) {
+        const uint32_t cb = (uint32_t)(1 + 6 + 1 + w + sbps);
+        if (cb < best) { best = cb; type = 0; }
+    } else {
+        if (cand_fixed) {
+            uint32_t est = (uint32_t)(1 + 6 + 1 + w + of * sbps);
+            est = (rb_f < 0xFFFFFFFFu - est) ? est + rb_f : 0xFFFFFFFFu;
+            if (est < best) { best = est; type = 2; }
+        }
+        if (cand_lpc) {
+            uint32_t est = (uint32_t)(1 + 6 + 1 + w + 4 + 5 + sbps * ol + A.lpc_prec * ol);
+            est = (rb_l < 0xFFFFFFFFu - est) ? est + rb_l : 0xFFFFFFFFu;
+            if (est != 0 && est < best) { best = est; type = 3; }
         }
     }
-    // ---- frame header (lane 0)
+    // ---- frame header + subframe header (lane 0; bytes go straight to LDS, CRC-8 on the fly)
     uint32_t hdr_bits = 0;
-    if (lane == 0) {
-        uint8_t h[16];
-        int hb = 0;
-        int bsc = 0, bsx = 0;
-        switch (n) {
-        case 192: bsc = 1; break;
-        case 576: bsc = 2; break;
-        case 1152: bsc = 3; break;
-        case 2304: bsc = 4; break;
-        case 4608: bsc = 5; break;
-        case 256: bsc = 8; break;
-        case 512: bsc = 9; break;
-        case 1024: bsc = 10; break;
-        case 2048: bsc = 11; break;
-        case 4096: bsc = 12; break;
-        default: bsc = bsx = (n <= 256 ? 6 : 7); break;
-        }
+    if (l0) {
+        uint32_t hb = 0, c8 = 0;
+        auto put8 = [&](uint32_t b) {
+            lds_put_bits2(fbuf, hb << 3, b, 8);
+            c8 = S.crc8[c8 ^ b];
+            hb++;
+        };
         const int sr = P.sample_rate;
         int src, srx = 0;
         switch (sr) {
@@ -1703,172 +1784,261 @@ __global__ void __launch_bounds__(256) k_encode_v2(const typename Elem<DT>::T *r
             else if (sr % 10 == 0 && sr / 10 <= 65535) src = srx = 14;
             else src = srx = 13;
         }
-        h[hb++] = 0xFF;
-        h[hb++] = 0xF8;
-        h[hb++] = (uint8_t)((bsc << 4) | src);
-        h[hb++] = (uint8_t)((0 << 4) | (4 << 1));  // mono, 16 bits
-        const uint32_t v = (uint32_t)fk;
-        if (v < 0x80) h[hb++] = (uint8_t)v;
-        else if (v < 0x800) { h[hb++] = (uint8_t)(0xC0 | (v >> 6)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
-        else if (v < 0x10000) { h[hb++] = (uint8_t)(0xE0 | (v >> 12)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
-        else { h[hb++] = (uint8_t)(0xF0 | (v >> 18)); h[hb++] = (uint8_t)(0x80 | ((v >> 12) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
-        if (bsx == 6) h[hb++] = (uint8_t)(n - 1);
-        else if (bsx == 7) { h[hb++] = (uint8_t)((n - 1) >> 8); h[hb++] = (uint8_t)(n - 1); }
-        if (srx == 12) h[hb++] = (uint8_t)(sr / 1000);
-        else if (srx == 13) { h[hb++] = (uint8_t)(sr >> 8); h[hb++] = (uint8_t)sr; }
-        else if (srx == 14) { h[hb++] = (uint8_t)((sr / 10) >> 8); h[hb++] = (uint8_t)(sr / 10); }
-        uint8_t c = 0;
-        for (int i = 0; i < hb; i++) c = S.crc8[c ^ h[i]];
-        h[hb++] = c;
-        for (int i = 0; i < hb; i++) lds_put_bits(fbuf, (uint32_t)(i * 8), h[i], 8);
-        hdr_bits = (uint32_t)(hb * 8);
-        // subframe header: 0, type(6), wasted flag, unary wasted
+        put8(0xFF);
+        put8(0xF8);
+        put8((uint32_t)((12 << 4) | src));  // block size code 12 = 4096
+        put8((uint32_t)(4 << 1));           // mono, 16 bits
+        const uint32_t v = (uint32_t)fk;    // UTF-8 coded frame number
+        if (v < 0x80) put8(v);
+        else if (v < 0x800) { put8(0xC0 | (v >> 6)); put8(0x80 | (v & 0x3F)); }
+        else if (v < 0x10000) { put8(0xE0 | (v >> 12)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
+        else if (v < 0x200000) { put8(0xF0 | (v >> 18)); put8(0x80 | ((v >> 12) & 0x3F)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
+        else if (v < 0x4000000) { put8(0xF8 | (v >> 24)); put8(0x80 | ((v >> 18) & 0x3F)); put8(0x80 | ((v >> 12) & 0x3F)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
+        else { put8(0xFC | (v >> 30)); put8(0x80 | ((v >> 24) & 0x3F)); put8(0x80 | ((v >> 18) & 0x3F)); put8(0x80 | ((v >> 12) & 0x3F)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
+        if (srx == 12) put8((uint32_t)(sr / 1000));
+        else if (srx == 13) { put8((uint32_t)(sr >> 8) & 0xFF); put8((uint32_t)sr & 0xFF); }
+        else if (srx == 14) { put8((uint32_t)((sr / 10) >> 8) & 0xFF); put8((uint32_t)(sr / 10) & 0xFF); }
+        put8(c8);  // CRC-8 (the table lookup of the last call is unused)
+        hdr_bits = hb << 3;
         const int typecode = type == 0 ? 0 : type == 1 ? 1 : type == 2 ? 8 + of : 32 + ol - 1;
-        lds_put_bits(fbuf, hdr_bits, (uint32_t)(typecode << 1) | (w ? 1u : 0u), 8);
-        if (w) lds_put_bits(fbuf, hdr_bits + 8 + (uint32_t)(w - 1), 1, 1);
+        lds_put_bits2(fbuf, hdr_bits, (uint32_t)(typecode << 1) | (w ? 1u : 0u), 8);
+        if (w) lds_put_bits2(fbuf, hdr_bits + 8 + (uint32_t)(w - 1), 1, 1);
     }
     hdr_bits = (uint32_t)__shfl((int)hdr_bits, 0);
     uint32_t pos = hdr_bits + 8 + (uint32_t)w;  // after the subframe header
     uint32_t end_bits;
+    bool ok = true;
+    const uint32_t smask = (1u << sbps) - 1u;
+    // phase A: everything but the bulk sample/residual packing, ending with the exact frame size
+    uint32_t C[4];
+    int shift = lshift, k = 0, lanes_per = 64, p = 0, o = 0, po = 0;
+    uint32_t run = 0;
     if (type == 0) {
-        if (lane == 0) lds_put_bits(fbuf, pos, (uint32_t)X(0) & ((1u << sbps) - 1u), sbps);
+        if (l0) lds_put_bits2(fbuf, pos, (uint32_t)X(0) & smask, sbps);
         end_bits = pos + (uint32_t)sbps;
     } else if (type == 1) {
-#pragma unroll
-        for (int j = 0; j < 64; j++)
-            if (j < nv) lds_put_bits(fbuf, pos + (uint32_t)(j0 + j) * sbps, (uint32_t)X(j) & ((1u << sbps) - 1u), sbps);
         end_bits = pos + (uint32_t)n * sbps;
     } else {
-        const int o = type == 2 ? of : ol;
-        const uint32_t *C = type == 2 ? CF : CL;
-        const int shift = type == 2 ? 0 : lshift;
-        const int po = type == 2 ? po_f : po_l;
-        const int k = type == 2 ? k_f : k_l;
-        const int lanes_per = 64 >> po;
-        const int p = lane / lanes_per;
-        // warm-up samples (lane 0 holds samples 0..63, o <= 8)
-        if (lane == 0) {
+        o = type == 2 ? of : ol;
+        po = type == 2 ? po_f : po_l;
+        k = type == 2 ? k_f : k_l;
+        lanes_per = 64 >> po;
+        p = lane / lanes_per;
+        if (type == 2) {
+            int32_t qf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (of == 1) qf[0] = 1;
+            else if (of == 2) { qf[0] = 2; qf[1] = -1; }
+            else if (of == 3) { qf[0] = 3; qf[1] = -3; qf[2] = 1; }
+            else if (of == 4) { qf[0] = 4; qf[1] = -6; qf[2] = 4; qf[3] = -1; }
+#pragma unroll
+            for (int m = 0; m < 4; m++) C[m] = pack2(qf[2 * m + 1], qf[2 * m]);
+            shift = 0;
+        } else {
+#pragma unroll
+            for (int m = 0; m < 4; m++) C[m] = CL[m];
+        }
+        if (l0) {
 #pragma unroll
             for (int i = 0; i < kMaxLpc; i++)
-                if (i < o) lds_put_bits(fbuf, pos + (uint32_t)i * sbps, (uint32_t)X(i) & ((1u << sbps) - 1u), sbps);
+                if (i < o) lds_put_bits2(fbuf, pos + (uint32_t)i * sbps, (uint32_t)X(i) & smask, sbps);
         }
         pos += (uint32_t)o * sbps;
         if (type == 3) {
-            if (lane == 0) {
-                lds_put_bits(fbuf, pos, (uint32_t)(A.lpc_prec - 1), 4);
-                lds_put_bits(fbuf, pos + 4, (uint32_t)lshift & 31u, 5);
-                for (int i = 0; i < o; i++)
-                    lds_put_bits(fbuf, pos + 9 + (uint32_t)i * A.lpc_prec, (uint32_t)A.q[i] & ((1u << A.lpc_prec) - 1u), A.lpc_prec);
+            if (l0) {
+                lds_put_bits2(fbuf, pos, (uint32_t)(A.lpc_prec - 1), 4);
+                lds_put_bits2(fbuf, pos + 4, (uint32_t)lshift & 31u, 5);
+#pragma unroll
+                for (int i = 0; i < kMaxLpc; i++)
+                    if (i < o)
+                        lds_put_bits2(fbuf, pos + 9 + (uint32_t)i * A.lpc_prec,
+                                      (uint32_t)A.q[i] & ((1u << A.lpc_prec) - 1u), A.lpc_prec);
             }
             pos += 9 + (uint32_t)o * A.lpc_prec;
         }
-        if (lane == 0) lds_put_bits(fbuf, pos, (uint32_t)po, 6);  // method RICE (00) + order (4 bits)
+        if (l0) lds_put_bits2(fbuf, pos, (uint32_t)po, 6);  // RICE (00) + partition order (4 bits)
         pos += 6;
-        // exact code lengths
+        // exact code lengths (masked warm-up samples: len 0)
         uint32_t lens = 0;
 #pragma unroll
         for (int j = 0; j < 64; j++) {
-            const int i = j0 + j;
-            if (j < nv && i >= o) {
-                const int32_t r = residual_at(E, O, C, shift, j, X(j));
-                const uint32_t u = ((uint32_t)r << 1) ^ (uint32_t)(r >> 31);
-                lens += 1u + (uint32_t)k + (u >> k);
-            }
+            const uint32_t u = zigzag(residual_at(E, C, shift, j, X(j)));
+            uint32_t len = 1u + (uint32_t)k + (u >> k);
+            if (j < kMaxLpc && l0 && j < o) len = 0;
+            lens += len;
         }
+        reg_fence(E);
         const uint64_t excl = wave_excl_scan_u64(lens, lane);
         const uint64_t total = (uint64_t)__shfl((long long)(excl + lens), 63);
         const uint64_t fin = (uint64_t)pos + 4ull * (uint64_t)(1 << po) + total;
-        if (fin + 64 > (uint64_t)kFrameWords * 32) {
-            if (lane == 0) atomicOr(err, 2);
-            return;
-        }
-        // parameter field of the partition starting at this lane
-        if (lane % lanes_per == 0) lds_put_bits(fbuf, pos + 4u * (uint32_t)p + (uint32_t)excl, (uint32_t)k, 4);
-        uint32_t run = pos + 4u * (uint32_t)(p + 1) + (uint32_t)excl;
-#pragma unroll
-        for (int j = 0; j < 64; j++) {
-            const int i = j0 + j;
-            if (j < nv && i >= o) {
-                const int32_t r = residual_at(E, O, C, shift, j, X(j));
-                const uint32_t u = ((uint32_t)r << 1) ^ (uint32_t)(r >> 31);
-                const uint32_t q = u >> k;
-                lds_put_bits(fbuf, run + q, (1u << k) | (u & ((1u << k) - 1u)), k + 1);
-                run += q + 1 + (uint32_t)k;
-            }
-        }
         end_bits = (uint32_t)fin;
+        if (fin + 64 > (uint64_t)kFrameWordsV3 * 32) ok = false;
+        run = pos + 4u * (uint32_t)(p + 1) + (uint32_t)excl;
+        if (ok && (lane & (lanes_per - 1)) == 0) lds_put_bits2(fbuf, run - 4u, (uint32_t)k, 4);
+    }
+    if (!ok) {
+        if (l0) atomicOr(err, 2);
+        end_bits = 0;
     }
     const uint32_t body = (end_bits + 7) >> 3;  // bytes before the CRC-16 footer
-    const uint64_t fbytes = (uint64_t)body + 2;
-    // ---- publish our aggregate, compute CRC-16 while predecessors resolve
-    if (lane == 0) {
+    const uint64_t fbytes = ok ? (uint64_t)body + 2 : 0;
+    // ---- publish our aggregate now, so successors' look-back resolves while we pack
+    if (l0) {
         const uint64_t v = (f == 0 ? kFlagIncl : kFlagAgg) | fbytes;
         __hip_atomic_store(&status[f], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // wave-level LDS visibility of the atomics above: all lanes' ds ops complete in order per wave
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    // phase B: bulk packing
+    if (type == 1) {
+        const uint32_t p0 = pos + (uint32_t)(64 * lane) * (uint32_t)sbps;
+#pragma unroll
+        for (int j = 0; j < 64; j++) lds_put_bits2(fbuf, p0 + (uint32_t)j * sbps, (uint32_t)X(j) & smask, sbps);
+    } else if (type >= 2 && ok && !(P.ablate & 4)) {
+        const uint32_t one = 1u << k, low = one - 1u;
+#pragma unroll
+        for (int j = 0; j < 64; j++) {
+            const uint32_t u = zigzag(residual_at(E, C, shift, j, X(j)));
+            uint32_t q = u >> k, code = (u & low) | one, adv = q + 1 + (uint32_t)k;
+            if (j < kMaxLpc && l0 && j < o) {
+                q = 0;
+                code = 0;
+                adv = 0;
+            }
+            lds_put_bits2(fbuf, run + q, code, k + 1);
+            run += adv;
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS atomics have landed
     __builtin_amdgcn_wave_barrier();
     uint32_t crc = 0;
-    {
-        const uint32_t ch = (body + 63) / 64;
-        const uint32_t b0 = min(body, (uint32_t)lane * ch), b1 = min(body, b0 + ch);
-        for (uint32_t b = b0; b < b1; b++) {
-            const uint8_t byte = (uint8_t)(fbuf[b >> 2] >> (24 - 8 * (b & 3)));
-            crc = ((crc << 8) & 0xFFFFu) ^ S.crc[((crc >> 8) ^ byte) & 0xFF];
+    if (ok && !(P.ablate & 2)) {
+        // slice-by-4 over 32-bit words, one contiguous word range per lane, combined with x^(8m) factors
+        const uint32_t nfw = body >> 2, tail = body & 3;
+        const uint32_t cw = (nfw + 63) >> 6;
+        const uint32_t wb = min(nfw, (uint32_t)lane * cw), we = min(nfw, wb + cw);
+        uint32_t c = 0;
+        for (uint32_t i = wb; i < we; i++) {
+            const uint32_t word = fbuf[i];
+            c = (uint32_t)S.crc4[3][((c >> 8) ^ (word >> 24)) & 0xFF] ^ S.crc4[2][((c & 0xFF) ^ (word >> 16)) & 0xFF] ^
+                S.crc4[1][(word >> 8) & 0xFF] ^ S.crc4[0][word & 0xFF];
         }
-        if (b1 > b0 && b1 < body) crc = gf_mulmod(crc, xpow8((uint64_t)(body - b1)));
+        uint32_t end = we * 4;
+        if (lane == (int)((nfw - 1) / cw)) {
+            const uint32_t word = fbuf[nfw];
+            for (uint32_t b = 0; b < tail; b++) {
+                const uint32_t byte = (word >> (24 - 8 * b)) & 0xFF;
+                c = ((c << 8) & 0xFFFFu) ^ S.crc4[0][((c >> 8) ^ byte) & 0xFF];
+            }
+            end += tail;
+        }
+        crc = gf_mulmod(c, g_xpow_bytes[body - end]);
 #pragma unroll
         for (int o2 = 32; o2 > 0; o2 >>= 1) crc ^= __shfl_xor(crc, o2);
+        if (l0) lds_put_bits2(fbuf, body << 3, crc, 16);
     }
-    // ---- decoupled look-back for the exclusive prefix
+    // ---- decoupled look-back for the exclusive prefix: the wave probes 64 predecessors per round
     uint64_t prefix = 0;
-    if (lane == 0 && f > 0) {
-        int64_t j = f - 1;
+    if (P.ablate & 1) {
+        prefix = (uint64_t)f * 8320;  // diagnostic: fixed slots, no waiting
+    } else if (f > 0) {
+        int64_t hi = f - 1;
         uint64_t accum = 0;
         long spins = 0;
         while (true) {
-            uint64_t sv = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((sv >> 62) == 0) {
-                if (++spins > (1l << 26)) {  // bounded: never hang the device
-                    atomicOr(err, 8);
+            const int64_t j = hi - lane;
+            uint64_t sv = kFlagIncl;  // before frame 0: inclusive 0
+            if (j >= 0) sv = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t flag = (uint32_t)(sv >> 62);
+            const uint64_t incl = __ballot(flag == 2);
+            const uint64_t zero = __ballot(flag == 0);
+            const int first = incl ? __builtin_ctzll(incl) : 64;  // nearest inclusive
+            const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
+            if (zero & need) {  // a needed predecessor has not published yet
+                if (++spins > (1l << 24)) {
+                    if (l0) atomicOr(err, 8);
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
                 continue;
             }
-            accum += sv & kValMask;
-            if ((sv >> 62) == 2) break;
-            j--;
+            const uint64_t mine = (lane <= first) ? (sv & kValMask) : 0;
+            accum += wave_sum_u64(mine);
+            if (first < 64) break;
+            hi -= 64;
         }
         prefix = accum;
-        __hip_atomic_store(&status[f], kFlagIncl | (prefix + fbytes), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (l0) {
+        if (f > 0 && !(P.ablate & 1))
+            __hip_atomic_store(&status[f], kFlagIncl | (prefix + fbytes), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         frame_off[f] = (int64_t)prefix;
-    } else if (lane == 0) {
-        frame_off[f] = 0;
     }
-    prefix = (uint64_t)__shfl((long long)prefix, 0);
-    // ---- store: body bytes from LDS then the CRC, at arena[prefix ..)
+    const uint32_t used_words = ok ? (uint32_t)((fbytes + 3) >> 2) + 2 : (uint32_t)kFrameWordsV3;
     if ((int64_t)(prefix + fbytes) > arena_cap) {
-        if (lane == 0) atomicOr(err, 16);
-        return;
+        if (l0) atomicOr(err, 16);
+    } else if (!(P.ablate & 16) && fbytes) {
+        // ---- store [prefix, prefix + fbytes): bytes up to 16-B alignment, 16-B chunks, byte tail
+        uint8_t *dst = arena + prefix;
+        const uint32_t a0 = min((uint32_t)fbytes, (uint32_t)((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15));
+        auto byte_at = [&](uint32_t b) -> uint8_t { return (uint8_t)(fbuf[b >> 2] >> (24 - 8 * (b & 3))); };
+        if ((uint32_t)lane < a0) dst[lane] = byte_at((uint32_t)lane);
+        const uint32_t n16 = ((uint32_t)fbytes - a0) >> 4;
+        const uint32_t r = a0 & 3, sb = a0 >> 2;
+        uint4 *d16 = reinterpret_cast<uint4 *>(dst + a0);
+        for (uint32_t ci = (uint32_t)lane; ci < n16; ci += 64) {
+            const uint32_t s = sb + 4 * ci;
+            const uint32_t w0 = __builtin_bswap32(fbuf[s]), w1 = __builtin_bswap32(fbuf[s + 1]);
+            const uint32_t w2 = __builtin_bswap32(fbuf[s + 2]), w3 = __builtin_bswap32(fbuf[s + 3]);
+            const uint32_t w4 = __builtin_bswap32(fbuf[s + 4]);
+            uint4 o4;
+            o4.x = __builtin_amdgcn_alignbyte(w1, w0, r);
+            o4.y = __builtin_amdgcn_alignbyte(w2, w1, r);
+            o4.z = __builtin_amdgcn_alignbyte(w3, w2, r);
+            o4.w = __builtin_amdgcn_alignbyte(w4, w3, r);
+            d16[ci] = o4;
+        }
+        const uint32_t tb = a0 + 16 * n16 + (uint32_t)lane;
+        if (tb < (uint32_t)fbytes) dst[tb] = byte_at(tb);
     }
-    uint8_t *dst = arena + prefix;
-    const uint64_t total_b = fbytes;
-    auto byte_at = [&](uint64_t b) -> uint32_t {
-        if (b < body) return (fbuf[b >> 2] >> (24 - 8 * (b & 3))) & 0xFFu;
-        return b == body ? (crc >> 8) & 0xFFu : crc & 0xFFu;
-    };
-    // aligned 4-byte words of the destination fully inside the frame
-    const uint64_t a0 = (4 - (prefix & 3)) & 3;  // leading unaligned bytes
-    for (uint64_t b = (uint64_t)lane; b < min(a0, total_b); b += 64) dst[b] = (uint8_t)byte_at(b);
-    const uint64_t nwords = (total_b > a0) ? (total_b - a0) / 4 : 0;
-    uint32_t *dw = reinterpret_cast<uint32_t *>(dst + a0);
-    for (uint64_t wi = (uint64_t)lane; wi < nwords; wi += 64) {
-        const uint64_t b = a0 + wi * 4;
-        const uint32_t v = byte_at(b) | (byte_at(b + 1) << 8) | (byte_at(b + 2) << 16) | (byte_at(b + 3) << 24);
-        dw[wi] = v;
+    // leave the bit buffer zeroed for this wave's next frame (LDS ops of one wave complete in order)
+    for (uint32_t i = (uint32_t)lane; i < used_words; i += 64) fbuf[i] = 0;
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *raster, EncodeParams P,
+                                                  const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
+                                                  const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap,
+                                                  int64_t *frame_off, uint64_t *status, int *ticket_ctr, int *err) {
+    __shared__ EncV3Shared S;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) (&S.crc4[0][0])[i] = (&c_crc16x4[0][0])[i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) S.crc8[i] = c_crc8[i];
+    for (int i = threadIdx.x; i < 4 * kFrameWordsV3; i += blockDim.x) (&S.bits[0][0])[i] = 0;
+    if (threadIdx.x == 0) S.lut_tile = -1;
+    while (true) {
+        __syncthreads();  // previous ticket's readers of S.ticket / S.lut are done
+        if (threadIdx.x == 0) {
+            const int tk = atomicAdd(ticket_ctr, 1);
+            S.ticket = tk;
+            S.want = ((int64_t)tk * 4 < P.nframes) ? tile_of_frame(tiles, P.ntiles, (int64_t)tk * 4) : -1;
+        }
+        __syncthreads();
+        const int64_t fbase = (int64_t)S.ticket * 4;
+        if (fbase >= P.nframes) break;
+        const int want = S.want;
+        if (want != S.lut_tile) {  // WG-uniform
+            const TileNorm tw = norms[want];
+            if (tw.mode == kNormLut) {
+                const int64_t R = tw.imax - tw.imin;
+                const int16_t *src = luts + (int64_t)want * kLutCap;
+                for (int64_t d = threadIdx.x; d <= R; d += blockDim.x) S.lut[d] = src[d];
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) S.lut_tile = want;
+        }
+        const int64_t f = fbase + wave;
+        if (f < P.nframes)
+            encode_frame_v3<DT>(raster, P, tiles, norms, luts, ana, arena, arena_cap, frame_off, status, err, S, want, f,
+                                lane);
     }
-    for (uint64_t b = a0 + nwords * 4 + (uint64_t)lane; b < total_b; b += 64) dst[b] = (uint8_t)byte_at(b);
 }
 
 __global__ void k_fast_finish(const int64_t *frame_off, const uint64_t *status, const TileGeom *tiles, int ntiles,
@@ -1912,6 +2082,22 @@ static int upload_tables(frs_ctx *ctx) {
     FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_crc8), t8, sizeof(t8), 0, hipMemcpyHostToDevice, ctx->stream));
     FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_crc16), t16, sizeof(t16), 0, hipMemcpyHostToDevice, ctx->stream));
     FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_xpow8), xp, sizeof(xp), 0, hipMemcpyHostToDevice, ctx->stream));
+    // slice-by-4 tables: T_k[v] = T_{k-1}[v] advanced by one zero byte
+    static uint16_t t4[4][256];
+    static uint16_t xb[kXpowBytes];
+    for (int i = 0; i < 256; i++) t4[0][i] = t16[i];
+    for (int k = 1; k < 4; k++)
+        for (int i = 0; i < 256; i++) {
+            const uint16_t c = t4[k - 1][i];
+            t4[k][i] = (uint16_t)(((c << 8) & 0xFFFF) ^ t16[c >> 8]);
+        }
+    uint32_t pw = 1;  // x^(8m) mod P
+    for (int m = 0; m < kXpowBytes; m++) {
+        xb[m] = (uint16_t)pw;
+        pw = mulmod(pw, 0x100);
+    }
+    FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_crc16x4), t4, sizeof(t4), 0, hipMemcpyHostToDevice, ctx->stream));
+    FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xpow_bytes), xb, sizeof(xb), 0, hipMemcpyHostToDevice, ctx->stream));
     FRS_HIP(hipStreamSynchronize(ctx->stream));
     g_tables_ready[ctx->device] = true;
     return FRS_OK;
@@ -2014,7 +2200,7 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     P.ntiles = ntiles;
     P.norm_mode = d->norm_mode;
     P.vec_ok = 0;
-    P.pad2 = 0;
+    P.ablate = ctx->ablate;
 
     int rc = upload_tables(ctx);
     if (rc) return rc;
@@ -2054,7 +2240,23 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     // 1. tile stats
     prof_begin(ctx, "stats", &ev);
     k_stats_init<<<(ntiles + 255) / 256, 256, 0, st>>>(dnorms, ntiles);
-    {
+    bool stats_vec = false;
+    if constexpr (sizeof(T) <= 2 && !Elem<DT>::is_float) {
+        const int64_t es = (int64_t)sizeof(T);
+        const uintptr_t b = reinterpret_cast<uintptr_t>(raster_dev) + (uintptr_t)(d->band0 * d->band_stride * es);
+        stats_vec = (b % 16 == 0) && ((d->row_stride * es) % 16 == 0) && ((d->band_stride * es) % 16 == 0) &&
+                    ((d->tile_w * es) % 16 == 0) && ((d->width * es) % 16 == 0);
+        if (stats_vec) {
+            const int64_t px = (int64_t)d->tile_h * d->tile_w * d->nbands;
+            // ~256 KB per work-group, at least ~2048 work-groups overall
+            int splits = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)d->tile_h * d->nbands, px * es / (256 << 10)));
+            while ((int64_t)splits * ntiles < 2048 && splits < d->tile_h * d->nbands) splits++;
+            dim3 grid(splits, ntiles);
+            k_tile_stats_vec<DT><<<grid, 256, 0, st>>>(reinterpret_cast<const T *>(raster_dev), P, ctx->tiles.as<TileGeom>(),
+                                                       ctx->norms.as<TileNorm>(), splits);
+        }
+    }
+    if (!stats_vec) {
         int64_t rows = (int64_t)d->tile_h * d->nbands;
         int splits = (int)std::min<int64_t>(rows, std::max<int64_t>(1, (int64_t)4096 / ntiles));
         if (splits < 1) splits = 1;
@@ -2084,9 +2286,15 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         int *ticket = reinterpret_cast<int *>(dstatus + nframes);
         FRS_HIP(hipMemsetAsync(dstatus, 0, sizeof(uint64_t) * (nframes + 1), st));
         prof_begin(ctx, "encode", &ev);
-        k_encode_v2<DT><<<(unsigned)((nframes + 3) / 4), 256, 0, st>>>(
-            raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(), dana, reinterpret_cast<uint8_t *>(arena_dev), arena_cap,
-            ctx->frame_off.as<int64_t>(), dstatus, ticket, err_flag);
+        {
+            int nwg_max = 0;
+            FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nwg_max, k_encode_v3<DT>, 256, 0));
+            int64_t grid = (int64_t)std::max(1, nwg_max) * ctx->num_cus;
+            grid = std::min<int64_t>(grid, (nframes + 3) / 4);
+            k_encode_v3<DT><<<(unsigned)grid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(), dana,
+                                                            reinterpret_cast<uint8_t *>(arena_dev), arena_cap,
+                                                            ctx->frame_off.as<int64_t>(), dstatus, ticket, err_flag);
+        }
         prof_end(ctx, "encode", ev);
         k_fast_finish<<<(ntiles + 1 + 255) / 256, 256, 0, st>>>(ctx->frame_off.as<int64_t>(), dstatus, dtiles, ntiles,
                                                                nframes, ctx->tile_sizes.as<int64_t>());

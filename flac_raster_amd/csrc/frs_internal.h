@@ -40,11 +40,13 @@ struct ProfEntry {
 
 struct frs_ctx {
     int device = 0;
+    int num_cus = 256;
     hipStream_t stream = nullptr;
     std::string err;
     // encode scratch
     DevBuf tiles, norms, analysis, slots, frame_bytes, frame_off, scan_tmp, window, tile_sizes, luts, status;
     bool force_generic = false;  // testing: route every job through the generic kernels
+    int ablate = 0;              // diagnostics: FRS_ABLATE bitmask (outputs invalid when set)
     // host staging (pinned)
     DevBuf raster_stage, arena_stage;  // device copies for the host-pointer entry points
     // decode scratch

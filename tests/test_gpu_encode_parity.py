@@ -130,3 +130,23 @@ def test_fast_path_matches_oracle(gpu_ctx, dtype, lo, hi, shape, tile):
     assert list(off) == list(o_off)
     assert arena.tobytes() == o_arena.tobytes()
     assert list(mn) == list(o_mn) and list(mx) == list(o_mx)
+
+
+@pytest.mark.parametrize("kind,shape,tile", [
+    ("noise", (1024, 1024), 512),     # VERBATIM-heavy frames (uniform full-range noise)
+    ("dem", (2048, 3072), 512),       # 1536 frames: look-back spans many 64-frame windows, many tickets per WG
+    ("dem", (512, 4096), 64),         # one frame per tile: a WG's 4 frames sit in 4 tiles
+])
+def test_fast_path_scale_and_noise(gpu_ctx, kind, shape, tile):
+    rng = np.random.default_rng(4242)
+    H, W = shape
+    if kind == "noise":
+        band = rng.integers(-32768, 32768, size=shape, dtype=np.int16)
+    else:
+        y, x = np.meshgrid(np.linspace(0, 20, H), np.linspace(0, 20, W), indexing="ij")
+        band = (1000 + 300 * np.sin(x * 0.8) * np.cos(y * 0.3) + 150 * np.sin(1.2 * x) * np.sin(1.1 * y)
+                + 50 * rng.random(shape)).astype(np.int16)
+    arena, off, mn, mx, bps = _gpu_tiles(gpu_ctx, band, tile)
+    o_arena, o_off, o_mn, o_mx = O.encode_tiles(band, tile, threads=8)
+    assert list(off) == list(o_off)
+    assert arena.tobytes() == o_arena.tobytes()
