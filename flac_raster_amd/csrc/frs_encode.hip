@@ -110,6 +110,14 @@ __device__ inline int tile_of_frame(const TileGeom *tiles, int ntiles, int64_t f
     return lo;
 }
 
+// frame -> tile table for the fast kernels (one load instead of a binary search per frame)
+__global__ void k_frame_tile(const TileGeom *tiles, int ntiles, int32_t *ftile) {
+    const int t = blockIdx.x;
+    if (t >= ntiles) return;
+    const TileGeom g = tiles[t];
+    for (int i = threadIdx.x; i < g.nframes; i += blockDim.x) ftile[g.frame_base + i] = t;
+}
+
 // ------------------------------------------------------------------------------------ tile stats
 __global__ void k_stats_init(TileNorm *norms, int ntiles) {
     int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1318,7 +1326,7 @@ template <int DT>
 __global__ void __launch_bounds__(256) k_analyze_v2(const typename Elem<DT>::T *raster, EncodeParams P,
                                                    const TileGeom *tiles, const TileNorm *norms,
                                                    const int16_t *luts, const float *__restrict__ window,
-                                                   SubAnalysis *out) {
+                                                   SubAnalysis *out, const int32_t *__restrict__ ftile) {
     using T = typename Elem<DT>::T;
     __shared__ float swin[kMaxBlock];
     __shared__ int16_t slut[4][kLutCap];
@@ -1327,7 +1335,7 @@ __global__ void __launch_bounds__(256) k_analyze_v2(const typename Elem<DT>::T *
     const int64_t f = ((int64_t)blockIdx.x * 4 + wave) * 64 + lane;
     const bool live = f < P.nframes;
     const int64_t fq = live ? f : P.nframes - 1;  // dead lanes re-read the last frame (no out-of-tile loads)
-    const int t = tile_of_frame(tiles, P.ntiles, fq);
+    const int t = ftile[fq];
     const TileGeom g = tiles[t];
     const int64_t s0 = (fq - g.frame_base) * P.blocksize;
     const int64_t tile_px = (int64_t)g.h * g.w;
@@ -1513,6 +1521,80 @@ __device__ inline uint64_t wave_excl_scan_u64(uint64_t v, int lane) {
     return incl - v;
 }
 
+// ---- cross-lane primitives without LDS round trips: DPP within rows of 16, permlane16/32_swap across
+//      rows (gfx950).  Butterfly steps must be applied in order 1, 2, 4, 8, 16, 32 (the mirror patterns
+//      pair whole sub-groups only once the lower steps have made each sub-group uniform).
+template <int CTRL> __device__ inline uint32_t dpp_mov(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, false);
+}
+template <int STEP> __device__ inline uint32_t bfly_partner(uint32_t v);
+template <> __device__ inline uint32_t bfly_partner<1>(uint32_t v) { return dpp_mov<0xB1>(v); }   // quad_perm [1,0,3,2]
+template <> __device__ inline uint32_t bfly_partner<2>(uint32_t v) { return dpp_mov<0x4E>(v); }   // quad_perm [2,3,0,1]
+template <> __device__ inline uint32_t bfly_partner<4>(uint32_t v) { return dpp_mov<0x141>(v); }  // row_half_mirror
+template <> __device__ inline uint32_t bfly_partner<8>(uint32_t v) { return dpp_mov<0x140>(v); }  // row_mirror
+template <> __device__ inline uint32_t bfly_partner<16>(uint32_t v) {
+    const auto p = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    return p[0] ^ p[1] ^ v;  // one of p[0], p[1] is v itself, the other the partner row's value
+}
+template <> __device__ inline uint32_t bfly_partner<32>(uint32_t v) {
+    const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return p[0] ^ p[1] ^ v;
+}
+template <int STEP> __device__ inline uint64_t bfly_partner64(uint64_t v) {
+    return ((uint64_t)bfly_partner<STEP>((uint32_t)(v >> 32)) << 32) | bfly_partner<STEP>((uint32_t)v);
+}
+__device__ inline uint32_t uni(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ inline uint32_t dpp_wave_sum_u32(uint32_t v) {  // total, wave-uniform (SGPR)
+    v += bfly_partner<1>(v);
+    v += bfly_partner<2>(v);
+    v += bfly_partner<4>(v);
+    v += bfly_partner<8>(v);
+    v += bfly_partner<16>(v);
+    v += bfly_partner<32>(v);
+    return uni(v);
+}
+__device__ inline uint64_t dpp_wave_sum_u64(uint64_t v) {
+    v += bfly_partner64<1>(v);
+    v += bfly_partner64<2>(v);
+    v += bfly_partner64<4>(v);
+    v += bfly_partner64<8>(v);
+    v += bfly_partner64<16>(v);
+    v += bfly_partner64<32>(v);
+    return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | uni((uint32_t)v);
+}
+__device__ inline uint32_t dpp_wave_or_u32(uint32_t v) {
+    v |= bfly_partner<1>(v);
+    v |= bfly_partner<2>(v);
+    v |= bfly_partner<4>(v);
+    v |= bfly_partner<8>(v);
+    v |= bfly_partner<16>(v);
+    v |= bfly_partner<32>(v);
+    return uni(v);
+}
+__device__ inline uint32_t dpp_wave_xor_u32(uint32_t v) {
+    v ^= bfly_partner<1>(v);
+    v ^= bfly_partner<2>(v);
+    v ^= bfly_partner<4>(v);
+    v ^= bfly_partner<8>(v);
+    v ^= bfly_partner<16>(v);
+    v ^= bfly_partner<32>(v);
+    return uni(v);
+}
+// inclusive prefix sum over the wave: row_shr 1/2/4/8 within rows, then row_bcast15 / row_bcast31
+__device__ inline uint32_t dpp_incl_scan_u32(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);
+    return v;
+}
+// value of lane - 1 (lane 0: 0)
+__device__ inline uint32_t dpp_wave_shr1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+}
+
 typedef short v2s16 __attribute__((ext_vector_type(2)));
 __device__ inline int32_t dot2(uint32_t a, uint32_t b, int32_t c) {
     return __builtin_amdgcn_sdot2(__builtin_bit_cast(v2s16, a), __builtin_bit_cast(v2s16, b), c, false);
@@ -1561,14 +1643,18 @@ constexpr uint64_t kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62, kValMask = (1u
 // selects.  LPC residuals stay in registers between the partition-sum, code-length and packing passes;
 // the fixed candidate's partition sums fall out of the fixed-predictor totals pass.
 constexpr int kFrameWordsV3 = 2176;  // 69632 bits >= worst exact frame (estimate < verbatim)
-constexpr int kXpowBytes = kFrameWordsV3 * 4 + 16;
+constexpr int kXpowBytes = kFrameWordsV3 * 4 + 64;  // multiple of 64 (LDS split tables)
 __constant__ uint16_t c_crc16x4[4][256];           // T_k[v] = CRC-16 of byte v followed by k zero bytes
 __device__ uint16_t g_xpow_bytes[kXpowBytes];      // x^(8m) mod P for m bytes
+__device__ unsigned long long g_lb_stats[4];       // diagnostics (FRS_ABLATE bit 64): frames, rounds, spins, distance
 
+constexpr int kXpowHi = (kXpowBytes + 63) / 64;
 struct EncV3Shared {
     uint32_t bits[4][kFrameWordsV3];
     int16_t lut[kLutCap];
     uint16_t crc4[4][256];
+    uint16_t xlo[64];       // x^(8m) mod P, m = 0..63
+    uint16_t xhi[kXpowHi];  // x^(8*64*m) mod P
     uint8_t crc8[256];
     int ticket;
     int want;
@@ -1596,10 +1682,11 @@ template <int DT>
 __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const EncodeParams &P,
                                        const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
                                        const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap, int64_t *frame_off,
-                                       uint64_t *status, int *err, EncV3Shared &S, int want, int64_t f, int lane) {
+                                       uint64_t *status, int *err, EncV3Shared &S, int want, int64_t f, int lane,
+                                       const int32_t *ftile) {
     using T = typename Elem<DT>::T;
     uint32_t *fbuf = S.bits[threadIdx.x >> 6];
-    const int t = tile_of_frame(tiles, P.ntiles, f);
+    const int t = ftile[f];
     const TileGeom g = tiles[t];
     const TileNorm tn = norms[t];
     const int16_t *lut = (t == want) ? S.lut : luts + (int64_t)t * kLutCap;
@@ -1624,10 +1711,8 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         });
     }
 #pragma unroll
-    for (int m = 0; m < 4; m++) {
-        const uint32_t h = __shfl_up(E[32 + m], 1);
-        E[m] = lane == 0 ? 0u : h;
-    }
+    for (int m = 0; m < 4; m++) E[m] = dpp_wave_shr1(E[32 + m]);
+    reg_fence(E);  // keeps the load/normalise phase from overlapping the totals pass (VGPR peak)
     auto X = [&](int j) -> int32_t {
         const uint32_t v = E[4 + (j >> 1)];
         return (j & 1) ? ((int32_t)v >> 16) : (int32_t)(int16_t)(v & 0xFFFFu);
@@ -1638,13 +1723,18 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     //      constant test, and lane 0's warm-up extras wk = sum_{i=k}^{3} |e_k(i)| for the fixed partition sums
     uint32_t lt[5] = {0, 0, 0, 0, 0}, wx[5] = {0, 0, 0, 0, 0};
     uint32_t diff = 0;
-    const int32_t x0 = __shfl((int)(int16_t)(E[4] & 0xFFFFu), 0);
+    const int32_t x0 = (int32_t)uni((uint32_t)(int32_t)(int16_t)(E[4] & 0xFFFFu));
     {
         const int32_t h1 = (int32_t)E[3] >> 16, h2 = (int16_t)(E[3] & 0xFFFFu);
         const int32_t h3 = (int32_t)E[2] >> 16, h4 = (int16_t)(E[2] & 0xFFFFu);
         int32_t a1 = h1, d1 = h1 - h2, d2 = (h1 - h2) - (h2 - h3), d3 = ((h1 - h2) - (h2 - h3)) - ((h2 - h3) - (h3 - h4));
 #pragma unroll
         for (int j = 0; j < 64; j++) {
+            if (j % 8 == 0 && j) {  // bound the scheduler's look-ahead (VGPR peak)
+#pragma unroll
+                for (int k = 0; k < 5; k++) asm volatile("" : "+v"(lt[k]));
+                asm volatile("" : "+v"(a1), "+v"(d1), "+v"(d2), "+v"(d3));
+            }
             const int32_t xi = X(j);
             const int32_t e[5] = {xi, xi - a1, xi - a1 - d1, xi - a1 - d1 - d2, xi - a1 - d1 - d2 - d3};
 #pragma unroll
@@ -1666,8 +1756,8 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     reg_fence(E);
     uint32_t tt[5];
 #pragma unroll
-    for (int k = 0; k < 5; k++) tt[k] = wave_sum_u32(lt[k]);
-    diff = wave_or_u32(diff);
+    for (int k = 0; k < 5; k++) tt[k] = dpp_wave_sum_u32(lt[k]);
+    diff = dpp_wave_or_u32(diff);
     int guess;
     {
         const uint32_t m = min(min(tt[1], tt[2]), min(tt[3], tt[4]));
@@ -1700,6 +1790,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     if (cand_lpc) {
 #pragma unroll
         for (int j = 0; j < 64; j++) {
+            if (j % 8 == 0 && j) asm volatile("" : "+v"(sl));
             const uint32_t a = (uint32_t)abs(residual_at(E, CL, lshift, j, X(j)));
             if (j < kMaxLpc) sl += (l0 && j < ol) ? 0u : a;
             else sl += a;
@@ -1712,21 +1803,29 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         best_bits = 0;
         best_po = 0;
         my_k = 0;
-        uint64_t gsum = (uint64_t)lane_sum + (uint64_t)__shfl_xor(lane_sum, 1);
+        uint64_t gsum = (uint64_t)lane_sum;
+        gsum += bfly_partner64<1>(gsum);
 #pragma unroll
         for (int po = 5; po >= 0; po--) {
-            if (po < 5) gsum += __shfl_xor(gsum, 1 << (5 - po));
+            if (po == 4) gsum += bfly_partner64<2>(gsum);
+            if (po == 3) gsum += bfly_partner64<4>(gsum);
+            if (po == 2) gsum += bfly_partner64<8>(gsum);
+            if (po == 1) gsum += bfly_partner64<16>(gsum);
+            if (po == 0) gsum += bfly_partner64<32>(gsum);
             const int lanes_per = 64 >> po;
             const uint32_t pbase = (uint32_t)(n >> po);
-            const uint32_t ns = lane < lanes_per ? pbase - (uint32_t)order : pbase;
-            const uint32_t div = 0x40000u / ns;
+            const bool first = lane < lanes_per;
+            const uint32_t ns = first ? pbase - (uint32_t)order : pbase;
+            // 0x40000 / ns: a power of two for every partition but the first (scalar division for that one)
+            const uint32_t div_first = uni(0x40000u / (pbase - (uint32_t)order));
+            const uint32_t div = first ? div_first : (64u << po);
             const uint64_t prod = gsum >= 1 ? ((gsum - 1) * div) >> 18 : 0;
             uint32_t k = (gsum < 2 || prod == 0) ? 0u : (uint32_t)ilog2_u64(prod) + 1;
             if (k >= 15) k = 14;
             uint64_t pb = 4 + (uint64_t)(1 + k) * ns + (k ? (gsum >> (k - 1)) : (gsum << 1)) - (ns >> 1);
             if (pb > 0xFFFFFFFFull) pb = 0xFFFFFFFFull;
             const uint32_t contrib = ((lane & (lanes_per - 1)) == 0) ? (uint32_t)pb : 0u;
-            const uint32_t bits = 6 + wave_sum_u32(contrib);
+            const uint32_t bits = 6 + dpp_wave_sum_u32(contrib);
             if (best_bits == 0 || bits < best_bits) {
                 best_bits = bits;
                 best_po = po;
@@ -1804,7 +1903,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         lds_put_bits2(fbuf, hdr_bits, (uint32_t)(typecode << 1) | (w ? 1u : 0u), 8);
         if (w) lds_put_bits2(fbuf, hdr_bits + 8 + (uint32_t)(w - 1), 1, 1);
     }
-    hdr_bits = (uint32_t)__shfl((int)hdr_bits, 0);
+    hdr_bits = uni(hdr_bits);
     uint32_t pos = hdr_bits + 8 + (uint32_t)w;  // after the subframe header
     uint32_t end_bits;
     bool ok = true;
@@ -1861,14 +1960,16 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         uint32_t lens = 0;
 #pragma unroll
         for (int j = 0; j < 64; j++) {
+            if (j % 8 == 0 && j) asm volatile("" : "+v"(lens));
             const uint32_t u = zigzag(residual_at(E, C, shift, j, X(j)));
             uint32_t len = 1u + (uint32_t)k + (u >> k);
             if (j < kMaxLpc && l0 && j < o) len = 0;
             lens += len;
         }
         reg_fence(E);
-        const uint64_t excl = wave_excl_scan_u64(lens, lane);
-        const uint64_t total = (uint64_t)__shfl((long long)(excl + lens), 63);
+        const uint32_t incl = dpp_incl_scan_u32(lens);
+        const uint64_t excl = incl - lens;
+        const uint64_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         const uint64_t fin = (uint64_t)pos + 4ull * (uint64_t)(1 << po) + total;
         end_bits = (uint32_t)fin;
         if (fin + 64 > (uint64_t)kFrameWordsV3 * 32) ok = false;
@@ -1895,6 +1996,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         const uint32_t one = 1u << k, low = one - 1u;
 #pragma unroll
         for (int j = 0; j < 64; j++) {
+            if (j % 8 == 0 && j) asm volatile("" : "+v"(run));
             const uint32_t u = zigzag(residual_at(E, C, shift, j, X(j)));
             uint32_t q = u >> k, code = (u & low) | one, adv = q + 1 + (uint32_t)k;
             if (j < kMaxLpc && l0 && j < o) {
@@ -1929,40 +2031,70 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
             }
             end += tail;
         }
-        crc = gf_mulmod(c, g_xpow_bytes[body - end]);
-#pragma unroll
-        for (int o2 = 32; o2 > 0; o2 >>= 1) crc ^= __shfl_xor(crc, o2);
+        const uint32_t m = body - end;
+        crc = dpp_wave_xor_u32(gf_mulmod(gf_mulmod(c, S.xlo[m & 63]), S.xhi[m >> 6]));
         if (l0) lds_put_bits2(fbuf, body << 3, crc, 16);
     }
-    // ---- decoupled look-back for the exclusive prefix: the wave probes 64 predecessors per round
+    // ---- decoupled look-back for the exclusive prefix.  Done last (after packing and the CRC): waiting
+    //      any earlier stalls work that predecessors' progress would otherwise overlap (measured).  ~3 x 1024 frames are in flight, so the nearest
+    //      inclusive predecessor is typically hundreds of frames back: each round probes 256 predecessors
+    //      (4 per lane, lane-major by distance) in one memory round trip.
     uint64_t prefix = 0;
     if (P.ablate & 1) {
         prefix = (uint64_t)f * 8320;  // diagnostic: fixed slots, no waiting
     } else if (f > 0) {
+        constexpr int kPer = 1;
         int64_t hi = f - 1;
         uint64_t accum = 0;
         long spins = 0;
         while (true) {
-            const int64_t j = hi - lane;
-            uint64_t sv = kFlagIncl;  // before frame 0: inclusive 0
-            if (j >= 0) sv = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t flag = (uint32_t)(sv >> 62);
-            const uint64_t incl = __ballot(flag == 2);
-            const uint64_t zero = __ballot(flag == 0);
-            const int first = incl ? __builtin_ctzll(incl) : 64;  // nearest inclusive
-            const uint64_t need = first >= 63 ? ~0ull : ((2ull << first) - 1);
-            if (zero & need) {  // a needed predecessor has not published yet
-                if (++spins > (1l << 24)) {
+            uint64_t sv[kPer];
+#pragma unroll
+            for (int i = 0; i < kPer; i++) {
+                const int64_t j = hi - (int64_t)(lane * kPer + i);
+                sv[i] = kFlagIncl;  // before frame 0: inclusive 0
+                if (j >= 0) sv[i] = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            int my_first = kPer;  // first inclusive entry of this lane (by distance)
+#pragma unroll
+            for (int i = kPer - 1; i >= 0; i--)
+                if ((sv[i] >> 62) == 2) my_first = i;
+            const uint64_t has = __ballot(my_first < kPer);
+            const int fl = has ? __builtin_ctzll(has) : 64;  // lane holding the nearest inclusive
+            const int first_i = fl < 64 ? __builtin_amdgcn_readlane(my_first, fl) : kPer;
+            // entries at distance <= (fl, first_i) are needed
+            bool missing = false;
+            uint64_t mine = 0;
+#pragma unroll
+            for (int i = 0; i < kPer; i++) {
+                const bool need = lane < fl || (lane == fl && i <= first_i);
+                if (need) {
+                    missing |= (sv[i] >> 62) == 0;
+                    mine += sv[i] & kValMask;
+                }
+            }
+            if (__ballot(missing)) {  // a needed predecessor has not published yet
+                if (++spins > (1l << 22)) {
                     if (l0) atomicOr(err, 8);
                     break;
                 }
-                __builtin_amdgcn_s_sleep(1);
+                // back off: polling waves otherwise flood L2 with 64-lane status reads
+                if (spins < 4) __builtin_amdgcn_s_sleep(2);
+                else if (spins < 16) __builtin_amdgcn_s_sleep(8);
+                else __builtin_amdgcn_s_sleep(32);
                 continue;
             }
-            const uint64_t mine = (lane <= first) ? (sv & kValMask) : 0;
-            accum += wave_sum_u64(mine);
-            if (first < 64) break;
-            hi -= 64;
+            accum += dpp_wave_sum_u64(mine);
+            if (fl < 64) {
+                if ((P.ablate & 64) && l0) {
+                    atomicAdd(&g_lb_stats[0], 1ull);
+                    atomicAdd(&g_lb_stats[1], (unsigned long long)((f - 1 - hi) / (64 * kPer) + 1));
+                    atomicAdd(&g_lb_stats[2], (unsigned long long)spins);
+                    atomicAdd(&g_lb_stats[3], (unsigned long long)(f - 1 - hi + fl * kPer + first_i));
+                }
+                break;
+            }
+            hi -= 64 * kPer;
         }
         prefix = accum;
     }
@@ -2006,11 +2138,14 @@ template <int DT>
 __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *raster, EncodeParams P,
                                                   const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
                                                   const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap,
-                                                  int64_t *frame_off, uint64_t *status, int *ticket_ctr, int *err) {
+                                                  int64_t *frame_off, uint64_t *status, int *ticket_ctr, int *err,
+                                                  const int32_t *__restrict__ ftile) {
     __shared__ EncV3Shared S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int i = threadIdx.x; i < 1024; i += blockDim.x) (&S.crc4[0][0])[i] = (&c_crc16x4[0][0])[i];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) S.crc8[i] = c_crc8[i];
+    for (int i = threadIdx.x; i < 64; i += blockDim.x) S.xlo[i] = g_xpow_bytes[i];
+    for (int i = threadIdx.x; i < kXpowHi; i += blockDim.x) S.xhi[i] = g_xpow_bytes[64 * i];
     for (int i = threadIdx.x; i < 4 * kFrameWordsV3; i += blockDim.x) (&S.bits[0][0])[i] = 0;
     if (threadIdx.x == 0) S.lut_tile = -1;
     while (true) {
@@ -2018,7 +2153,7 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
         if (threadIdx.x == 0) {
             const int tk = atomicAdd(ticket_ctr, 1);
             S.ticket = tk;
-            S.want = ((int64_t)tk * 4 < P.nframes) ? tile_of_frame(tiles, P.ntiles, (int64_t)tk * 4) : -1;
+            S.want = ((int64_t)tk * 4 < P.nframes) ? ftile[(int64_t)tk * 4] : -1;
         }
         __syncthreads();
         const int64_t fbase = (int64_t)S.ticket * 4;
@@ -2037,7 +2172,7 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
         const int64_t f = fbase + wave;
         if (f < P.nframes)
             encode_frame_v3<DT>(raster, P, tiles, norms, luts, ana, arena, arena_cap, frame_off, status, err, S, want, f,
-                                lane);
+                                lane, ftile);
     }
 }
 
@@ -2277,10 +2412,13 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         FRS_HIP(ctx->luts.ensure(sizeof(int16_t) * (size_t)kLutCap * ntiles));
         FRS_HIP(ctx->status.ensure(sizeof(uint64_t) * (nframes + 1) + 64));
         k_build_lut<DT><<<ntiles, 256, 0, st>>>(dnorms, ctx->luts.as<int16_t>());
+        FRS_HIP(ctx->frame_tile.ensure(sizeof(int32_t) * nframes));
+        k_frame_tile<<<ntiles, 64, 0, st>>>(dtiles, ntiles, ctx->frame_tile.as<int32_t>());
         prof_begin(ctx, "analyze", &ev);
         k_analyze_v2<DT><<<(unsigned)((nframes + 255) / 256), 256, 0, st>>>(raster, P, dtiles, dnorms,
                                                                              ctx->luts.as<int16_t>(),
-                                                                             ctx->window.as<float>(), dana);
+                                                                             ctx->window.as<float>(), dana,
+                                                                             ctx->frame_tile.as<int32_t>());
         prof_end(ctx, "analyze", ev);
         uint64_t *dstatus = ctx->status.as<uint64_t>();
         int *ticket = reinterpret_cast<int *>(dstatus + nframes);
@@ -2293,9 +2431,20 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
             grid = std::min<int64_t>(grid, (nframes + 3) / 4);
             k_encode_v3<DT><<<(unsigned)grid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(), dana,
                                                             reinterpret_cast<uint8_t *>(arena_dev), arena_cap,
-                                                            ctx->frame_off.as<int64_t>(), dstatus, ticket, err_flag);
+                                                            ctx->frame_off.as<int64_t>(), dstatus, ticket, err_flag,
+                                                            ctx->frame_tile.as<int32_t>());
         }
         prof_end(ctx, "encode", ev);
+        if (P.ablate & 64) {
+            unsigned long long st4[4];
+            FRS_HIP(hipMemcpyFromSymbolAsync(st4, HIP_SYMBOL(g_lb_stats), sizeof(st4), 0, hipMemcpyDeviceToHost, st));
+            FRS_HIP(hipStreamSynchronize(st));
+            fprintf(stderr, "[lookback] frames %llu rounds/frame %.3f spins/frame %.3f dist/frame %.1f\n", st4[0],
+                    (double)st4[1] / std::max(1ull, st4[0]), (double)st4[2] / std::max(1ull, st4[0]),
+                    (double)st4[3] / std::max(1ull, st4[0]));
+            const unsigned long long z[4] = {0, 0, 0, 0};
+            FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lb_stats), z, sizeof(z), 0, hipMemcpyHostToDevice, st));
+        }
         k_fast_finish<<<(ntiles + 1 + 255) / 256, 256, 0, st>>>(ctx->frame_off.as<int64_t>(), dstatus, dtiles, ntiles,
                                                                nframes, ctx->tile_sizes.as<int64_t>());
         std::vector<TileNorm> hn(ntiles);
