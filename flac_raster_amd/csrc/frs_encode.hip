@@ -1676,369 +1676,66 @@ __device__ inline void reg_fence(uint32_t *E) {
     for (int m = 0; m < 36; m++) asm volatile("" : "+v"(E[m]));
 }
 
+// |a - b| + c on unsigned operands (v_sad_u32; the compiler does not form it from the pattern)
+__device__ inline uint32_t sad_u32(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_sad_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
+// OR a left-aligned code (its first bit in bit 31) into the bit buffer at bit position pos
+__device__ inline void lds_put_left(uint32_t *buf, uint32_t pos, uint32_t codeL) {
+    const uint32_t hi = __builtin_amdgcn_alignbit(0u, codeL, pos);  // codeL >> (pos & 31)
+    const uint32_t lo = __builtin_amdgcn_alignbit(codeL, 0u, pos);  // codeL << (32 - (pos & 31)); 0 if aligned
+    uint32_t *w = buf + (pos >> 5);
+    atomicOr(w, hi);
+    atomicOr(w + 1, lo);
+}
+
 __device__ inline uint32_t zigzag(int32_t r) { return ((uint32_t)r << 1) ^ (uint32_t)(r >> 31); }
 
-template <int DT>
-__device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const EncodeParams &P,
-                                       const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
-                                       const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap, int64_t *frame_off,
-                                       uint64_t *status, int *err, EncV3Shared &S, int want, int64_t f, int lane,
-                                       const int32_t *ftile) {
-    using T = typename Elem<DT>::T;
-    uint32_t *fbuf = S.bits[threadIdx.x >> 6];
-    const int t = ftile[f];
-    const TileGeom g = tiles[t];
-    const TileNorm tn = norms[t];
-    const int16_t *lut = (t == want) ? S.lut : luts + (int64_t)t * kLutCap;
-    const int64_t fk = f - g.frame_base;
-    const int64_t s0 = fk * kMaxBlock;
-    constexpr int n = kMaxBlock;
-    const SubAnalysis A = ana[f];
-    const int w = A.wasted;
-    const int sbps = 16 - w;
-    const T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
-
-    // ---- this lane's 64 samples, normalised and shifted, packed as int16 pairs E[4 + m] = (x[2m], x[2m+1]);
-    //      E[0..3] = the previous lane's last 8 samples (zeros on lane 0)
-    uint32_t E[36];
-    {
-        Chunk64<DT> ch;
-        ch.load(base, P.row_stride, g.w, s0 + 64 * lane, P.vec_ok && (g.w % 64) == 0, 64);
-        int32_t lo = 0;
-        norm_chunk<DT>(ch, tn, lut, [&](int j, int32_t x) {
-            if (j & 1) E[4 + (j >> 1)] = pack2(lo, x >> w);
-            else lo = x >> w;
-        });
-    }
-#pragma unroll
-    for (int m = 0; m < 4; m++) E[m] = dpp_wave_shr1(E[32 + m]);
-    reg_fence(E);  // keeps the load/normalise phase from overlapping the totals pass (VGPR peak)
-    auto X = [&](int j) -> int32_t {
-        const uint32_t v = E[4 + (j >> 1)];
-        return (j & 1) ? ((int32_t)v >> 16) : (int32_t)(int16_t)(v & 0xFFFFu);
-    };
-    const bool l0 = lane == 0;
-
-    // ---- fixed predictor totals over samples 4..n-1 (fixed.c FLAC__fixed_compute_best_predictor), the
-    //      constant test, and lane 0's warm-up extras wk = sum_{i=k}^{3} |e_k(i)| for the fixed partition sums
-    uint32_t lt[5] = {0, 0, 0, 0, 0}, wx[5] = {0, 0, 0, 0, 0};
-    uint32_t diff = 0;
-    const int32_t x0 = (int32_t)uni((uint32_t)(int32_t)(int16_t)(E[4] & 0xFFFFu));
-    {
-        const int32_t h1 = (int32_t)E[3] >> 16, h2 = (int16_t)(E[3] & 0xFFFFu);
-        const int32_t h3 = (int32_t)E[2] >> 16, h4 = (int16_t)(E[2] & 0xFFFFu);
-        int32_t a1 = h1, d1 = h1 - h2, d2 = (h1 - h2) - (h2 - h3), d3 = ((h1 - h2) - (h2 - h3)) - ((h2 - h3) - (h3 - h4));
-#pragma unroll
-        for (int j = 0; j < 64; j++) {
-            if (j % 8 == 0 && j) {  // bound the scheduler's look-ahead (VGPR peak)
-#pragma unroll
-                for (int k = 0; k < 5; k++) asm volatile("" : "+v"(lt[k]));
-                asm volatile("" : "+v"(a1), "+v"(d1), "+v"(d2), "+v"(d3));
-            }
-            const int32_t xi = X(j);
-            const int32_t e[5] = {xi, xi - a1, xi - a1 - d1, xi - a1 - d1 - d2, xi - a1 - d1 - d2 - d3};
-#pragma unroll
-            for (int k = 0; k < 5; k++) {
-                const uint32_t ae = (uint32_t)abs(e[k]);
-                if (j >= 4) lt[k] += ae;
-                else {
-                    lt[k] += l0 ? 0u : ae;
-                    if (j >= k) wx[k] += l0 ? ae : 0u;
-                }
-            }
-            diff |= (uint32_t)(xi ^ x0);
-            a1 = xi;
-            d1 = e[1];
-            d2 = e[2];
-            d3 = e[3];
-        }
-    }
-    reg_fence(E);
-    uint32_t tt[5];
-#pragma unroll
-    for (int k = 0; k < 5; k++) tt[k] = dpp_wave_sum_u32(lt[k]);
-    diff = dpp_wave_or_u32(diff);
-    int guess;
-    {
-        const uint32_t m = min(min(tt[1], tt[2]), min(tt[3], tt[4]));
-        if (tt[0] <= m) guess = 0;
-        else if (tt[1] <= min(min(tt[2], tt[3]), tt[4])) guess = 1;
-        else if (tt[2] <= min(tt[3], tt[4])) guess = 2;
-        else if (tt[3] <= tt[4]) guess = 3;
-        else guess = 4;
-    }
-    const double dn = (double)(n - 4);
-    uint32_t tg = tt[0], sf = lt[0] + wx[0];
-#pragma unroll
-    for (int k = 1; k < 5; k++)
-        if (guess == k) {
-            tg = tt[k];
-            sf = lt[k] + wx[k];
-        }
-    const float fb1 = (float)(tt[1] > 0 ? log(M_LN2 * (double)tt[1] / dn) / M_LN2 : 0.0);
-    const float fbg = (float)(tg > 0 ? log(M_LN2 * (double)tg / dn) / M_LN2 : 0.0);
-    const bool constant = fb1 == 0.0f && diff == 0;
-    const bool cand_fixed = !constant && !(fbg >= (float)sbps);
-    const bool cand_lpc = !constant && (A.flags & kFlagLpcOk);
-    const int of = guess, ol = A.lpc_order, lshift = A.lpc_shift;
-
-    uint32_t CL[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) CL[k] = pack2(A.q[2 * k + 1], A.q[2 * k]);
-    // ---- this lane's LPC |r| sum (residuals are recomputed by the later passes: cheaper than 64 live VGPRs)
-    uint32_t sl = 0;
-    if (cand_lpc) {
-#pragma unroll
-        for (int j = 0; j < 64; j++) {
-            if (j % 8 == 0 && j) asm volatile("" : "+v"(sl));
-            const uint32_t a = (uint32_t)abs(residual_at(E, CL, lshift, j, X(j)));
-            if (j < kMaxLpc) sl += (l0 && j < ol) ? 0u : a;
-            else sl += a;
-        }
-    }
-    reg_fence(E);
-    // ---- set_partitioned_rice_ (stream_encoder.c): orders 5..0, group sums merged by lane shuffles;
-    //      n = 4096 so max order is 5 for every predictor order <= 8
-    auto rice = [&](uint32_t lane_sum, int order, uint32_t &best_bits, int &best_po, int &my_k) {
-        best_bits = 0;
-        best_po = 0;
-        my_k = 0;
-        uint64_t gsum = (uint64_t)lane_sum;
-        gsum += bfly_partner64<1>(gsum);
-#pragma unroll
-        for (int po = 5; po >= 0; po--) {
-            if (po == 4) gsum += bfly_partner64<2>(gsum);
-            if (po == 3) gsum += bfly_partner64<4>(gsum);
-            if (po == 2) gsum += bfly_partner64<8>(gsum);
-            if (po == 1) gsum += bfly_partner64<16>(gsum);
-            if (po == 0) gsum += bfly_partner64<32>(gsum);
-            const int lanes_per = 64 >> po;
-            const uint32_t pbase = (uint32_t)(n >> po);
-            const bool first = lane < lanes_per;
-            const uint32_t ns = first ? pbase - (uint32_t)order : pbase;
-            // 0x40000 / ns: a power of two for every partition but the first (scalar division for that one)
-            const uint32_t div_first = uni(0x40000u / (pbase - (uint32_t)order));
-            const uint32_t div = first ? div_first : (64u << po);
-            const uint64_t prod = gsum >= 1 ? ((gsum - 1) * div) >> 18 : 0;
-            uint32_t k = (gsum < 2 || prod == 0) ? 0u : (uint32_t)ilog2_u64(prod) + 1;
-            if (k >= 15) k = 14;
-            uint64_t pb = 4 + (uint64_t)(1 + k) * ns + (k ? (gsum >> (k - 1)) : (gsum << 1)) - (ns >> 1);
-            if (pb > 0xFFFFFFFFull) pb = 0xFFFFFFFFull;
-            const uint32_t contrib = ((lane & (lanes_per - 1)) == 0) ? (uint32_t)pb : 0u;
-            const uint32_t bits = 6 + dpp_wave_sum_u32(contrib);
-            if (best_bits == 0 || bits < best_bits) {
-                best_bits = bits;
-                best_po = po;
-                my_k = (int)k;
-            }
-        }
-    };
-    uint32_t rb_f = 0, rb_l = 0;
-    int po_f = 0, po_l = 0, k_f = 0, k_l = 0;
-    if (cand_fixed) rice(sf, of, rb_f, po_f, k_f);
-    if (cand_lpc) rice(sl, ol, rb_l, po_l, k_l);
-    // ---- choose (process_subframe_: VERBATIM, then CONSTANT | FIXED, LPC; strict <)
-    uint32_t best = (uint32_t)(1 + 6 + 1 + w + n * sbps);
-    int type = 1;
-    if (constant) {
-        const uint32_t cb = (uint32_t)(1 + 6 + 1 + w + sbps);
-        if (cb < best) { best = cb; type = 0; }
-    } else {
-        if (cand_fixed) {
-            uint32_t est = (uint32_t)(1 + 6 + 1 + w + of * sbps);
-            est = (rb_f < 0xFFFFFFFFu - est) ? est + rb_f : 0xFFFFFFFFu;
-            if (est < best) { best = est; type = 2; }
-        }
-        if (cand_lpc) {
-            uint32_t est = (uint32_t)(1 + 6 + 1 + w + 4 + 5 + sbps * ol + A.lpc_prec * ol);
-            est = (rb_l < 0xFFFFFFFFu - est) ? est + rb_l : 0xFFFFFFFFu;
-            if (est != 0 && est < best) { best = est; type = 3; }
-        }
-    }
-    // ---- frame header + subframe header (lane 0; bytes go straight to LDS, CRC-8 on the fly)
-    uint32_t hdr_bits = 0;
-    if (l0) {
-        uint32_t hb = 0, c8 = 0;
-        auto put8 = [&](uint32_t b) {
-            lds_put_bits2(fbuf, hb << 3, b, 8);
-            c8 = S.crc8[c8 ^ b];
-            hb++;
-        };
-        const int sr = P.sample_rate;
-        int src, srx = 0;
-        switch (sr) {
-        case 88200: src = 1; break;
-        case 176400: src = 2; break;
-        case 192000: src = 3; break;
-        case 8000: src = 4; break;
-        case 16000: src = 5; break;
-        case 22050: src = 6; break;
-        case 24000: src = 7; break;
-        case 32000: src = 8; break;
-        case 44100: src = 9; break;
-        case 48000: src = 10; break;
-        case 96000: src = 11; break;
-        default:
-            if (sr <= 255000 && sr % 1000 == 0) src = srx = 12;
-            else if (sr % 10 == 0 && sr / 10 <= 65535) src = srx = 14;
-            else src = srx = 13;
-        }
-        put8(0xFF);
-        put8(0xF8);
-        put8((uint32_t)((12 << 4) | src));  // block size code 12 = 4096
-        put8((uint32_t)(4 << 1));           // mono, 16 bits
-        const uint32_t v = (uint32_t)fk;    // UTF-8 coded frame number
-        if (v < 0x80) put8(v);
-        else if (v < 0x800) { put8(0xC0 | (v >> 6)); put8(0x80 | (v & 0x3F)); }
-        else if (v < 0x10000) { put8(0xE0 | (v >> 12)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
-        else if (v < 0x200000) { put8(0xF0 | (v >> 18)); put8(0x80 | ((v >> 12) & 0x3F)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
-        else if (v < 0x4000000) { put8(0xF8 | (v >> 24)); put8(0x80 | ((v >> 18) & 0x3F)); put8(0x80 | ((v >> 12) & 0x3F)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
-        else { put8(0xFC | (v >> 30)); put8(0x80 | ((v >> 24) & 0x3F)); put8(0x80 | ((v >> 18) & 0x3F)); put8(0x80 | ((v >> 12) & 0x3F)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
-        if (srx == 12) put8((uint32_t)(sr / 1000));
-        else if (srx == 13) { put8((uint32_t)(sr >> 8) & 0xFF); put8((uint32_t)sr & 0xFF); }
-        else if (srx == 14) { put8((uint32_t)((sr / 10) >> 8) & 0xFF); put8((uint32_t)(sr / 10) & 0xFF); }
-        put8(c8);  // CRC-8 (the table lookup of the last call is unused)
-        hdr_bits = hb << 3;
-        const int typecode = type == 0 ? 0 : type == 1 ? 1 : type == 2 ? 8 + of : 32 + ol - 1;
-        lds_put_bits2(fbuf, hdr_bits, (uint32_t)(typecode << 1) | (w ? 1u : 0u), 8);
-        if (w) lds_put_bits2(fbuf, hdr_bits + 8 + (uint32_t)(w - 1), 1, 1);
-    }
-    hdr_bits = uni(hdr_bits);
-    uint32_t pos = hdr_bits + 8 + (uint32_t)w;  // after the subframe header
-    uint32_t end_bits;
+struct PendingFrame {  // a frame whose bytes sit in the wave's bit buffer, offset not yet resolved
+    int64_t f = -1;
+    uint64_t fbytes = 0;
     bool ok = true;
-    const uint32_t smask = (1u << sbps) - 1u;
-    // phase A: everything but the bulk sample/residual packing, ending with the exact frame size
-    uint32_t C[4];
-    int shift = lshift, k = 0, lanes_per = 64, p = 0, o = 0, po = 0;
-    uint32_t run = 0;
-    if (type == 0) {
-        if (l0) lds_put_bits2(fbuf, pos, (uint32_t)X(0) & smask, sbps);
-        end_bits = pos + (uint32_t)sbps;
-    } else if (type == 1) {
-        end_bits = pos + (uint32_t)n * sbps;
-    } else {
-        o = type == 2 ? of : ol;
-        po = type == 2 ? po_f : po_l;
-        k = type == 2 ? k_f : k_l;
-        lanes_per = 64 >> po;
-        p = lane / lanes_per;
-        if (type == 2) {
-            int32_t qf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (of == 1) qf[0] = 1;
-            else if (of == 2) { qf[0] = 2; qf[1] = -1; }
-            else if (of == 3) { qf[0] = 3; qf[1] = -3; qf[2] = 1; }
-            else if (of == 4) { qf[0] = 4; qf[1] = -6; qf[2] = 4; qf[3] = -1; }
-#pragma unroll
-            for (int m = 0; m < 4; m++) C[m] = pack2(qf[2 * m + 1], qf[2 * m]);
-            shift = 0;
-        } else {
-#pragma unroll
-            for (int m = 0; m < 4; m++) C[m] = CL[m];
-        }
-        if (l0) {
-#pragma unroll
-            for (int i = 0; i < kMaxLpc; i++)
-                if (i < o) lds_put_bits2(fbuf, pos + (uint32_t)i * sbps, (uint32_t)X(i) & smask, sbps);
-        }
-        pos += (uint32_t)o * sbps;
-        if (type == 3) {
-            if (l0) {
-                lds_put_bits2(fbuf, pos, (uint32_t)(A.lpc_prec - 1), 4);
-                lds_put_bits2(fbuf, pos + 4, (uint32_t)lshift & 31u, 5);
-#pragma unroll
-                for (int i = 0; i < kMaxLpc; i++)
-                    if (i < o)
-                        lds_put_bits2(fbuf, pos + 9 + (uint32_t)i * A.lpc_prec,
-                                      (uint32_t)A.q[i] & ((1u << A.lpc_prec) - 1u), A.lpc_prec);
-            }
-            pos += 9 + (uint32_t)o * A.lpc_prec;
-        }
-        if (l0) lds_put_bits2(fbuf, pos, (uint32_t)po, 6);  // RICE (00) + partition order (4 bits)
-        pos += 6;
-        // exact code lengths (masked warm-up samples: len 0)
-        uint32_t lens = 0;
-#pragma unroll
-        for (int j = 0; j < 64; j++) {
-            if (j % 8 == 0 && j) asm volatile("" : "+v"(lens));
-            const uint32_t u = zigzag(residual_at(E, C, shift, j, X(j)));
-            uint32_t len = 1u + (uint32_t)k + (u >> k);
-            if (j < kMaxLpc && l0 && j < o) len = 0;
-            lens += len;
-        }
-        reg_fence(E);
-        const uint32_t incl = dpp_incl_scan_u32(lens);
-        const uint64_t excl = incl - lens;
-        const uint64_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        const uint64_t fin = (uint64_t)pos + 4ull * (uint64_t)(1 << po) + total;
-        end_bits = (uint32_t)fin;
-        if (fin + 64 > (uint64_t)kFrameWordsV3 * 32) ok = false;
-        run = pos + 4u * (uint32_t)(p + 1) + (uint32_t)excl;
-        if (ok && (lane & (lanes_per - 1)) == 0) lds_put_bits2(fbuf, run - 4u, (uint32_t)k, 4);
+};
+
+__device__ inline void sample_rate_code(int sr, int &src, int &srx) {  // RFC 9639 9.1.2
+    srx = 0;
+    switch (sr) {
+    case 88200: src = 1; break;
+    case 176400: src = 2; break;
+    case 192000: src = 3; break;
+    case 8000: src = 4; break;
+    case 16000: src = 5; break;
+    case 22050: src = 6; break;
+    case 24000: src = 7; break;
+    case 32000: src = 8; break;
+    case 44100: src = 9; break;
+    case 48000: src = 10; break;
+    case 96000: src = 11; break;
+    default:
+        if (sr <= 255000 && sr % 1000 == 0) src = srx = 12;
+        else if (sr % 10 == 0 && sr / 10 <= 65535) src = srx = 14;
+        else src = srx = 13;
     }
-    if (!ok) {
-        if (l0) atomicOr(err, 2);
-        end_bits = 0;
-    }
-    const uint32_t body = (end_bits + 7) >> 3;  // bytes before the CRC-16 footer
-    const uint64_t fbytes = ok ? (uint64_t)body + 2 : 0;
-    // ---- publish our aggregate now, so successors' look-back resolves while we pack
-    if (l0) {
-        const uint64_t v = (f == 0 ? kFlagIncl : kFlagAgg) | fbytes;
-        __hip_atomic_store(&status[f], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // phase B: bulk packing
-    if (type == 1) {
-        const uint32_t p0 = pos + (uint32_t)(64 * lane) * (uint32_t)sbps;
-#pragma unroll
-        for (int j = 0; j < 64; j++) lds_put_bits2(fbuf, p0 + (uint32_t)j * sbps, (uint32_t)X(j) & smask, sbps);
-    } else if (type >= 2 && ok && !(P.ablate & 4)) {
-        const uint32_t one = 1u << k, low = one - 1u;
-#pragma unroll
-        for (int j = 0; j < 64; j++) {
-            if (j % 8 == 0 && j) asm volatile("" : "+v"(run));
-            const uint32_t u = zigzag(residual_at(E, C, shift, j, X(j)));
-            uint32_t q = u >> k, code = (u & low) | one, adv = q + 1 + (uint32_t)k;
-            if (j < kMaxLpc && l0 && j < o) {
-                q = 0;
-                code = 0;
-                adv = 0;
-            }
-            lds_put_bits2(fbuf, run + q, code, k + 1);
-            run += adv;
-        }
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS atomics have landed
-    __builtin_amdgcn_wave_barrier();
-    uint32_t crc = 0;
-    if (ok && !(P.ablate & 2)) {
-        // slice-by-4 over 32-bit words, one contiguous word range per lane, combined with x^(8m) factors
-        const uint32_t nfw = body >> 2, tail = body & 3;
-        const uint32_t cw = (nfw + 63) >> 6;
-        const uint32_t wb = min(nfw, (uint32_t)lane * cw), we = min(nfw, wb + cw);
-        uint32_t c = 0;
-        for (uint32_t i = wb; i < we; i++) {
-            const uint32_t word = fbuf[i];
-            c = (uint32_t)S.crc4[3][((c >> 8) ^ (word >> 24)) & 0xFF] ^ S.crc4[2][((c & 0xFF) ^ (word >> 16)) & 0xFF] ^
-                S.crc4[1][(word >> 8) & 0xFF] ^ S.crc4[0][word & 0xFF];
-        }
-        uint32_t end = we * 4;
-        if (lane == (int)((nfw - 1) / cw)) {
-            const uint32_t word = fbuf[nfw];
-            for (uint32_t b = 0; b < tail; b++) {
-                const uint32_t byte = (word >> (24 - 8 * b)) & 0xFF;
-                c = ((c << 8) & 0xFFFFu) ^ S.crc4[0][((c >> 8) ^ byte) & 0xFF];
-            }
-            end += tail;
-        }
-        const uint32_t m = body - end;
-        crc = dpp_wave_xor_u32(gf_mulmod(gf_mulmod(c, S.xlo[m & 63]), S.xhi[m >> 6]));
-        if (l0) lds_put_bits2(fbuf, body << 3, crc, 16);
-    }
-    // ---- decoupled look-back for the exclusive prefix.  Done last (after packing and the CRC): waiting
-    //      any earlier stalls work that predecessors' progress would otherwise overlap (measured).  ~3 x 1024 frames are in flight, so the nearest
-    //      inclusive predecessor is typically hundreds of frames back: each round probes 256 predecessors
-    //      (4 per lane, lane-major by distance) in one memory round trip.
+}
+
+// bytes of a fixed-blocksize (4096) frame header incl. CRC-8: sync/codes (4) + UTF-8 frame number + rate ext
+__device__ inline uint32_t frame_header_bytes(uint32_t v, int srx) {
+    const uint32_t u = v < 0x80 ? 1 : v < 0x800 ? 2 : v < 0x10000 ? 3 : v < 0x200000 ? 4 : v < 0x4000000 ? 5 : 6;
+    return 4 + u + (srx == 12 ? 1 : (srx == 13 || srx == 14) ? 2 : 0) + 1;
+}
+
+// Offset of a finished frame (decoupled look-back), inclusive publish, store of its bytes from the wave's
+// bit buffer, and re-zeroing of that buffer.
+__device__ inline void resolve_and_store(const EncodeParams &P, PendingFrame &pf, uint32_t *fbuf, uint8_t *arena,
+                                         int64_t arena_cap, int64_t *frame_off, uint64_t *status, int *err, int lane) {
+    const int64_t f = pf.f;
+    const uint64_t fbytes = pf.fbytes;
+    const bool ok = pf.ok;
+    const bool l0 = lane == 0;
+    // ---- decoupled look-back for the exclusive prefix (kPer predecessors per lane and round)
     uint64_t prefix = 0;
     if (P.ablate & 1) {
         prefix = (uint64_t)f * 8320;  // diagnostic: fixed slots, no waiting
@@ -2132,6 +1829,417 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     }
     // leave the bit buffer zeroed for this wave's next frame (LDS ops of one wave complete in order)
     for (uint32_t i = (uint32_t)lane; i < used_words; i += 64) fbuf[i] = 0;
+    pf.f = -1;
+}
+
+template <int DT>
+__device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const EncodeParams &P,
+                                       const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
+                                       const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap, int64_t *frame_off,
+                                       uint64_t *status, int *err, EncV3Shared &S, int want, int64_t f, int lane,
+                                       const int32_t *ftile, PendingFrame &prev) {
+    using T = typename Elem<DT>::T;
+    uint32_t *fbuf = S.bits[threadIdx.x >> 6];
+    const int t = ftile[f];
+    const TileGeom g = tiles[t];
+    TileNorm tn = norms[t];
+    // the WG's LDS LUT belongs to tile `want`; a frame of another tile takes the exact division instead
+    if (t != want && tn.mode == kNormLut) tn.mode = kNormSlow;
+    const int16_t *lut = S.lut;
+    const int64_t fk = f - g.frame_base;
+    const int64_t s0 = fk * kMaxBlock;
+    constexpr int n = kMaxBlock;
+    const SubAnalysis A = ana[f];
+    const int w = A.wasted;
+    const int sbps = 16 - w;
+    const T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
+
+    // ---- this lane's 64 samples, normalised and shifted, packed as int16 pairs E[4 + m] = (x[2m], x[2m+1]);
+    //      E[0..3] = the previous lane's last 8 samples (zeros on lane 0)
+    uint32_t E[36];
+    {
+        Chunk64<DT> ch;
+        ch.load(base, P.row_stride, g.w, s0 + 64 * lane, P.vec_ok && (g.w % 64) == 0, 64);
+        int32_t lo = 0;
+        norm_chunk<DT>(ch, tn, lut, [&](int j, int32_t x) {
+            if (j & 1) E[4 + (j >> 1)] = pack2(lo, x >> w);
+            else lo = x >> w;
+        });
+    }
+#pragma unroll
+    for (int m = 0; m < 4; m++) E[m] = dpp_wave_shr1(E[32 + m]);
+    reg_fence(E);  // keeps the load/normalise phase from overlapping the totals pass (VGPR peak)
+    auto X = [&](int j) -> int32_t {
+        const uint32_t v = E[4 + (j >> 1)];
+        return (j & 1) ? ((int32_t)v >> 16) : (int32_t)(int16_t)(v & 0xFFFFu);
+    };
+    const bool l0 = lane == 0;
+
+    // ---- fixed predictor totals over samples 4..n-1 (fixed.c FLAC__fixed_compute_best_predictor) and
+    //      lane 0's warm-up extras wk = sum_{i=k}^{3} |e_k(i)| for the fixed partition sums.  Differences are
+    //      carried sign-flipped (y = e ^ 2^31) so |e_{k+1}| = v_sad_u32(y_k(i), y_k(i-1)) in one op.
+    uint32_t lt[5] = {0, 0, 0, 0, 0}, wx[5] = {0, 0, 0, 0, 0};
+    {
+        constexpr uint32_t M = 0x80000000u;
+        const int32_t h1 = (int32_t)E[3] >> 16, h2 = (int16_t)(E[3] & 0xFFFFu);
+        const int32_t h3 = (int32_t)E[2] >> 16, h4 = (int16_t)(E[2] & 0xFFFFu);
+        // biased state of sample i-1: y0 = x, y1 = e1, y2 = e2, y3 = e3
+        uint32_t p0 = (uint32_t)h1 ^ M, p1 = (uint32_t)(h1 - h2) ^ M, p2 = (uint32_t)((h1 - h2) - (h2 - h3)) ^ M;
+        uint32_t p3 = (uint32_t)(((h1 - h2) - (h2 - h3)) - ((h2 - h3) - (h3 - h4))) ^ M;
+#pragma unroll
+        for (int j = 0; j < 64; j++) {
+            if (j % 8 == 0 && j) {  // bound the scheduler's look-ahead (VGPR peak)
+#pragma unroll
+                for (int k = 0; k < 5; k++) asm volatile("" : "+v"(lt[k]));
+                asm volatile("" : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3));
+            }
+            const uint32_t y0 = (uint32_t)X(j) ^ M;
+            const uint32_t y1 = (y0 - p0) ^ M;
+            const uint32_t y2 = (y1 - p1) ^ M;
+            const uint32_t y3 = (y2 - p2) ^ M;
+            if (j >= 4) {
+                lt[0] = sad_u32(y0, M, lt[0]);
+                lt[1] = sad_u32(y0, p0, lt[1]);
+                lt[2] = sad_u32(y1, p1, lt[2]);
+                lt[3] = sad_u32(y2, p2, lt[3]);
+                lt[4] = sad_u32(y3, p3, lt[4]);
+            } else {
+                const uint32_t ae[5] = {sad_u32(y0, M, 0), sad_u32(y0, p0, 0), sad_u32(y1, p1, 0), sad_u32(y2, p2, 0),
+                                        sad_u32(y3, p3, 0)};
+#pragma unroll
+                for (int k = 0; k < 5; k++) {
+                    lt[k] += l0 ? 0u : ae[k];
+                    if (j >= k) wx[k] += l0 ? ae[k] : 0u;
+                }
+            }
+            p0 = y0;
+            p1 = y1;
+            p2 = y2;
+            p3 = y3;
+        }
+    }
+    reg_fence(E);
+    uint32_t tt[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) tt[k] = dpp_wave_sum_u32(lt[k]);
+    int guess;
+    {
+        const uint32_t m = min(min(tt[1], tt[2]), min(tt[3], tt[4]));
+        if (tt[0] <= m) guess = 0;
+        else if (tt[1] <= min(min(tt[2], tt[3]), tt[4])) guess = 1;
+        else if (tt[2] <= min(tt[3], tt[4])) guess = 2;
+        else if (tt[3] <= tt[4]) guess = 3;
+        else guess = 4;
+    }
+    const double dn = (double)(n - 4);
+    uint32_t tg = tt[0], sf = lt[0] + wx[0];
+#pragma unroll
+    for (int k = 1; k < 5; k++)
+        if (guess == k) {
+            tg = tt[k];
+            sf = lt[k] + wx[k];
+        }
+    const float fb1 = (float)(tt[1] > 0 ? log(M_LN2 * (double)tt[1] / dn) / M_LN2 : 0.0);
+    const float fbg = (float)(tg > 0 ? log(M_LN2 * (double)tg / dn) / M_LN2 : 0.0);
+    // constant test (all samples equal) only where libFLAC reaches it: fixed bits[1] == 0
+    bool constant = false;
+    if (fb1 == 0.0f) {
+        reg_fence(E);
+        const uint32_t x0 = uni(E[4] & 0xFFFFu);
+        const uint32_t xx = x0 | (x0 << 16);  // both halves of a packed pair equal to sample 0
+        uint32_t diff = 0;
+#pragma unroll
+        for (int m = 4; m < 36; m++) diff |= E[m] ^ xx;
+        constant = dpp_wave_or_u32(diff) == 0;
+    }
+    const bool cand_fixed = !constant && !(fbg >= (float)sbps);
+    const bool cand_lpc = !constant && (A.flags & kFlagLpcOk);
+    const int of = guess, ol = A.lpc_order, lshift = A.lpc_shift;
+
+    uint32_t CL[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) CL[k] = pack2(A.q[2 * k + 1], A.q[2 * k]);
+    // ---- this lane's LPC |r| sum (residuals are recomputed by the later passes: cheaper than 64 live VGPRs)
+    uint32_t sl = 0;
+    if (cand_lpc) {
+#pragma unroll
+        for (int j = 0; j < 64; j++) {
+            if (j % 8 == 0 && j) asm volatile("" : "+v"(sl));
+            const uint32_t a = (uint32_t)abs(residual_at(E, CL, lshift, j, X(j)));
+            if (j < kMaxLpc) sl += (l0 && j < ol) ? 0u : a;
+            else sl += a;
+        }
+    }
+    reg_fence(E);
+    // ---- set_partitioned_rice_ (stream_encoder.c): orders 5..0, group sums merged by lane shuffles;
+    //      n = 4096 so max order is 5 for every predictor order <= 8
+    auto rice64 = [&](uint32_t lane_sum, int order, uint32_t &best_bits, int &best_po, int &my_k) {
+        best_bits = 0;
+        best_po = 0;
+        my_k = 0;
+        uint64_t gsum = (uint64_t)lane_sum;
+        gsum += bfly_partner64<1>(gsum);
+#pragma unroll
+        for (int po = 5; po >= 0; po--) {
+            if (po == 4) gsum += bfly_partner64<2>(gsum);
+            if (po == 3) gsum += bfly_partner64<4>(gsum);
+            if (po == 2) gsum += bfly_partner64<8>(gsum);
+            if (po == 1) gsum += bfly_partner64<16>(gsum);
+            if (po == 0) gsum += bfly_partner64<32>(gsum);
+            const int lanes_per = 64 >> po;
+            const uint32_t pbase = (uint32_t)(n >> po);
+            const bool first = lane < lanes_per;
+            const uint32_t ns = first ? pbase - (uint32_t)order : pbase;
+            // 0x40000 / ns: a power of two for every partition but the first (scalar division for that one)
+            const uint32_t div_first = uni(0x40000u / (pbase - (uint32_t)order));
+            const uint32_t div = first ? div_first : (64u << po);
+            const uint64_t prod = gsum >= 1 ? ((gsum - 1) * div) >> 18 : 0;
+            uint32_t k = (gsum < 2 || prod == 0) ? 0u : (uint32_t)ilog2_u64(prod) + 1;
+            if (k >= 15) k = 14;
+            uint64_t pb = 4 + (uint64_t)(1 + k) * ns + (k ? (gsum >> (k - 1)) : (gsum << 1)) - (ns >> 1);
+            if (pb > 0xFFFFFFFFull) pb = 0xFFFFFFFFull;
+            const uint32_t contrib = ((lane & (lanes_per - 1)) == 0) ? (uint32_t)pb : 0u;
+            const uint32_t bits = 6 + dpp_wave_sum_u32(contrib);
+            if (best_bits == 0 || bits < best_bits) {
+                best_bits = bits;
+                best_po = po;
+                my_k = (int)k;
+            }
+        }
+    };
+    // 32-bit form of the same search, exact when every lane sum is < 2^24 (group sums < 2^30): the division
+    // by a non-first partition's size is a shift, and k ? s >> (k-1) : s << 1 == (2s) >> k
+    auto rice32 = [&](uint32_t lane_sum, int order, uint32_t &best_bits, int &best_po, int &my_k) {
+        best_bits = 0;
+        best_po = 0;
+        my_k = 0;
+        uint32_t g = lane_sum;
+        g += bfly_partner<1>(g);
+#pragma unroll
+        for (int po = 5; po >= 0; po--) {
+            if (po == 4) g += bfly_partner<2>(g);
+            if (po == 3) g += bfly_partner<4>(g);
+            if (po == 2) g += bfly_partner<8>(g);
+            if (po == 1) g += bfly_partner<16>(g);
+            if (po == 0) g += bfly_partner<32>(g);
+            const int lanes_per = 64 >> po;
+            const uint32_t pbase = (uint32_t)(n >> po);
+            const bool first = lane < lanes_per;
+            const uint32_t ns = first ? pbase - (uint32_t)order : pbase;
+            const uint32_t div_first = uni(0x40000u / (pbase - (uint32_t)order));
+            const uint32_t pf = (uint32_t)(((uint64_t)(g - 1u) * div_first) >> 18);
+            const uint32_t pr = (g - 1u) >> (12 - po);
+            const uint32_t prod = first ? pf : pr;
+            uint32_t k = (g < 2 || prod == 0) ? 0u : 32u - (uint32_t)__builtin_clz(prod);
+            k = min(k, 14u);
+            const uint32_t pb = 4 + (1 + k) * ns + ((2 * g) >> k) - (ns >> 1);
+            const uint32_t contrib = ((lane & (lanes_per - 1)) == 0) ? pb : 0u;
+            const uint32_t bits = 6 + dpp_wave_sum_u32(contrib);
+            if (best_bits == 0 || bits < best_bits) {
+                best_bits = bits;
+                best_po = po;
+                my_k = (int)k;
+            }
+        }
+    };
+    auto rice = [&](uint32_t lane_sum, int order, uint32_t &best_bits, int &best_po, int &my_k) {
+        if (__ballot(lane_sum >= (1u << 24)) == 0) rice32(lane_sum, order, best_bits, best_po, my_k);
+        else rice64(lane_sum, order, best_bits, best_po, my_k);
+    };
+    uint32_t rb_f = 0, rb_l = 0;
+    int po_f = 0, po_l = 0, k_f = 0, k_l = 0;
+    if (cand_fixed) rice(sf, of, rb_f, po_f, k_f);
+    if (cand_lpc) rice(sl, ol, rb_l, po_l, k_l);
+    // ---- choose (process_subframe_: VERBATIM, then CONSTANT | FIXED, LPC; strict <)
+    uint32_t best = (uint32_t)(1 + 6 + 1 + w + n * sbps);
+    int type = 1;
+    if (constant) {
+        const uint32_t cb = (uint32_t)(1 + 6 + 1 + w + sbps);
+        if (cb < best) { best = cb; type = 0; }
+    } else {
+        if (cand_fixed) {
+            uint32_t est = (uint32_t)(1 + 6 + 1 + w + of * sbps);
+            est = (rb_f < 0xFFFFFFFFu - est) ? est + rb_f : 0xFFFFFFFFu;
+            if (est < best) { best = est; type = 2; }
+        }
+        if (cand_lpc) {
+            uint32_t est = (uint32_t)(1 + 6 + 1 + w + 4 + 5 + sbps * ol + A.lpc_prec * ol);
+            est = (rb_l < 0xFFFFFFFFu - est) ? est + rb_l : 0xFFFFFFFFu;
+            if (est != 0 && est < best) { best = est; type = 3; }
+        }
+    }
+    // ---- phase A: sizes only (no writes to the bit buffer, which still holds the previous frame)
+    int src, srx;
+    sample_rate_code(P.sample_rate, src, srx);
+    const uint32_t hb = frame_header_bytes((uint32_t)fk, srx);
+    const uint32_t hdr_bits = hb << 3;
+    const uint32_t pos0 = hdr_bits + 8 + (uint32_t)w;  // after the subframe header
+    uint32_t pos = pos0;
+    uint32_t end_bits;
+    bool ok = true;
+    uint32_t C[4];
+    int shift = lshift, k = 0, lanes_per = 64, p = 0, o = 0, po = 0;
+    uint32_t run = 0;
+    if (type == 0) {
+        end_bits = pos + (uint32_t)sbps;
+    } else if (type == 1) {
+        end_bits = pos + (uint32_t)n * sbps;
+    } else {
+        o = type == 2 ? of : ol;
+        po = type == 2 ? po_f : po_l;
+        k = type == 2 ? k_f : k_l;
+        lanes_per = 64 >> po;
+        p = lane / lanes_per;
+        if (type == 2) {
+            int32_t qf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (of == 1) qf[0] = 1;
+            else if (of == 2) { qf[0] = 2; qf[1] = -1; }
+            else if (of == 3) { qf[0] = 3; qf[1] = -3; qf[2] = 1; }
+            else if (of == 4) { qf[0] = 4; qf[1] = -6; qf[2] = 4; qf[3] = -1; }
+#pragma unroll
+            for (int m = 0; m < 4; m++) C[m] = pack2(qf[2 * m + 1], qf[2 * m]);
+            shift = 0;
+        } else {
+#pragma unroll
+            for (int m = 0; m < 4; m++) C[m] = CL[m];
+        }
+        pos += (uint32_t)o * sbps;
+        if (type == 3) pos += 9 + (uint32_t)o * A.lpc_prec;
+        pos += 6;
+        // exact code lengths (masked warm-up samples: len 0)
+        uint32_t lens = 0;
+#pragma unroll
+        for (int j = 0; j < 64; j++) {
+            if (j % 8 == 0 && j) asm volatile("" : "+v"(lens));
+            const uint32_t u = zigzag(residual_at(E, C, shift, j, X(j)));
+            uint32_t len = 1u + (uint32_t)k + (u >> k);
+            if (j < kMaxLpc && l0 && j < o) len = 0;
+            lens += len;
+        }
+        reg_fence(E);
+        const uint32_t incl = dpp_incl_scan_u32(lens);
+        const uint64_t excl = incl - lens;
+        const uint64_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        const uint64_t fin = (uint64_t)pos + 4ull * (uint64_t)(1 << po) + total;
+        end_bits = (uint32_t)fin;
+        if (fin + 64 > (uint64_t)kFrameWordsV3 * 32) ok = false;
+        run = pos + 4u * (uint32_t)(p + 1) + (uint32_t)excl;
+    }
+    if (!ok) {
+        if (l0) atomicOr(err, 2);
+        end_bits = 0;
+    }
+    const uint32_t body = (end_bits + 7) >> 3;  // bytes before the CRC-16 footer
+    const uint64_t fbytes = ok ? (uint64_t)body + 2 : 0;
+    if (l0) {  // publish our aggregate
+        const uint64_t v = (f == 0 ? kFlagIncl : kFlagAgg) | fbytes;
+        __hip_atomic_store(&status[f], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // ---- the previous frame of this wave: its predecessors have had a whole phase A to publish, so the
+    //      look-back rarely waits; store it and free the bit buffer
+    if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
+    reg_fence(E);
+    // ---- phase B: every bit of this frame into the (zeroed) buffer, then the CRC-16
+    if (l0) {
+        uint32_t hbits = 0, c8 = 0;
+        auto put8 = [&](uint32_t b) {
+            lds_put_bits2(fbuf, hbits, b, 8);
+            c8 = S.crc8[c8 ^ b];
+            hbits += 8;
+        };
+        const int sr = P.sample_rate;
+        put8(0xFF);
+        put8(0xF8);
+        put8((uint32_t)((12 << 4) | src));  // block size code 12 = 4096
+        put8((uint32_t)(4 << 1));           // mono, 16 bits
+        const uint32_t v = (uint32_t)fk;    // UTF-8 coded frame number
+        if (v < 0x80) put8(v);
+        else if (v < 0x800) { put8(0xC0 | (v >> 6)); put8(0x80 | (v & 0x3F)); }
+        else if (v < 0x10000) { put8(0xE0 | (v >> 12)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
+        else if (v < 0x200000) { put8(0xF0 | (v >> 18)); put8(0x80 | ((v >> 12) & 0x3F)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
+        else if (v < 0x4000000) { put8(0xF8 | (v >> 24)); put8(0x80 | ((v >> 18) & 0x3F)); put8(0x80 | ((v >> 12) & 0x3F)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
+        else { put8(0xFC | (v >> 30)); put8(0x80 | ((v >> 24) & 0x3F)); put8(0x80 | ((v >> 18) & 0x3F)); put8(0x80 | ((v >> 12) & 0x3F)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
+        if (srx == 12) put8((uint32_t)(sr / 1000));
+        else if (srx == 13) { put8((uint32_t)(sr >> 8) & 0xFF); put8((uint32_t)sr & 0xFF); }
+        else if (srx == 14) { put8((uint32_t)((sr / 10) >> 8) & 0xFF); put8((uint32_t)(sr / 10) & 0xFF); }
+        put8(c8);  // CRC-8 (the table lookup of the last call is unused)
+        const int typecode = type == 0 ? 0 : type == 1 ? 1 : type == 2 ? 8 + of : 32 + ol - 1;
+        lds_put_bits2(fbuf, hdr_bits, (uint32_t)(typecode << 1) | (w ? 1u : 0u), 8);
+        if (w) lds_put_bits2(fbuf, hdr_bits + 8 + (uint32_t)(w - 1), 1, 1);
+        const uint32_t smask = (1u << sbps) - 1u;
+        if (type == 0) lds_put_bits2(fbuf, pos0, (uint32_t)X(0) & smask, sbps);
+        if (type >= 2) {
+            uint32_t q = pos0;
+#pragma unroll
+            for (int i = 0; i < kMaxLpc; i++)
+                if (i < o) lds_put_bits2(fbuf, q + (uint32_t)i * sbps, (uint32_t)X(i) & smask, sbps);
+            q += (uint32_t)o * sbps;
+            if (type == 3) {
+                lds_put_bits2(fbuf, q, (uint32_t)(A.lpc_prec - 1), 4);
+                lds_put_bits2(fbuf, q + 4, (uint32_t)lshift & 31u, 5);
+#pragma unroll
+                for (int i = 0; i < kMaxLpc; i++)
+                    if (i < o)
+                        lds_put_bits2(fbuf, q + 9 + (uint32_t)i * A.lpc_prec,
+                                      (uint32_t)A.q[i] & ((1u << A.lpc_prec) - 1u), A.lpc_prec);
+                q += 9 + (uint32_t)o * A.lpc_prec;
+            }
+            lds_put_bits2(fbuf, q, (uint32_t)po, 6);  // RICE (00) + partition order (4 bits)
+        }
+    }
+    if (type >= 2 && ok && (lane & (lanes_per - 1)) == 0) lds_put_bits2(fbuf, run - 4u, (uint32_t)k, 4);
+    if (type == 1) {
+        const uint32_t p0 = pos + (uint32_t)(64 * lane) * (uint32_t)sbps;
+        const uint32_t shl = 32u - (uint32_t)sbps;
+#pragma unroll
+        for (int j = 0; j < 64; j++) lds_put_left(fbuf, p0 + (uint32_t)j * sbps, (uint32_t)X(j) << shl);
+    } else if (type >= 2 && ok && !(P.ablate & 4)) {
+        // code = stop bit + k low bits, left-aligned: (u << (31 - k)) with the stop bit forced on
+        const uint32_t sh = 31u - (uint32_t)k, oneL = 0x80000000u, lowL = (k ? (0xFFFFFFFFu >> (32 - k)) : 0u) << sh;
+#pragma unroll
+        for (int j = 0; j < 64; j++) {
+            if (j % 8 == 0 && j) asm volatile("" : "+v"(run));
+            const uint32_t u = zigzag(residual_at(E, C, shift, j, X(j)));
+            uint32_t q = u >> k, codeL = ((u << sh) & lowL) | oneL, adv = q + 1 + (uint32_t)k;
+            if (j < kMaxLpc && l0 && j < o) {
+                q = 0;
+                codeL = 0;
+                adv = 0;
+            }
+            lds_put_left(fbuf, run + q, codeL);
+            run += adv;
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS atomics have landed
+    __builtin_amdgcn_wave_barrier();
+    uint32_t crc = 0;
+    if (ok && !(P.ablate & 2)) {
+        // slice-by-4 over 32-bit words, one contiguous word range per lane, combined with x^(8m) factors
+        const uint32_t nfw = body >> 2, tail = body & 3;
+        const uint32_t cw = (nfw + 63) >> 6;
+        const uint32_t wb = min(nfw, (uint32_t)lane * cw), we = min(nfw, wb + cw);
+        uint32_t c = 0;
+        for (uint32_t i = wb; i < we; i++) {
+            const uint32_t word = fbuf[i];
+            c = (uint32_t)S.crc4[3][((c >> 8) ^ (word >> 24)) & 0xFF] ^ S.crc4[2][((c & 0xFF) ^ (word >> 16)) & 0xFF] ^
+                S.crc4[1][(word >> 8) & 0xFF] ^ S.crc4[0][word & 0xFF];
+        }
+        uint32_t end = we * 4;
+        if (lane == (int)((nfw - 1) / cw)) {
+            const uint32_t word = fbuf[nfw];
+            for (uint32_t b = 0; b < tail; b++) {
+                const uint32_t byte = (word >> (24 - 8 * b)) & 0xFF;
+                c = ((c << 8) & 0xFFFFu) ^ S.crc4[0][((c >> 8) ^ byte) & 0xFF];
+            }
+            end += tail;
+        }
+        const uint32_t m = body - end;
+        crc = dpp_wave_xor_u32(gf_mulmod(gf_mulmod(c, S.xlo[m & 63]), S.xhi[m >> 6]));
+        if (l0) lds_put_bits2(fbuf, body << 3, crc, 16);
+    }
+    prev.f = f;
+    prev.fbytes = fbytes;
+    prev.ok = ok;
 }
 
 template <int DT>
@@ -2148,6 +2256,8 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
     for (int i = threadIdx.x; i < kXpowHi; i += blockDim.x) S.xhi[i] = g_xpow_bytes[64 * i];
     for (int i = threadIdx.x; i < 4 * kFrameWordsV3; i += blockDim.x) (&S.bits[0][0])[i] = 0;
     if (threadIdx.x == 0) S.lut_tile = -1;
+    PendingFrame prev;
+    uint32_t *fbuf = S.bits[wave];
     while (true) {
         __syncthreads();  // previous ticket's readers of S.ticket / S.lut are done
         if (threadIdx.x == 0) {
@@ -2172,8 +2282,9 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
         const int64_t f = fbase + wave;
         if (f < P.nframes)
             encode_frame_v3<DT>(raster, P, tiles, norms, luts, ana, arena, arena_cap, frame_off, status, err, S, want, f,
-                                lane, ftile);
+                                lane, ftile, prev);
     }
+    if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
 }
 
 __global__ void k_fast_finish(const int64_t *frame_off, const uint64_t *status, const TileGeom *tiles, int ntiles,
