@@ -31,6 +31,9 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E peak 8.0 TB/s
+METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"] if (ROOT / "BASELINE.json").exists() else \
+    "Mpixels/sec encode (create-streaming) + bbox-extract ms, 1/2/4/8 GPU; bit-exact vs ref"
+KERNEL_SYMBOL = {"encode": "frs::k_encode_v3<3>", "analyze": "frs::k_analyze_v2<3>", "stats": "frs::k_tile_stats_vec<3>"}
 
 
 def parse():
@@ -42,10 +45,11 @@ def parse():
     ap.add_argument("--width", type=int, default=40000)
     ap.add_argument("--bands", type=int, default=4)
     ap.add_argument("--tile", type=int, default=512)
-    ap.add_argument("--cpu-tiles", type=int, default=316, help="tiles in the CPU-baseline sample")
+    ap.add_argument("--cpu-tiles", type=int, default=632, help="tiles in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--traffic", type=float, default=None, help="measured HBM bytes per encode launch (PMC)")
+    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
+                    help="tools/pmc_traffic.py output of a rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE pass of this bench")
     return ap.parse_args()
 
 
@@ -134,6 +138,7 @@ def main():
         total_px = rows * W
 
     kernels = {k: ctx.profile_avg_ms(k) for k in ("stats", "analyze", "encode", "compact")}
+    kernels = {k: v for k, v in kernels.items() if v > 0}
     comp_bytes = int(off[-1])
     px_rank = rows * W
     # algorithmic bytes per launch: stats reads 2 B/px; analyze reads 2 B/px; encode reads
@@ -147,7 +152,7 @@ def main():
     value = total_px / (elapsed / args.steps) / 1e6
 
     result = {
-        "metric": "Mpixels/sec encode (create-streaming), band-1 tiles of a 40000x40000x4 int16 raster, tile 512, level 5",
+        "metric": METRIC,
         "value": round(value, 1),
         "unit": "Mpixels/s",
         "n_gpus": world,
@@ -165,7 +170,7 @@ def main():
         "kernels_ms": {k: round(v, 4) for k, v in kernels.items()},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": args.traffic},
+                     "traffic": traffic_for(args.traffic_json, dom, px_rank)},
     }
 
     if rank == 0 and not args.no_cpu:
@@ -175,6 +180,19 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def traffic_for(path, kernel, px):
+    """HBM bytes per launch of `kernel` from a committed PMC summary (tools/pmc_traffic.py) measured on this
+    same workload (C4 slab of `px` pixels); None when absent or taken on another workload."""
+    try:
+        d = json.loads(Path(path).read_text())
+    except (OSError, ValueError):
+        return None
+    if d.get("pixels_per_launch") not in (None, px):
+        return None
+    k = d.get("kernels", {}).get(KERNEL_SYMBOL.get(kernel, kernel))
+    return None if k is None else round(k["bytes"])
 
 
 def cpu_baseline(ctx, raster, rows, W, T, off, arena, args):

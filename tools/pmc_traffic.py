@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""HBM traffic per kernel launch from rocprofv3 --pmc passes (run_counter_collection.csv).
+
+Usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json [--label TEXT] [--pixels PIXELS_PER_LAUNCH]
+
+FETCH_SIZE and WRITE_SIZE are in KB per dispatch (summed over TCC instances here).  On gfx950 FETCH_SIZE
+counts half the bytes of wide streaming reads, so it is doubled (MI355X_MICROARCH.md, "HBM [CDNA4]");
+WRITE_SIZE is taken as is.  The JSON maps kernel short names to mean bytes per launch, and bench.py copies
+the dominant kernel's figure into roofline.traffic.
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+
+def per_dispatch(d, counter):
+    vals = defaultdict(float)
+    names = {}
+    for f in Path(d).rglob("run_counter_collection.csv"):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if r["Counter_Name"] != counter:
+                    continue
+                vals[r["Dispatch_Id"]] += float(r["Counter_Value"])
+                names[r["Dispatch_Id"]] = r["Kernel_Name"].split("(")[0].replace("void ", "")
+    out = defaultdict(list)
+    for k, v in vals.items():
+        out[names[k]].append(v)
+    return {k: sum(v) / len(v) for k, v in out.items()}
+
+
+def main():
+    fetch, write, dst = sys.argv[1], sys.argv[2], sys.argv[3]
+    label = sys.argv[sys.argv.index("--label") + 1] if "--label" in sys.argv else ""
+    pixels = int(sys.argv[sys.argv.index("--pixels") + 1]) if "--pixels" in sys.argv else None
+    fr = per_dispatch(fetch, "FETCH_SIZE")
+    wr = per_dispatch(write, "WRITE_SIZE")
+    kernels = {}
+    for k in sorted(set(fr) | set(wr)):
+        rd = 2 * fr.get(k, 0.0) * 1024
+        wb = wr.get(k, 0.0) * 1024
+        kernels[k] = {"read_bytes": rd, "write_bytes": wb, "bytes": rd + wb}
+    json.dump({"label": label, "pixels_per_launch": pixels, "fetch_correction": 2.0, "kernels": kernels},
+              open(dst, "w"), indent=1)
+    for k, v in kernels.items():
+        print(f"{k}: read {v['read_bytes'] / 1e9:.3f} GB write {v['write_bytes'] / 1e9:.3f} GB")
+
+
+if __name__ == "__main__":
+    main()
