@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--cpu-tiles", type=int, default=632, help="tiles in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--queries", type=int, default=1000, help="C5 bbox-extract queries (0: skip)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                     help="tools/pmc_traffic.py output of a rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE pass of this bench")
     return ap.parse_args()
@@ -104,10 +105,10 @@ def main():
             gathered = [torch.empty_like(mine) for _ in range(world)]
             dist.all_gather(gathered, mine)
             torch.cuda.synchronize()
-        return off
+        return off, mn, mx
 
     for _ in range(args.warmup):
-        off = step()
+        off, mn, mx = step()
 
     def barrier():
         if dist is not None:
@@ -121,7 +122,7 @@ def main():
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        off = step()
+        off, mn, mx = step()
     barrier()
     t1 = time.perf_counter()
     ctx.profile(False)
@@ -173,6 +174,8 @@ def main():
                      "traffic": traffic_for(args.traffic_json, dom, px_rank)},
     }
 
+    if rank == 0 and args.queries > 0:
+        result["bbox_extract"] = bbox_extract(ctx, raster, arena, off, mn, mx, rows, W, T, args.queries)
     if rank == 0 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(ctx, raster, rows, W, T, off, arena, args)
     if rank == 0:
@@ -180,6 +183,62 @@ def main():
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def bbox_extract(ctx, raster, arena, off, tmin, tmax, rows, W, T, nq):
+    """C5: `nq` bbox queries against the streaming data this rank just encoded, device
+    resident.  Query = uniform tile-aligned centre, side U[0.1, 2.0] * tile_size * pixel (10 m,
+    from_origin(500000, 4000000, 10, 10)), clipped to the raster; end-to-end latency = selection (first
+    intersecting tile, cli.py:976-987) + decode of that tile's frames + de-normalisation + copy of the
+    tile to host memory.  The decoded tiles are checked against the raster (the C4 round trip is
+    lossless)."""
+    from flac_raster_amd import geotiff, streaming
+
+    tr = geotiff.Affine(10.0, 0.0, 500000.0, 0.0, -10.0, 4000000.0)
+    grid = streaming.tile_grid(rows, W, T)
+    frames = []
+    for i, (col, row, w, h) in enumerate(grid):
+        _, bb = streaming.tile_transform_and_bbox(tr, col, row, w, h)
+        frames.append({"frame_id": i, "bbox": bb, "window": {"col_off": col, "row_off": row, "width": w, "height": h},
+                       "byte_offset": int(off[i]), "byte_size": int(off[i + 1] - off[i])})
+    index = {"transform": list(tr) + [0.0, 0.0, 1.0], "width": W, "height": rows, "tile_size": T, "frames": frames}
+    left, top = 500000.0, 4000000.0
+    right, bottom = left + W * 10.0, top - rows * 10.0
+    rng = np.random.default_rng(7)
+    pcm = ctx.alloc(T * T * 4)
+    out = ctx.alloc(T * T * 2)
+    host = np.empty(T * T, dtype=np.int16)
+    lat = []
+    checked, lossless = 0, True
+    for q in range(nq + 10):  # 10 untimed warm-up queries
+        col, row, w, h = grid[int(rng.integers(len(grid)))]
+        cx, cy = left + (col + w / 2) * 10.0, top - (row + h / 2) * 10.0
+        half = rng.uniform(0.1, 2.0) * T * 10.0 / 2
+        bbox = [max(left, cx - half), max(bottom, cy - half), min(right, cx + half), min(top, cy + half)]
+        t0 = time.perf_counter()
+        f = streaming.first_intersecting(index, bbox)
+        i = f["frame_id"]
+        n = f["window"]["width"] * f["window"]["height"]
+        ctx.decode_frames_device(arena, np.array([off[i], off[i + 1]], dtype=np.int64), [n], channels=1, bps=16,
+                                 pcm=pcm)
+        ctx.denormalize_device(pcm.ptr, n, float(tmin[i]), float(tmax[i]), np.int16, out.ptr, pcm_bps=16)
+        out.download(n * 2, 0, out=host[:n].view(np.uint8))
+        dt = time.perf_counter() - t0
+        if q >= 10:
+            lat.append(dt)
+        if q % 100 == 0:  # spot-check: decoded tile == raster window (band 1)
+            wnd = f["window"]
+            ref = np.empty((wnd["height"], W), dtype=np.int16)
+            raster.download(wnd["height"] * W * 2, wnd["row_off"] * W * 2, out=ref.view(np.uint8).reshape(-1))
+            got = host[:n].reshape(wnd["height"], wnd["width"])
+            lossless &= bool(np.array_equal(got, ref[:, wnd["col_off"]:wnd["col_off"] + wnd["width"]]))
+            checked += 1
+    pcm.close()
+    out.close()
+    ms = np.array(lat) * 1e3
+    return {"p50_ms": round(float(np.percentile(ms, 50)), 3), "p90_ms": round(float(np.percentile(ms, 90)), 3),
+            "queries": nq, "n_gpus": 1, "path": "device-resident streaming data: select + decode + denormalise + D2H",
+            "lossless_spot_checks": checked, "lossless": lossless}
 
 
 def traffic_for(path, kernel, px):

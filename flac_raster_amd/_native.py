@@ -70,7 +70,8 @@ def load_library(path: Optional[os.PathLike] = None):
     with _lib_lock:
         if _lib is not None and path is None:
             return _lib
-        p = Path(path) if path else LIB_PATH
+        # FRS_LIB_PATH: an alternative build of the same library (A/B experiments on one GPU box)
+        p = Path(path) if path else Path(os.environ.get("FRS_LIB_PATH", str(LIB_PATH)))
         if not p.exists():
             raise NativeUnavailable(
                 f"{p} is not built; run `python -c 'import __graft_entry__ as g; g.build()'` "

@@ -6,6 +6,8 @@
 
 #include <string>
 
+#include <vector>
+
 #include "frs_internal.h"
 
 namespace frs {
@@ -197,10 +199,20 @@ int frs_decode_frames_device(frs_ctx *ctx, const uint8_t *blob_dev, const int64_
         return FRS_E_ARG;
     }
     FRS_HIP(hipSetDevice(ctx->device));
-    const int64_t nbytes = nstreams ? stream_off[nstreams] - stream_off[0] : 0;
-    (void)nbytes;
-    return frs::decode_job(ctx, blob_dev, nstreams ? stream_off[nstreams] : 0, stream_off, nstreams, channels, bps,
-                           blocksize, pcm_dev, pcm_off);
+    if (nstreams == 0) return FRS_OK;
+    // only [stream_off[0], stream_off[nstreams]) is scanned: a tile query inside a large arena touches
+    // just its own bytes
+    const int64_t base = stream_off[0];
+    std::vector<int64_t> rel(nstreams + 1);
+    for (int s = 0; s <= nstreams; s++) {
+        rel[s] = stream_off[s] - base;
+        if (s && rel[s] < rel[s - 1]) {
+            ctx->err = "stream offsets must be non-decreasing";
+            return FRS_E_ARG;
+        }
+    }
+    return frs::decode_job(ctx, blob_dev + base, rel[nstreams], rel.data(), nstreams, channels, bps, blocksize,
+                           pcm_dev, pcm_off);
 }
 
 int frs_decode_frames(frs_ctx *ctx, const uint8_t *blob_host, const int64_t *stream_off, int32_t nstreams,

@@ -1266,6 +1266,14 @@ __global__ void __launch_bounds__(256) k_build_lut(const TileNorm *norms, int16_
     }
 }
 
+// n / d for n < 2^32 via a double reciprocal (inv = 1.0 / d): the estimate is off by at most one, fixed up
+__device__ inline uint32_t udiv_inv(uint32_t n, uint32_t d, double inv) {
+    uint32_t q = (uint32_t)((double)n * inv);
+    const int64_t r = (int64_t)n - (int64_t)q * d;
+    q = r < 0 ? q - 1 : (r >= (int64_t)d ? q + 1 : q);
+    return q;
+}
+
 // 64 consecutive elements of a frame, kept packed in 32-bit words (int16: 32 words; uint8: 16 words).
 // vec: 16-byte loads of one row segment; otherwise an element gather with a row cursor.
 template <int DT> struct Chunk64 {
@@ -1281,46 +1289,81 @@ template <int DT> struct Chunk64 {
         else if constexpr (sizeof(T) == 2) return (T)((w[j >> 1] >> (16 * (j & 1))) & 0xFFFFu);
         else return __builtin_bit_cast(T, w[j]);
     }
-    __device__ inline void load(const T *base, int64_t row_stride, int width, int64_t s, bool vec, int nvalid) {
-        if (vec) {
-            const int64_t row = s / width;
-            const int col = (int)(s - row * width);
-            const uint4 *p = reinterpret_cast<const uint4 *>(base + row * row_stride + col);
+    // 16-byte loads of one row segment (p 16-B aligned, the 64 elements inside one row)
+    __device__ inline void load_vec(const T *p_) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(p_);
 #pragma unroll
-            for (int k = 0; k < kWords / 4; k++) {
-                const uint4 v = p[k];
-                w[4 * k] = v.x;
-                w[4 * k + 1] = v.y;
-                w[4 * k + 2] = v.z;
-                w[4 * k + 3] = v.w;
+        for (int k = 0; k < kWords / 4; k++) {
+            const uint4 v = p[k];
+            w[4 * k] = v.x;
+            w[4 * k + 1] = v.y;
+            w[4 * k + 2] = v.z;
+            w[4 * k + 3] = v.w;
+        }
+    }
+    // element gather with a row cursor starting at (row, col) (frames that cross rows mid-chunk)
+    __device__ inline void load_gather(const T *base, int64_t row_stride, int width, int64_t row, int col,
+                                       int nvalid) {
+#pragma unroll
+        for (int k = 0; k < kWords; k++) w[k] = 0;
+        const T *rp = base + row * row_stride;
+        for (int j = 0; j < nvalid; j++) {
+            uint32_t v;
+            if constexpr (sizeof(T) == 4) v = __builtin_bit_cast(uint32_t, rp[col]);
+            else v = (uint32_t)(std::make_unsigned_t<T>)rp[col];
+#pragma unroll
+            for (int k = 0; k < kWords; k++) {
+                constexpr int per = 4 / (int)sizeof(T);
+                if (k == j / per) {
+                    const int sh = (int)(8 * sizeof(T)) * (j % per);
+                    w[k] |= (sizeof(T) == 4) ? v : (v << sh);
+                }
             }
-        } else {
-#pragma unroll
-            for (int k = 0; k < kWords; k++) w[k] = 0;
-            int64_t row = s / width;
-            int col = (int)(s - row * width);
-            const T *rp = base + row * row_stride;
-            for (int j = 0; j < nvalid; j++) {
-                uint32_t v;
-                if constexpr (sizeof(T) == 4) v = __builtin_bit_cast(uint32_t, rp[col]);
-                else v = (uint32_t)(std::make_unsigned_t<T>)rp[col];
-                // dynamic insert (rare path): rebuild through a small switch-free loop
-#pragma unroll
-                for (int k = 0; k < kWords; k++) {
-                    constexpr int per = 4 / (int)sizeof(T);
-                    if (k == j / per) {
-                        const int sh = (int)(8 * sizeof(T)) * (j % per);
-                        w[k] |= (sizeof(T) == 4) ? v : (v << sh);
-                    }
-                }
-                if (++col == width) {
-                    col = 0;
-                    rp += row_stride;
-                }
+            if (++col == width) {
+                col = 0;
+                rp += row_stride;
             }
         }
     }
+    __device__ inline void load(const T *base, int64_t row_stride, int width, int64_t row, int col, bool vec,
+                                int nvalid) {
+        if (vec) load_vec(base + row * row_stride + col);
+        else load_gather(base, row_stride, width, row, col, nvalid);
+    }
 };
+
+// normalise elements [8b, 8b + 8) of a chunk (b compile-time after unrolling)
+template <int DT>
+__device__ inline void norm_block8(const Chunk64<DT> &ch, int b, const TileNorm &tn, const int16_t *lut, int32_t *x) {
+    switch (tn.mode) {
+    case kNormLut: {
+        const int32_t mn = (int32_t)tn.imin;
+#pragma unroll
+        for (int j = 0; j < 8; j++) x[j] = (int32_t)lut[(int32_t)ch.get(8 * b + j) - mn];
+        break;
+    }
+    case kNormZero:
+#pragma unroll
+        for (int j = 0; j < 8; j++) x[j] = 0;
+        break;
+    case kNormFastDiv: {
+        const int32_t mn = (int32_t)tn.imin;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const double a = (double)(2 * ((int32_t)ch.get(8 * b + j) - mn));
+            const double q0 = a * tn.rinv;
+            const double r = fma(-q0, tn.den, a);
+            const double q1 = fma(r, tn.rinv, q0);
+            x[j] = (int32_t)(int16_t)(int32_t)((q1 - 1.0) * 32767.0);
+        }
+        break;
+    }
+    default:
+#pragma unroll
+        for (int j = 0; j < 8; j++) x[j] = norm_fast<DT>(ch.get(8 * b + j), tn, lut);
+        break;
+    }
+}
 
 template <int DT>
 __global__ void __launch_bounds__(256) k_analyze_v2(const typename Elem<DT>::T *raster, EncodeParams P,
@@ -1341,7 +1384,7 @@ __global__ void __launch_bounds__(256) k_analyze_v2(const typename Elem<DT>::T *
     const int64_t tile_px = (int64_t)g.h * g.w;
     const int n = live ? (int)min((int64_t)P.blocksize, tile_px - s0) : 0;
     TileNorm tn = norms[t];
-    // LUT: one per wave when the wave's frames share a tile
+    // LUT: one per wave when the wave's frames share a tile; other LUT tiles take the exact division
     const int t0 = __shfl(t, 0);
     const bool uni = __all(t == t0);
     const bool wave_lut = uni && tn.mode == kNormLut;
@@ -1363,14 +1406,27 @@ __global__ void __launch_bounds__(256) k_analyze_v2(const typename Elem<DT>::T *
 #pragma unroll
     for (int j = 0; j < 8; j++) prev[j] = 0.0;
 
-    // fast path: every frame is a full block (host guarantees), 64 chunks of 64 samples per lane
+    // fast path: every frame is a full block (host guarantees), 64 chunks of 64 samples per lane; a
+    // row/column cursor walks the tile (no per-chunk division); the next chunk's loads are issued before
+    // the current chunk's FMAs
+    const uint32_t r0 = udiv_inv((uint32_t)s0, (uint32_t)g.w, 1.0 / (double)g.w);
+    int64_t crow = r0;
+    int ccol = (int)((uint32_t)s0 - r0 * (uint32_t)g.w);
+    auto advance = [&]() {
+        ccol += 64;
+        while (ccol >= g.w) {
+            ccol -= g.w;
+            crow++;
+        }
+    };
     for (int c = 0; c < kMaxBlock / 64; c++) {
         const int i0 = c * 64;
         float xf[64];
         {
-            Chunk64<DT> ch;
-            ch.load(base, P.row_stride, g.w, s0 + i0, vec, 64);
-            norm_chunk<DT>(ch, tn, lut, [&](int j, int32_t x) {
+            Chunk64<DT> chc;
+            chc.load(base, P.row_stride, g.w, crow, ccol, vec, 64);
+            advance();
+            norm_chunk<DT>(chc, tn, lut, [&](int j, int32_t x) {
                 or_acc |= (uint32_t)x;
                 xf[j] = (float)x;
             });
@@ -1859,7 +1915,9 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     uint32_t E[36];
     {
         Chunk64<DT> ch;
-        ch.load(base, P.row_stride, g.w, s0 + 64 * lane, P.vec_ok && (g.w % 64) == 0, 64);
+        const uint32_t sl0 = (uint32_t)s0 + 64u * (uint32_t)lane;  // tile pixels < 2^31
+        const uint32_t row = udiv_inv(sl0, (uint32_t)g.w, 1.0 / (double)g.w);
+        ch.load(base, P.row_stride, g.w, row, (int)(sl0 - row * (uint32_t)g.w), P.vec_ok && (g.w % 64) == 0, 64);
         int32_t lo = 0;
         norm_chunk<DT>(ch, tn, lut, [&](int j, int32_t x) {
             if (j & 1) E[4 + (j >> 1)] = pack2(lo, x >> w);

@@ -13,6 +13,7 @@ only the first intersecting tile.
 from __future__ import annotations
 
 import json
+import math
 import logging
 import struct
 from dataclasses import dataclass
@@ -188,11 +189,42 @@ def select_frame(index: Dict, tile_id: Optional[int] = None, last: bool = False,
                 dmin, best = d, f
         return best
     if bbox is not None:
-        hits = intersecting(index, bbox)
-        if not hits:
+        hit = first_intersecting(index, bbox)
+        if hit is None:
             raise LookupError(f"No tiles intersect with bbox {bbox}")
-        return hits[0]
+        return hit
     raise ValueError("Must specify --tile-id, --bbox, --center, or --last")
+
+
+def first_intersecting(index: Dict, bbox: Sequence[float]) -> Optional[Dict]:
+    """intersecting(index, bbox)[0] (cli.py:976-987) without the linear scan when the index is the
+    row-major tile grid create-streaming writes: only tiles within one tile of the bbox's pixel footprint
+    are tested, in index order, with the same strict inequalities on the stored bboxes."""
+    T, W, H, t = index.get("tile_size"), index.get("width"), index.get("height"), index.get("transform")
+    frames = index["frames"]
+    ok = bool(T and W and H and t and len(t) >= 6 and t[1] == 0 and t[3] == 0 and t[0] != 0 and t[4] != 0)
+    if ok:
+        tc, tr = -(-int(W) // int(T)), -(-int(H) // int(T))
+        ok = len(frames) == tc * tr
+    if not ok:
+        hits = intersecting(index, bbox)
+        return hits[0] if hits else None
+    x0, y0, x1, y1 = bbox
+    a, c, e, f = float(t[0]), float(t[2]), float(t[4]), float(t[5])
+    ca, cb = sorted(((x0 - c) / a, (x1 - c) / a))
+    ra, rb = sorted(((y0 - f) / e, (y1 - f) / e))
+    ct0, ct1 = max(0, int(math.floor(ca / T)) - 1), min(tc - 1, int(math.floor(cb / T)) + 1)
+    rt0, rt1 = max(0, int(math.floor(ra / T)) - 1), min(tr - 1, int(math.floor(rb / T)) + 1)
+    for r in range(rt0, rt1 + 1):
+        for cc in range(ct0, ct1 + 1):
+            fr = frames[r * tc + cc]
+            if fr["frame_id"] != r * tc + cc:  # not the plain grid order: fall back to the scan
+                hits = intersecting(index, bbox)
+                return hits[0] if hits else None
+            b = fr["bbox"]
+            if x0 < b[2] and x1 > b[0] and y0 < b[3] and y1 > b[1]:
+                return fr
+    return None
 
 
 def intersecting(index: Dict, bbox: Sequence[float]) -> List[Dict]:

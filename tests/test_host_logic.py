@@ -83,3 +83,32 @@ def test_streaming_header_parse():
     js = container.index_json(idx)
     n, back = container.parse_streaming_header(struct.pack(">I", len(js)) + js)
     assert n == len(js) and back == idx
+
+
+def test_first_intersecting_matches_linear_scan():
+    """streaming.first_intersecting == intersecting(...)[0] (cli.py:976-987) on a create-streaming grid,
+    including bboxes that touch tile edges exactly (strict inequalities)."""
+    from flac_raster_amd import geotiff, streaming
+    tr = geotiff.Affine(10.0, 0.0, 500000.0, 0.0, -10.0, 4000000.0)
+    H, W, T = 2100, 3000, 512
+    frames = []
+    for i, (col, row, w, h) in enumerate(streaming.tile_grid(H, W, T)):
+        _, bb = streaming.tile_transform_and_bbox(tr, col, row, w, h)
+        frames.append({"frame_id": i, "bbox": bb})
+    index = {"transform": list(tr) + [0.0, 0.0, 1.0], "width": W, "height": H, "tile_size": T, "frames": frames}
+    rng = np.random.default_rng(3)
+    left, top = 500000.0, 4000000.0
+    right, bottom = left + W * 10, top - H * 10
+    edges_x = [left + k * T * 10 for k in range(W // T + 1)]
+    edges_y = [top - k * T * 10 for k in range(H // T + 1)]
+    for q in range(3000):
+        if q % 3 == 0:  # snapped to tile edges
+            x0, x1 = sorted(rng.choice(edges_x, 2))
+            y0, y1 = sorted(rng.choice(edges_y, 2))
+        else:
+            x0, x1 = sorted(rng.uniform(left - 5000, right + 5000, 2))
+            y0, y1 = sorted(rng.uniform(bottom - 5000, top + 5000, 2))
+        bbox = [x0, y0, x1, y1]
+        hits = streaming.intersecting(index, bbox)
+        got = streaming.first_intersecting(index, bbox)
+        assert (got is None and not hits) or (hits and got is hits[0]), bbox
