@@ -210,7 +210,10 @@ def bbox_extract(ctx, raster, arena, off, tmin, tmax, rows, W, T, nq):
     host = np.empty(T * T, dtype=np.int16)
     lat = []
     checked, lossless = 0, True
+    ctx.profile(True)
     for q in range(nq + 10):  # 10 untimed warm-up queries
+        if q == 10:
+            ctx.profile_reset()
         col, row, w, h = grid[int(rng.integers(len(grid)))]
         cx, cy = left + (col + w / 2) * 10.0, top - (row + h / 2) * 10.0
         half = rng.uniform(0.1, 2.0) * T * 10.0 / 2
@@ -233,12 +236,14 @@ def bbox_extract(ctx, raster, arena, off, tmin, tmax, rows, W, T, nq):
             got = host[:n].reshape(wnd["height"], wnd["width"])
             lossless &= bool(np.array_equal(got, ref[:, wnd["col_off"]:wnd["col_off"] + wnd["width"]]))
             checked += 1
+    ctx.profile(False)
+    kern = {k: round(ctx.profile_avg_ms(k), 4) for k in ("decode", "decode_span", "decode_frames")}
     pcm.close()
     out.close()
     ms = np.array(lat) * 1e3
     return {"p50_ms": round(float(np.percentile(ms, 50)), 3), "p90_ms": round(float(np.percentile(ms, 90)), 3),
             "queries": nq, "n_gpus": 1, "path": "device-resident streaming data: select + decode + denormalise + D2H",
-            "lossless_spot_checks": checked, "lossless": lossless}
+            "kernels_ms": kern, "lossless_spot_checks": checked, "lossless": lossless}
 
 
 def traffic_for(path, kernel, px):

@@ -127,6 +127,118 @@ __global__ void k_span_crc(const uint8_t *blob, const int64_t *soff, int ns, con
     ends[i] = e;
 }
 
+
+// Span check, one wave per candidate: the span [p, e) to the next candidate e (or the stream end) is
+// staged in LDS and its CRC-16 computed by all 64 lanes (slice-by-4 per lane, lanes combined with
+// x^(8m) factors); on a mismatch the next candidate is tried.  Spans longer than the LDS stage use the
+// single-lane byte loop.  ends[i] = e or -1.
+// dword k of the blob (bytes 4k..4k+3, little-endian), never touching bytes at or past `end`
+__device__ inline uint32_t load_word_guarded(const uint8_t *blob, int64_t k, int64_t end) {
+    const int64_t b = 4 * k;
+    if (b + 4 <= end) return *reinterpret_cast<const uint32_t *>(blob + b);
+    uint32_t v = 0;
+    for (int j = 0; j < 4; j++)
+        if (b + j < end) v |= (uint32_t)blob[b + j] << (8 * j);
+    return v;
+}
+
+constexpr int kSpanWords = 6144;  // 24 KB stage
+__device__ uint16_t d_xpow_lo[256];   // x^(8m) mod P, m < 256
+__device__ uint16_t d_xpow_hi[4096];  // x^(8*256*m) mod P
+
+__device__ inline uint32_t dec_gfmul(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 15; i >= 0; i--) {
+        r <<= 1;
+        if (r & 0x10000u) r ^= 0x18005u;
+        if ((b >> i) & 1u) r ^= a;
+    }
+    return r;
+}
+
+__global__ void __launch_bounds__(64) k_span_crc_wave(const uint8_t *blob, const int64_t *soff, int ns,
+                                                     const int64_t *cpos, const int *ncand, int64_t max_frame,
+                                                     int64_t *ends) {
+    __shared__ uint32_t stage[kSpanWords + 1];
+    __shared__ uint16_t t4[4][256];
+    __shared__ uint16_t xlo[256];
+    const int lane = threadIdx.x;
+    for (int k = lane; k < 1024; k += 64) (&t4[0][0])[k] = 0;
+    for (int k = lane; k < 256; k += 64) {
+        uint16_t c = d_crc16[k];
+        t4[0][k] = c;
+#pragma unroll
+        for (int j = 1; j < 4; j++) {
+            c = (uint16_t)(((c << 8) & 0xFFFF) ^ d_crc16[c >> 8]);
+            t4[j][k] = c;
+        }
+        xlo[k] = d_xpow_lo[k];
+    }
+    __syncthreads();
+    const int nc = *ncand;
+    const int i = blockIdx.x;
+    if (i >= nc) return;
+    const int64_t p = cpos[i];
+    const int s = stream_of(soff, ns, p);
+    const int64_t send = soff[s + 1];
+    const int64_t lim = min(send, p + max_frame);
+    int64_t result = -1;
+    for (int j = i + 1;; j++) {
+        int64_t e = (j < nc) ? cpos[j] : send;
+        if (e > send) e = send;
+        if (e > lim) break;
+        if (e >= p + 7) {
+            const int64_t wb = p >> 2, we = (e + 3) >> 2;  // aligned words covering [p, e)
+            const int64_t nwords = we - wb;
+            uint32_t crc = 0;
+            if (nwords <= kSpanWords) {
+                for (int64_t k = lane; k < nwords; k += 64) stage[k] = load_word_guarded(blob, wb + k, send);
+                __builtin_amdgcn_s_waitcnt(0xC07F);
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t nb = (uint32_t)(e - 2 - p);  // bytes covered by the CRC
+                const uint32_t off0 = (uint32_t)(p & 3);    // byte offset of p in stage
+                auto byte_at = [&](uint32_t b) -> uint32_t {  // b relative to p
+                    const uint32_t a = b + off0;
+                    return (stage[a >> 2] >> (8 * (a & 3))) & 0xFFu;
+                };
+                const uint32_t ch = ((nb + 63) / 64 + 3) & ~3u;  // bytes per lane, multiple of 4
+                const uint32_t b0 = min(nb, (uint32_t)lane * ch), b1 = min(nb, b0 + ch);
+                uint32_t c = 0, b = b0;
+                for (; b + 4 <= b1; b += 4) {
+                    const uint32_t a = b + off0;
+                    const uint32_t lo = stage[a >> 2], hi = stage[(a >> 2) + 1];
+                    const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, a & 3);  // bytes b..b+3, LE
+                    c = (uint32_t)t4[3][((c >> 8) ^ (w & 0xFF)) & 0xFF] ^ t4[2][((c & 0xFF) ^ ((w >> 8) & 0xFF)) & 0xFF] ^
+                        t4[1][(w >> 16) & 0xFF] ^ t4[0][w >> 24];
+                }
+                for (; b < b1; b++) c = ((c << 8) & 0xFFFFu) ^ t4[0][((c >> 8) ^ byte_at(b)) & 0xFF];
+                const uint32_t m = nb - b1;  // bytes after this lane's chunk
+                c = dec_gfmul(dec_gfmul(c, xlo[m & 255]), d_xpow_hi[m >> 8]);
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) c ^= __shfl_xor(c, o);
+                crc = c;
+                const uint32_t got = (byte_at(nb) << 8) | byte_at(nb + 1);
+                __builtin_amdgcn_wave_barrier();
+                if (crc == got) {
+                    result = e;
+                    break;
+                }
+            } else {  // rare: a span longer than the stage
+                uint32_t c = 0;
+                for (int64_t b = p; b < e - 2; b++) c = ((c << 8) & 0xFFFFu) ^ d_crc16[((c >> 8) ^ blob[b]) & 0xFF];
+                const uint32_t got = ((uint32_t)blob[e - 2] << 8) | blob[e - 1];
+                if (c == got) {
+                    result = e;
+                    break;
+                }
+            }
+        }
+        if (e >= send) break;
+    }
+    if (lane == 0) ends[i] = result;
+}
+
 __device__ inline int find_pos(const int64_t *cpos, int n, int64_t p) {
     int lo = 0, hi = n - 1;
     while (lo <= hi) {
@@ -175,16 +287,25 @@ struct BitReader {
         err = false;
     }
     __device__ inline void refill() {
-        while (avail <= 56) {
-            const int64_t byte = (pos_bits + avail) >> 3;
-            uint64_t b = 0;
-            if (byte < (end_bits >> 3)) b = base[byte];
-            else if (byte >= (end_bits >> 3) + 8) {
-                err = true;
-                return;
+        while (avail <= 32) {
+            const int64_t byte = (pos_bits + avail) >> 3;  // next byte not yet in the cache (avail % 8 == 0)
+            const int64_t endb = end_bits >> 3;
+            if (byte + 8 <= endb) {
+                // 4 bytes via the two aligned dwords around them (no per-byte loads)
+                const uint32_t *w = reinterpret_cast<const uint32_t *>(base + (byte & ~(int64_t)3));
+                const uint32_t v = __builtin_bswap32(__builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(byte & 3)));
+                cache |= (uint64_t)v << (32 - avail);
+                avail += 32;
+            } else {
+                uint64_t b = 0;
+                if (byte < endb) b = base[byte];
+                else if (byte >= endb + 8) {
+                    err = true;
+                    return;
+                }
+                cache |= b << (56 - avail);
+                avail += 8;
             }
-            cache |= b << (56 - avail);
-            avail += 8;
         }
     }
     __device__ inline uint32_t bits(int n) {  // n <= 32
@@ -229,13 +350,11 @@ struct BitReader {
     }
 };
 
-__global__ void __launch_bounds__(64) k_decode_frames(const uint8_t *blob, const int64_t *soff, int ns,
-                                                     const int64_t *poff, const int64_t *cpos, const int64_t *ends,
-                                                     const int64_t *fbase, const int64_t *frame_cand, int64_t nframes,
-                                                     int channels, int stream_bps, int32_t *pcm, int blocksize,
-                                                     int *nvalid) {
-    const int64_t fi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (fi >= nframes) return;
+__device__ __attribute__((always_inline)) inline void decode_one_frame(const uint8_t *blob, const uint8_t *bits_base, int64_t bits_shift,
+                                        const int64_t *soff, int ns, const int64_t *poff, const int64_t *cpos,
+                                        const int64_t *ends, const int64_t *fbase, const int64_t *frame_cand,
+                                        int64_t fi, int channels, int stream_bps, int32_t *pcm, int blocksize,
+                                        int *nvalid) {
     const int64_t ci = frame_cand[fi];
     const int64_t fpos = cpos[ci];
     const int64_t fend_known = ends[ci];
@@ -247,8 +366,8 @@ __global__ void __launch_bounds__(64) k_decode_frames(const uint8_t *blob, const
     const int64_t first = kk * blocksize;
     if (!cd.ok || cd.frame_no != kk || cd.bs > blocksize || first + cd.bs > nsamp) return;
     int32_t *outb = pcm + (poff[s] + first) * channels;
-    BitReader br;
-    br.init(blob, fpos + cd.hdr_len, fend_known);
+    BitReader br;  // bits_base[k] = blob[k + bits_shift] (LDS stage or the blob itself)
+    br.init(bits_base, fpos + cd.hdr_len - bits_shift, fend_known - bits_shift);
     const int nch = channels;
     // decode subframes straight into the output (interleaved), then verify the CRC
     for (int c = 0; c < nch; c++) {
@@ -287,7 +406,47 @@ __global__ void __launch_bounds__(64) k_decode_frames(const uint8_t *blob, const
             const int pb = method == 0 ? 4 : 5, esc = (1 << pb) - 1;
             if ((bs >> po) < o || (bs & ((1 << po) - 1))) return;
             int i = o;
-            // history for reconstruction kept in registers (up to 32 taps read back from output)
+            if (o <= 8) {
+                // history in registers: h[m] = x[i-1-m]; coefficient m = 0 for m >= o (branch-free taps)
+                int32_t cq[8];
+                int32_t h[8];
+#pragma unroll
+                for (int m = 0; m < 8; m++) {
+                    int32_t cm = 0;
+                    if (lpc) cm = m < o ? q[m] : 0;
+                    else if (o == 1) cm = m == 0 ? 1 : 0;
+                    else if (o == 2) cm = m == 0 ? 2 : m == 1 ? -1 : 0;
+                    else if (o == 3) cm = m == 0 ? 3 : m == 1 ? -3 : m == 2 ? 1 : 0;
+                    else if (o == 4) cm = m == 0 ? 4 : m == 1 ? -6 : m == 2 ? 4 : m == 3 ? -1 : 0;
+                    cq[m] = cm;
+                    h[m] = m < o ? x[(int64_t)(o - 1 - m) * nch] : 0;
+                }
+                for (int p = 0; p < (1 << po); p++) {
+                    const int ns = (bs >> po) - (p == 0 ? o : 0);
+                    const int kp = (int)br.bits(pb);
+                    int nb = 0;
+                    if (kp == esc) nb = (int)br.bits(5);
+                    for (int j = 0; j < ns; j++, i++) {
+                        int32_t r;
+                        if (kp == esc) r = nb ? br.sbits(nb) : 0;
+                        else {
+                            const uint32_t qq = br.unary();
+                            const uint32_t u = (qq << kp) | br.bits(kp);
+                            r = (int32_t)((u >> 1) ^ (uint32_t)(-(int32_t)(u & 1)));
+                        }
+                        int64_t pred = 0;
+#pragma unroll
+                        for (int m = 0; m < 8; m++) pred += (int64_t)cq[m] * h[m];
+                        pred >>= shift;
+                        const int32_t v = (int32_t)(r + pred);
+                        x[(int64_t)i * nch] = v;
+#pragma unroll
+                        for (int m = 7; m > 0; m--) h[m] = h[m - 1];
+                        h[0] = v;
+                    }
+                    if (br.err) return;
+                }
+            } else
             for (int p = 0; p < (1 << po); p++) {
                 const int ns = (bs >> po) - (p == 0 ? o : 0);
                 const int kp = (int)br.bits(pb);
@@ -338,9 +497,52 @@ __global__ void __launch_bounds__(64) k_decode_frames(const uint8_t *blob, const
         }
     }
     // the decoded subframes must end exactly at the CRC-16 footer found by k_span_crc
-    const int64_t fend = (br.pos_bits + 7) >> 3;
+    const int64_t fend = ((br.pos_bits + 7) >> 3) + bits_shift;
     if (br.err || fend + 2 != fend_known) return;
     atomicAdd(nvalid, 1);
+}
+
+
+__global__ void __launch_bounds__(64) k_decode_frames(const uint8_t *blob, const int64_t *soff, int ns,
+                                                     const int64_t *poff, const int64_t *cpos, const int64_t *ends,
+                                                     const int64_t *fbase, const int64_t *frame_cand, int64_t nframes,
+                                                     int channels, int stream_bps, int32_t *pcm, int blocksize,
+                                                     int *nvalid) {
+    const int64_t fi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (fi >= nframes) return;
+    decode_one_frame(blob, blob, 0, soff, ns, poff, cpos, ends, fbase, frame_cand, fi, channels, stream_bps, pcm,
+                     blocksize, nvalid);
+}
+
+// One wave per frame: the frame's bytes are staged in LDS by the whole wave (coalesced dword loads), then
+// lane 0 decodes from LDS (bit refills are LDS reads instead of dependent global loads).  Frames larger
+// than the stage are decoded straight from global memory.
+constexpr int kDecStageWords = 6144;  // 24 KB
+__global__ void __launch_bounds__(64) k_decode_frames_wave(const uint8_t *blob, const int64_t *soff, int ns,
+                                                          const int64_t *poff, const int64_t *cpos,
+                                                          const int64_t *ends, const int64_t *fbase,
+                                                          const int64_t *frame_cand, int64_t nframes, int channels,
+                                                          int stream_bps, int32_t *pcm, int blocksize, int *nvalid) {
+    __shared__ uint32_t stage[kDecStageWords + 4];
+    const int64_t fi = blockIdx.x;
+    if (fi >= nframes) return;
+    const int lane = threadIdx.x;
+    const int64_t ci = frame_cand[fi];
+    const int64_t fpos = cpos[ci], fend = ends[ci];
+    const int s = stream_of(soff, ns, fpos);
+    const int64_t send = soff[s + 1];
+    const int64_t wb = fpos >> 2, we = (fend + 3) >> 2;
+    const bool staged = we - wb <= kDecStageWords;
+    if (staged)
+        for (int64_t k = lane; k < we - wb + 4; k += 64) stage[k] = load_word_guarded(blob, wb + k, send);
+    __syncthreads();
+    if (lane != 0) return;
+    if (staged)
+        decode_one_frame(blob, reinterpret_cast<const uint8_t *>(stage), wb * 4, soff, ns, poff, cpos, ends, fbase,
+                         frame_cand, fi, channels, stream_bps, pcm, blocksize, nvalid);
+    else
+        decode_one_frame(blob, blob, 0, soff, ns, poff, cpos, ends, fbase, frame_cand, fi, channels, stream_bps, pcm,
+                         blocksize, nvalid);
 }
 
 // converter.py:88-110 (fp32, round half to even) after the pyflac/soundfile WAV round trip.
@@ -381,6 +583,30 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         }
         FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(d_crc8), t8, sizeof(t8), 0, hipMemcpyHostToDevice, st));
         FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(d_crc16), t16, sizeof(t16), 0, hipMemcpyHostToDevice, st));
+        auto mulmod = [](uint32_t a, uint32_t b) {
+            uint32_t r = 0;
+            for (int i = 15; i >= 0; i--) {
+                r <<= 1;
+                if (r & 0x10000u) r ^= 0x18005u;
+                if ((b >> i) & 1u) r ^= a;
+            }
+            return r;
+        };
+        static uint16_t lo[256], hi[4096];
+        uint32_t pw = 1;
+        for (int m = 0; m < 256; m++) {
+            lo[m] = (uint16_t)pw;
+            pw = mulmod(pw, 0x100);
+        }
+        const uint32_t step = pw;  // x^(8*256)
+        pw = 1;
+        for (int m = 0; m < 4096; m++) {
+            hi[m] = (uint16_t)pw;
+            pw = mulmod(pw, step);
+        }
+        FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(d_xpow_lo), lo, sizeof(lo), 0, hipMemcpyHostToDevice, st));
+        FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(d_xpow_hi), hi, sizeof(hi), 0, hipMemcpyHostToDevice, st));
+        FRS_HIP(hipStreamSynchronize(st));
         g_dec_tables[ctx->device] = true;
     }
     if (blob_bytes <= 0 || nstreams <= 0) return FRS_OK;
@@ -425,15 +651,22 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         ctx->err = "too many frame sync candidates";
         return FRS_E_CORRUPT;
     }
+    prof_end(ctx, "decode", ev);
     if (hc > 0) {
-        k_span_crc<<<(hc + 63) / 64, 64, 0, st>>>(blob_dev, dsoff, nstreams, flags, cpos, ncand, max_frame, ends);
+        prof_begin(ctx, "decode_span", &ev);
+        if (max_frame < (int64_t)4096 * 256)  // x^(8m) table range
+            k_span_crc_wave<<<hc, 64, 0, st>>>(blob_dev, dsoff, nstreams, cpos, ncand, max_frame, ends);
+        else
+            k_span_crc<<<(hc + 63) / 64, 64, 0, st>>>(blob_dev, dsoff, nstreams, flags, cpos, ncand, max_frame, ends);
         k_chain<<<(nstreams + 63) / 64, 64, 0, st>>>(dsoff, nstreams, cpos, ncand, ends, dfbase, dchain, bad);
-        k_decode_frames<<<(unsigned)((frames + 63) / 64), 64, 0, st>>>(blob_dev, dsoff, nstreams,
+        prof_end(ctx, "decode_span", ev);
+        prof_begin(ctx, "decode_frames", &ev);
+        k_decode_frames_wave<<<(unsigned)frames, 64, 0, st>>>(blob_dev, dsoff, nstreams,
                                                                       ctx->dec_poff.as<int64_t>(), cpos, ends, dfbase,
                                                                       dchain, frames, channels, bps, pcm_dev, blocksize,
                                                                       nvalid);
+        prof_end(ctx, "decode_frames", ev);
     }
-    prof_end(ctx, "decode", ev);
     int hv[3] = {0, 0, 0};
     FRS_HIP(hipMemcpyAsync(hv, ncand, sizeof(int) * 3, hipMemcpyDeviceToHost, st));
     FRS_HIP(hipStreamSynchronize(st));
