@@ -270,6 +270,8 @@ __global__ void k_chain(const int64_t *soff, int ns, const int64_t *cpos, const 
     if (cur != soff[s + 1]) atomicAdd(bad, 1);
 }
 
+constexpr int kDecResMax = 4096;  // residual buffer (LDS) of the fast subframe path
+
 // MSB-first bit reader over global bytes (bounded)
 struct BitReader {
     const uint8_t *base;
@@ -285,6 +287,13 @@ struct BitReader {
         cache = 0;
         avail = 0;
         err = false;
+    }
+    // reposition at an arbitrary bit (the cache invariant wants byte-aligned loads)
+    __device__ inline void seek_bits(int64_t p) {
+        pos_bits = (p >> 3) << 3;
+        cache = 0;
+        avail = 0;
+        if (p & 7) bits((int)(p & 7));
     }
     __device__ inline void refill() {
         while (avail <= 32) {
@@ -350,11 +359,68 @@ struct BitReader {
     }
 };
 
+// Rice codes of one partition straight from the LDS stage (words w, MSB-first after a byte swap): a 64-bit
+// cache refilled 32 bits at a time from a word fetched one refill ahead.  pos_bits (relative to w) is
+// advanced; false if the codes run past max_bits.
+__device__ __attribute__((always_inline)) inline bool rice_run_lds(const uint32_t *w, int64_t &pos_bits,
+                                                                   int64_t max_bits, int ns, int k, int32_t *out) {
+    uint32_t wi = (uint32_t)(pos_bits >> 5);
+    const int off = (int)(pos_bits & 31);
+    uint64_t c = ((((uint64_t)__builtin_bswap32(w[wi])) << 32) | __builtin_bswap32(w[wi + 1])) << off;
+    int n = 64 - off;
+    wi += 2;
+    uint32_t nw = __builtin_bswap32(w[wi]);
+    const uint32_t wmax = (uint32_t)((max_bits + 31) >> 5) + 2;
+    for (int j = 0; j < ns; j++) {
+        if (n < 32) {
+            c |= (uint64_t)nw << (32 - n);
+            n += 32;
+            nw = __builtin_bswap32(w[++wi]);
+        }
+        uint32_t q;
+        const int z = c ? __builtin_clzll(c) : 64;
+        if (z < 32) {
+            q = (uint32_t)z;
+            c <<= z + 1;
+            n -= z + 1;
+        } else {  // long unary run
+            q = 0;
+            while (true) {
+                const int zz = c ? __builtin_clzll(c) : 64;
+                if (zz < n) {
+                    q += (uint32_t)zz;
+                    c = (zz + 1 >= 64) ? 0 : (c << (zz + 1));
+                    n -= zz + 1;
+                    break;
+                }
+                q += (uint32_t)n;
+                c = (uint64_t)nw << 32;
+                n = 32;
+                nw = __builtin_bswap32(w[++wi]);
+                if (wi > wmax) return false;
+            }
+        }
+        if (n < 32) {
+            c |= (uint64_t)nw << (32 - n);
+            n += 32;
+            nw = __builtin_bswap32(w[++wi]);
+        }
+        const uint32_t low = k ? (uint32_t)(c >> (64 - k)) : 0u;
+        c <<= k;
+        n -= k;
+        const uint32_t u = (q << k) | low;
+        out[j] = (int32_t)((u >> 1) ^ (uint32_t)(-(int32_t)(u & 1)));
+        if (wi > wmax) return false;
+    }
+    pos_bits = (int64_t)wi * 32 - n;
+    return pos_bits <= max_bits;
+}
+
 __device__ __attribute__((always_inline)) inline void decode_one_frame(const uint8_t *blob, const uint8_t *bits_base, int64_t bits_shift,
                                         const int64_t *soff, int ns, const int64_t *poff, const int64_t *cpos,
                                         const int64_t *ends, const int64_t *fbase, const int64_t *frame_cand,
                                         int64_t fi, int channels, int stream_bps, int32_t *pcm, int blocksize,
-                                        int *nvalid) {
+                                        int *nvalid, int32_t *resbuf, const uint32_t *lds_words) {
     const int64_t ci = frame_cand[fi];
     const int64_t fpos = cpos[ci];
     const int64_t fend_known = ends[ci];
@@ -392,9 +458,11 @@ __device__ __attribute__((always_inline)) inline void decode_one_frame(const uin
             if (o > bs) return;
             int32_t q[32];
             int shift = 0;
+            int prec_lpc = 0;
             for (int i = 0; i < o; i++) x[(int64_t)i * nch] = br.sbits(sbps);
             if (lpc) {
                 const int prec = (int)br.bits(4) + 1;
+                prec_lpc = prec;
                 if (prec == 16) return;
                 shift = br.sbits(5);
                 if (shift < 0) return;
@@ -406,7 +474,91 @@ __device__ __attribute__((always_inline)) inline void decode_one_frame(const uin
             const int pb = method == 0 ? 4 : 5, esc = (1 << pb) - 1;
             if ((bs >> po) < o || (bs & ((1 << po) - 1))) return;
             int i = o;
-            if (o <= 8) {
+            int lg = 0;
+            while ((1 << lg) < o) lg++;
+            const bool narrow = sbps <= 23 && (lpc ? prec_lpc : 3) + sbps + lg <= 31;
+            if (resbuf && narrow && bs <= kDecResMax) {
+                // ---- phase 1: every residual of the subframe into LDS (tight Rice loop: refill only when
+                //      fewer than 32 bits are cached, long unary runs via the generic reader)
+                for (int p = 0; p < (1 << po); p++) {
+                    const int ns = (bs >> po) - (p == 0 ? o : 0);
+                    const int kp = (int)br.bits(pb);
+                    if (kp == esc) {
+                        const int nb = (int)br.bits(5);
+                        for (int j = 0; j < ns; j++) resbuf[i++] = nb ? br.sbits(nb) : 0;
+                    } else if (lds_words) {
+                        int64_t pbits = br.pos_bits;
+                        if (!rice_run_lds(lds_words, pbits, br.end_bits, ns, kp, resbuf + i)) return;
+                        i += ns;
+                        br.seek_bits(pbits);
+                    } else {
+                        for (int j = 0; j < ns; j++) {
+                            if (br.avail < 32) br.refill();
+                            const uint64_t c = br.cache;
+                            const int z = c ? __builtin_clzll(c) : 64;
+                            uint32_t qq;
+                            if (z < br.avail) {
+                                qq = (uint32_t)z;
+                                br.cache = c << (z + 1);
+                                br.avail -= z + 1;
+                                br.pos_bits += z + 1;
+                            } else {
+                                qq = br.unary();
+                            }
+                            uint32_t low = 0;
+                            if (kp) {
+                                if (br.avail < kp) br.refill();
+                                low = (uint32_t)(br.cache >> (64 - kp));
+                                br.cache <<= kp;
+                                br.avail -= kp;
+                                br.pos_bits += kp;
+                            }
+                            const uint32_t u = (qq << kp) | low;
+                            resbuf[i++] = (int32_t)((u >> 1) ^ (uint32_t)(-(int32_t)(u & 1)));
+                        }
+                    }
+                    if (br.err) return;
+                }
+                // ---- phase 2: reconstruction with an 8-register ring R[k] = x[i0 - 8 + k]; the taps on older
+                //      samples are summed first so only the newest tap is on the critical path
+                int32_t cq[8], R[8];
+#pragma unroll
+                for (int m = 0; m < 8; m++) {
+                    int32_t cm = 0;
+                    if (lpc) cm = m < o ? q[m] : 0;
+                    else if (o == 1) cm = m == 0 ? 1 : 0;
+                    else if (o == 2) cm = m == 0 ? 2 : m == 1 ? -1 : 0;
+                    else if (o == 3) cm = m == 0 ? 3 : m == 1 ? -3 : m == 2 ? 1 : 0;
+                    else if (o == 4) cm = m == 0 ? 4 : m == 1 ? -6 : m == 2 ? 4 : m == 3 ? -1 : 0;
+                    cq[m] = cm;
+                    const int src = o - 8 + m;
+                    R[m] = src >= 0 ? x[(int64_t)src * nch] : 0;
+                }
+                // keep the ring, taps and output cursor in VGPRs (vector ALU; the scalar unit would spill)
+                int32_t vshift = shift;
+                int32_t *xo = x;
+#pragma unroll
+                for (int m = 0; m < 8; m++) asm volatile("" : "+v"(cq[m]), "+v"(R[m]));
+                asm volatile("" : "+v"(vshift));
+                for (int i0 = o; i0 < bs; i0 += 8) {
+                    int32_t rr[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) rr[u] = (i0 + u < bs) ? resbuf[i0 + u] : 0;
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        if (i0 + u < bs) {
+                            int32_t older = 0;
+#pragma unroll
+                            for (int m = 1; m < 8; m++) older += __mul24(cq[m], R[(u - 1 - m + 16) & 7]);
+                            const int32_t pred = older + __mul24(cq[0], R[(u - 1 + 8) & 7]);
+                            const int32_t v = rr[u] + (pred >> vshift);
+                            xo[(int64_t)(i0 + u) * nch] = v;
+                            R[u] = v;
+                        }
+                    }
+                }
+                i = bs;
+            } else if (o <= 8) {
                 // history in registers: h[m] = x[i-1-m]; coefficient m = 0 for m >= o (branch-free taps)
                 int32_t cq[8];
                 int32_t h[8];
@@ -511,7 +663,7 @@ __global__ void __launch_bounds__(64) k_decode_frames(const uint8_t *blob, const
     const int64_t fi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (fi >= nframes) return;
     decode_one_frame(blob, blob, 0, soff, ns, poff, cpos, ends, fbase, frame_cand, fi, channels, stream_bps, pcm,
-                     blocksize, nvalid);
+                     blocksize, nvalid, nullptr, nullptr);
 }
 
 // One wave per frame: the frame's bytes are staged in LDS by the whole wave (coalesced dword loads), then
@@ -524,6 +676,7 @@ __global__ void __launch_bounds__(64) k_decode_frames_wave(const uint8_t *blob, 
                                                           const int64_t *frame_cand, int64_t nframes, int channels,
                                                           int stream_bps, int32_t *pcm, int blocksize, int *nvalid) {
     __shared__ uint32_t stage[kDecStageWords + 4];
+    __shared__ int32_t resbuf[kDecResMax];
     const int64_t fi = blockIdx.x;
     if (fi >= nframes) return;
     const int lane = threadIdx.x;
@@ -539,10 +692,10 @@ __global__ void __launch_bounds__(64) k_decode_frames_wave(const uint8_t *blob, 
     if (lane != 0) return;
     if (staged)
         decode_one_frame(blob, reinterpret_cast<const uint8_t *>(stage), wb * 4, soff, ns, poff, cpos, ends, fbase,
-                         frame_cand, fi, channels, stream_bps, pcm, blocksize, nvalid);
+                         frame_cand, fi, channels, stream_bps, pcm, blocksize, nvalid, resbuf, stage);
     else
         decode_one_frame(blob, blob, 0, soff, ns, poff, cpos, ends, fbase, frame_cand, fi, channels, stream_bps, pcm,
-                         blocksize, nvalid);
+                         blocksize, nvalid, resbuf, nullptr);
 }
 
 // converter.py:88-110 (fp32, round half to even) after the pyflac/soundfile WAV round trip.
