@@ -1609,6 +1609,26 @@ __device__ inline uint32_t dpp_wave_sum_u32(uint32_t v) {  // total, wave-unifor
     v += bfly_partner<32>(v);
     return uni(v);
 }
+// N independent wave sums advanced in lockstep (their DPP/permlane wait states overlap)
+template <int N> __device__ inline void dpp_wave_sum_multi(const uint32_t *in, uint32_t *out) {
+    uint32_t v[N];
+#pragma unroll
+    for (int i = 0; i < N; i++) v[i] = in[i];
+#pragma unroll
+    for (int i = 0; i < N; i++) v[i] += bfly_partner<1>(v[i]);
+#pragma unroll
+    for (int i = 0; i < N; i++) v[i] += bfly_partner<2>(v[i]);
+#pragma unroll
+    for (int i = 0; i < N; i++) v[i] += bfly_partner<4>(v[i]);
+#pragma unroll
+    for (int i = 0; i < N; i++) v[i] += bfly_partner<8>(v[i]);
+#pragma unroll
+    for (int i = 0; i < N; i++) v[i] += bfly_partner<16>(v[i]);
+#pragma unroll
+    for (int i = 0; i < N; i++) v[i] += bfly_partner<32>(v[i]);
+#pragma unroll
+    for (int i = 0; i < N; i++) out[i] = uni(v[i]);
+}
 __device__ inline uint64_t dpp_wave_sum_u64(uint64_t v) {
     v += bfly_partner64<1>(v);
     v += bfly_partner64<2>(v);
@@ -1663,21 +1683,49 @@ __device__ inline uint32_t pack2(int32_t lo, int32_t hi) { return ((uint32_t)lo 
 // residual of local sample index j (0..63, compile-time) of this lane given the even pairs E[] (E[0..3]:
 // the previous lane's last 8 samples, E[4 + m] = (x[2m], x[2m+1])).  C[] = (q1,q0),(q3,q2),(q5,q4),(q7,q6).
 // Odd j uses odd-aligned pairs (x[j-2], x[j-1]) = perm(E[m], E[m-1]).
+// first product of a residual chain as VOP3P with an inline-zero accumulator (v_dot2c would need a v_mov 0)
+__device__ inline int32_t dot2_z(uint32_t a, uint32_t b) {
+    int32_t d;
+    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+
 __device__ inline int32_t residual_at(const uint32_t *E, const uint32_t *C, int shift, int j, int32_t x) {
     int32_t s = 0;
     const int m = 4 + (j >> 1);
     if ((j & 1) == 0) {
-        s = dot2(E[m - 1], C[0], s);
+        s = dot2_z(E[m - 1], C[0]);
         s = dot2(E[m - 2], C[1], s);
         s = dot2(E[m - 3], C[2], s);
         s = dot2(E[m - 4], C[3], s);
     } else {
-        s = dot2(__builtin_amdgcn_perm(E[m], E[m - 1], 0x05040302u), C[0], s);
+        s = dot2_z(__builtin_amdgcn_perm(E[m], E[m - 1], 0x05040302u), C[0]);
         s = dot2(__builtin_amdgcn_perm(E[m - 1], E[m - 2], 0x05040302u), C[1], s);
         s = dot2(__builtin_amdgcn_perm(E[m - 2], E[m - 3], 0x05040302u), C[2], s);
         s = dot2(__builtin_amdgcn_perm(E[m - 3], E[m - 4], 0x05040302u), C[3], s);
     }
     return x - (s >> shift);
+}
+
+// residuals of samples 2m and 2m+1 of this lane with their v_dot2 chains interleaved (no dependent-dot
+// wait states): the even sample uses aligned pairs E[], the odd one pairs re-aligned by v_perm
+__device__ inline void residual_pair(const uint32_t *E, const uint32_t *C, int shift, int m, int32_t &re, int32_t &ro) {
+    const int b = 4 + m;
+    const uint32_t o0 = __builtin_amdgcn_perm(E[b], E[b - 1], 0x05040302u);
+    const uint32_t o1 = __builtin_amdgcn_perm(E[b - 1], E[b - 2], 0x05040302u);
+    const uint32_t o2 = __builtin_amdgcn_perm(E[b - 2], E[b - 3], 0x05040302u);
+    const uint32_t o3 = __builtin_amdgcn_perm(E[b - 3], E[b - 4], 0x05040302u);
+    int32_t se = dot2_z(E[b - 1], C[0]);
+    int32_t so = dot2_z(o0, C[0]);
+    se = dot2(E[b - 2], C[1], se);
+    so = dot2(o1, C[1], so);
+    se = dot2(E[b - 3], C[2], se);
+    so = dot2(o2, C[2], so);
+    se = dot2(E[b - 4], C[3], se);
+    so = dot2(o3, C[3], so);
+    const uint32_t v = E[b];
+    re = (int32_t)(int16_t)(v & 0xFFFFu) - (se >> shift);
+    ro = ((int32_t)v >> 16) - (so >> shift);
 }
 
 __device__ inline void lds_put_bits(uint32_t *buf, uint32_t pos, uint32_t val, int nbits) {
@@ -1893,7 +1941,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
                                        const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
                                        const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap, int64_t *frame_off,
                                        uint64_t *status, int *err, EncV3Shared &S, int want, int64_t f, int lane,
-                                       const int32_t *ftile, PendingFrame &prev) {
+                                       const int32_t *ftile, PendingFrame &prev, const uint4 *hdr_tab, int hdr_n) {
     using T = typename Elem<DT>::T;
     uint32_t *fbuf = S.bits[threadIdx.x >> 6];
     const int t = ftile[f];
@@ -1978,8 +2026,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     }
     reg_fence(E);
     uint32_t tt[5];
-#pragma unroll
-    for (int k = 0; k < 5; k++) tt[k] = dpp_wave_sum_u32(lt[k]);
+    dpp_wave_sum_multi<5>(lt, tt);
     int guess;
     {
         const uint32_t m = min(min(tt[1], tt[2]), min(tt[3], tt[4]));
@@ -2021,11 +2068,17 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     uint32_t sl = 0;
     if (cand_lpc) {
 #pragma unroll
-        for (int j = 0; j < 64; j++) {
-            if (j % 8 == 0 && j) asm volatile("" : "+v"(sl));
-            const uint32_t a = (uint32_t)abs(residual_at(E, CL, lshift, j, X(j)));
-            if (j < kMaxLpc) sl += (l0 && j < ol) ? 0u : a;
-            else sl += a;
+        for (int m = 0; m < 32; m++) {
+            if (m % 4 == 0 && m) asm volatile("" : "+v"(sl));
+            int32_t re, ro;
+            residual_pair(E, CL, lshift, m, re, ro);
+            const uint32_t ae = (uint32_t)abs(re), ao = (uint32_t)abs(ro);
+            if (2 * m < kMaxLpc) {
+                sl += (l0 && 2 * m < ol) ? 0u : ae;
+                sl += (l0 && 2 * m + 1 < ol) ? 0u : ao;
+            } else {
+                sl += ae + ao;
+            }
         }
     }
     reg_fence(E);
@@ -2104,10 +2157,68 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         if (__ballot(lane_sum >= (1u << 24)) == 0) rice32(lane_sum, order, best_bits, best_po, my_k);
         else rice64(lane_sum, order, best_bits, best_po, my_k);
     };
+    // both candidates' searches in one loop (independent DPP chains overlap); exact 32-bit form when every
+    // lane sum is < 2^24, else the 64-bit form per candidate
+    auto rice32x2 = [&](uint32_t sa, int oa, uint32_t sb, int ob, uint32_t *bb, int *bp, int *bk) {
+        uint32_t g[2] = {sa, sb};
+        const int ord[2] = {oa, ob};
+        bb[0] = bb[1] = 0;
+        bp[0] = bp[1] = 0;
+        bk[0] = bk[1] = 0;
+#pragma unroll
+        for (int c = 0; c < 2; c++) g[c] += bfly_partner<1>(g[c]);
+#pragma unroll
+        for (int po = 5; po >= 0; po--) {
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+                if (po == 4) g[c] += bfly_partner<2>(g[c]);
+                if (po == 3) g[c] += bfly_partner<4>(g[c]);
+                if (po == 2) g[c] += bfly_partner<8>(g[c]);
+                if (po == 1) g[c] += bfly_partner<16>(g[c]);
+                if (po == 0) g[c] += bfly_partner<32>(g[c]);
+            }
+            const int lanes_per = 64 >> po;
+            const uint32_t pbase = (uint32_t)(n >> po);
+            const bool first = lane < lanes_per;
+            uint32_t contrib[2], kk[2];
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+                const uint32_t ns = first ? pbase - (uint32_t)ord[c] : pbase;
+                const uint32_t div_first = uni(0x40000u / (pbase - (uint32_t)ord[c]));
+                const uint32_t pf = (uint32_t)(((uint64_t)(g[c] - 1u) * div_first) >> 18);
+                const uint32_t pr = (g[c] - 1u) >> (12 - po);
+                const uint32_t prod = first ? pf : pr;
+                uint32_t k = (g[c] < 2 || prod == 0) ? 0u : 32u - (uint32_t)__builtin_clz(prod);
+                k = min(k, 14u);
+                kk[c] = k;
+                const uint32_t pb = 4 + (1 + k) * ns + ((2 * g[c]) >> k) - (ns >> 1);
+                contrib[c] = ((lane & (lanes_per - 1)) == 0) ? pb : 0u;
+            }
+            uint32_t tot[2];
+            dpp_wave_sum_multi<2>(contrib, tot);
+#pragma unroll
+            for (int c = 0; c < 2; c++) {
+                const uint32_t bits = 6 + tot[c];
+                if (bb[c] == 0 || bits < bb[c]) {
+                    bb[c] = bits;
+                    bp[c] = po;
+                    bk[c] = (int)kk[c];
+                }
+            }
+        }
+    };
     uint32_t rb_f = 0, rb_l = 0;
     int po_f = 0, po_l = 0, k_f = 0, k_l = 0;
-    if (cand_fixed) rice(sf, of, rb_f, po_f, k_f);
-    if (cand_lpc) rice(sl, ol, rb_l, po_l, k_l);
+    if (cand_fixed && cand_lpc && __ballot(sf >= (1u << 24) || sl >= (1u << 24)) == 0) {
+        uint32_t bb[2];
+        int bp[2], bk[2];
+        rice32x2(sf, of, sl, ol, bb, bp, bk);
+        rb_f = bb[0], po_f = bp[0], k_f = bk[0];
+        rb_l = bb[1], po_l = bp[1], k_l = bk[1];
+    } else {
+        if (cand_fixed) rice(sf, of, rb_f, po_f, k_f);
+        if (cand_lpc) rice(sl, ol, rb_l, po_l, k_l);
+    }
     // ---- choose (process_subframe_: VERBATIM, then CONSTANT | FIXED, LPC; strict <)
     uint32_t best = (uint32_t)(1 + 6 + 1 + w + n * sbps);
     int type = 1;
@@ -2129,7 +2240,11 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     // ---- phase A: sizes only (no writes to the bit buffer, which still holds the previous frame)
     int src, srx;
     sample_rate_code(P.sample_rate, src, srx);
-    const uint32_t hb = frame_header_bytes((uint32_t)fk, srx);
+    // frame header bytes: host table by frame number within the stream (words MSB-first; .w = length)
+    const bool tab = fk < hdr_n;
+    uint4 hrow = make_uint4(0, 0, 0, 0);
+    if (tab) hrow = hdr_tab[fk];
+    const uint32_t hb = tab ? (hrow.w & 0xFFu) : frame_header_bytes((uint32_t)fk, srx);
     const uint32_t hdr_bits = hb << 3;
     const uint32_t pos0 = hdr_bits + 8 + (uint32_t)w;  // after the subframe header
     uint32_t pos = pos0;
@@ -2167,12 +2282,17 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         // exact code lengths (masked warm-up samples: len 0)
         uint32_t lens = 0;
 #pragma unroll
-        for (int j = 0; j < 64; j++) {
-            if (j % 8 == 0 && j) asm volatile("" : "+v"(lens));
-            const uint32_t u = zigzag(residual_at(E, C, shift, j, X(j)));
-            uint32_t len = 1u + (uint32_t)k + (u >> k);
-            if (j < kMaxLpc && l0 && j < o) len = 0;
-            lens += len;
+        for (int m = 0; m < 32; m++) {
+            if (m % 4 == 0 && m) asm volatile("" : "+v"(lens));
+            int32_t re, ro;
+            residual_pair(E, C, shift, m, re, ro);
+            const uint32_t ue = zigzag(re), uo = zigzag(ro);
+            uint32_t le = 1u + (uint32_t)k + (ue >> k), lo = 1u + (uint32_t)k + (uo >> k);
+            if (2 * m < kMaxLpc) {
+                if (l0 && 2 * m < o) le = 0;
+                if (l0 && 2 * m + 1 < o) lo = 0;
+            }
+            lens += le + lo;
         }
         reg_fence(E);
         const uint32_t incl = dpp_incl_scan_u32(lens);
@@ -2198,6 +2318,13 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
     reg_fence(E);
     // ---- phase B: every bit of this frame into the (zeroed) buffer, then the CRC-16
+    if (l0 && tab) {
+        // 13 header bytes at most; the 4th word's low byte holds the length (byte 15: never a header byte)
+        fbuf[0] = hrow.x;
+        fbuf[1] = hrow.y;
+        fbuf[2] = hrow.z;
+        fbuf[3] = hrow.w & 0xFFFFFF00u;
+    }
     if (l0) {
         uint32_t hbits = 0, c8 = 0;
         auto put8 = [&](uint32_t b) {
@@ -2206,6 +2333,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
             hbits += 8;
         };
         const int sr = P.sample_rate;
+        if (!tab) {
         put8(0xFF);
         put8(0xF8);
         put8((uint32_t)((12 << 4) | src));  // block size code 12 = 4096
@@ -2221,6 +2349,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         else if (srx == 13) { put8((uint32_t)(sr >> 8) & 0xFF); put8((uint32_t)sr & 0xFF); }
         else if (srx == 14) { put8((uint32_t)((sr / 10) >> 8) & 0xFF); put8((uint32_t)(sr / 10) & 0xFF); }
         put8(c8);  // CRC-8 (the table lookup of the last call is unused)
+        }
         const int typecode = type == 0 ? 0 : type == 1 ? 1 : type == 2 ? 8 + of : 32 + ol - 1;
         lds_put_bits2(fbuf, hdr_bits, (uint32_t)(typecode << 1) | (w ? 1u : 0u), 8);
         if (w) lds_put_bits2(fbuf, hdr_bits + 8 + (uint32_t)(w - 1), 1, 1);
@@ -2255,17 +2384,23 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         // code = stop bit + k low bits, left-aligned: (u << (31 - k)) with the stop bit forced on
         const uint32_t sh = 31u - (uint32_t)k, oneL = 0x80000000u, lowL = (k ? (0xFFFFFFFFu >> (32 - k)) : 0u) << sh;
 #pragma unroll
-        for (int j = 0; j < 64; j++) {
-            if (j % 8 == 0 && j) asm volatile("" : "+v"(run));
-            const uint32_t u = zigzag(residual_at(E, C, shift, j, X(j)));
-            uint32_t q = u >> k, codeL = ((u << sh) & lowL) | oneL, adv = q + 1 + (uint32_t)k;
-            if (j < kMaxLpc && l0 && j < o) {
-                q = 0;
-                codeL = 0;
-                adv = 0;
+        for (int m = 0; m < 32; m++) {
+            if (m % 4 == 0 && m) asm volatile("" : "+v"(run));
+            int32_t re, ro;
+            residual_pair(E, C, shift, m, re, ro);
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int j = 2 * m + h;
+                const uint32_t u = zigzag(h ? ro : re);
+                uint32_t q = u >> k, codeL = ((u << sh) & lowL) | oneL, adv = q + 1 + (uint32_t)k;
+                if (j < kMaxLpc && l0 && j < o) {
+                    q = 0;
+                    codeL = 0;
+                    adv = 0;
+                }
+                lds_put_left(fbuf, run + q, codeL);
+                run += adv;
             }
-            lds_put_left(fbuf, run + q, codeL);
-            run += adv;
         }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS atomics have landed
@@ -2305,7 +2440,8 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
                                                   const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
                                                   const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap,
                                                   int64_t *frame_off, uint64_t *status, int *ticket_ctr, int *err,
-                                                  const int32_t *__restrict__ ftile) {
+                                                  const int32_t *__restrict__ ftile, const uint4 *__restrict__ hdr_tab,
+                                                  int hdr_n) {
     __shared__ EncV3Shared S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int i = threadIdx.x; i < 1024; i += blockDim.x) (&S.crc4[0][0])[i] = (&c_crc16x4[0][0])[i];
@@ -2340,7 +2476,7 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
         const int64_t f = fbase + wave;
         if (f < P.nframes)
             encode_frame_v3<DT>(raster, P, tiles, norms, luts, ana, arena, arena_cap, frame_off, status, err, S, want, f,
-                                lane, ftile, prev);
+                                lane, ftile, prev, hdr_tab, hdr_n);
     }
     if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
 }
@@ -2592,6 +2728,69 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         uint64_t *dstatus = ctx->status.as<uint64_t>();
         int *ticket = reinterpret_cast<int *>(dstatus + nframes);
         FRS_HIP(hipMemsetAsync(dstatus, 0, sizeof(uint64_t) * (nframes + 1), st));
+        // frame-header table by frame number within a stream (fast path: mono, 16-bit, blocksize 4096)
+        int hdr_n = 0;
+        {
+            int32_t maxf = 0;
+            for (const TileGeom &tg : tiles) maxf = std::max(maxf, tg.nframes);
+            hdr_n = std::min<int32_t>(maxf, 1 << 16);
+            if (ctx->hdr_tab_n != hdr_n || ctx->hdr_tab_sr != d->sample_rate) {
+                int src, srx = 0;
+                const int sr = d->sample_rate;
+                switch (sr) {
+                case 88200: src = 1; break;
+                case 176400: src = 2; break;
+                case 192000: src = 3; break;
+                case 8000: src = 4; break;
+                case 16000: src = 5; break;
+                case 22050: src = 6; break;
+                case 24000: src = 7; break;
+                case 32000: src = 8; break;
+                case 44100: src = 9; break;
+                case 48000: src = 10; break;
+                case 96000: src = 11; break;
+                default:
+                    if (sr <= 255000 && sr % 1000 == 0) src = srx = 12;
+                    else if (sr % 10 == 0 && sr / 10 <= 65535) src = srx = 14;
+                    else src = srx = 13;
+                }
+                uint8_t c8t[256];
+                for (int i = 0; i < 256; i++) {
+                    uint8_t c = (uint8_t)i;
+                    for (int k = 0; k < 8; k++) c = (c & 0x80) ? (uint8_t)((c << 1) ^ 0x07) : (uint8_t)(c << 1);
+                    c8t[i] = c;
+                }
+                std::vector<uint32_t> tab((size_t)hdr_n * 4, 0);
+                for (int fk = 0; fk < hdr_n; fk++) {
+                    uint8_t h[16] = {0};
+                    int hb = 0;
+                    h[hb++] = 0xFF;
+                    h[hb++] = 0xF8;
+                    h[hb++] = (uint8_t)((12 << 4) | src);
+                    h[hb++] = (uint8_t)(4 << 1);
+                    const uint32_t v = (uint32_t)fk;
+                    if (v < 0x80) h[hb++] = (uint8_t)v;
+                    else if (v < 0x800) { h[hb++] = (uint8_t)(0xC0 | (v >> 6)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+                    else { h[hb++] = (uint8_t)(0xE0 | (v >> 12)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+                    if (srx == 12) h[hb++] = (uint8_t)(sr / 1000);
+                    else if (srx == 13) { h[hb++] = (uint8_t)(sr >> 8); h[hb++] = (uint8_t)sr; }
+                    else if (srx == 14) { h[hb++] = (uint8_t)((sr / 10) >> 8); h[hb++] = (uint8_t)(sr / 10); }
+                    uint8_t c = 0;
+                    for (int i = 0; i < hb; i++) c = c8t[c ^ h[i]];
+                    h[hb++] = c;
+                    for (int w = 0; w < 4; w++)
+                        tab[(size_t)fk * 4 + w] = ((uint32_t)h[4 * w] << 24) | ((uint32_t)h[4 * w + 1] << 16) |
+                                                  ((uint32_t)h[4 * w + 2] << 8) | h[4 * w + 3];
+                    tab[(size_t)fk * 4 + 3] = (tab[(size_t)fk * 4 + 3] & 0xFFFFFF00u) | (uint32_t)hb;
+                }
+                FRS_HIP(ctx->hdr_tab.ensure(sizeof(uint32_t) * tab.size() + 16));
+                FRS_HIP(hipMemcpyAsync(ctx->hdr_tab.ptr, tab.data(), sizeof(uint32_t) * tab.size(),
+                                       hipMemcpyHostToDevice, st));
+                FRS_HIP(hipStreamSynchronize(st));
+                ctx->hdr_tab_n = hdr_n;
+                ctx->hdr_tab_sr = d->sample_rate;
+            }
+        }
         prof_begin(ctx, "encode", &ev);
         {
             int nwg_max = 0;
@@ -2601,7 +2800,8 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
             k_encode_v3<DT><<<(unsigned)grid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(), dana,
                                                             reinterpret_cast<uint8_t *>(arena_dev), arena_cap,
                                                             ctx->frame_off.as<int64_t>(), dstatus, ticket, err_flag,
-                                                            ctx->frame_tile.as<int32_t>());
+                                                            ctx->frame_tile.as<int32_t>(), ctx->hdr_tab.as<uint4>(),
+                                                            hdr_n);
         }
         prof_end(ctx, "encode", ev);
         if (P.ablate & 64) {

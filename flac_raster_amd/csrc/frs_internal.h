@@ -44,7 +44,9 @@ struct frs_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     // encode scratch
-    DevBuf tiles, norms, analysis, slots, frame_bytes, frame_off, scan_tmp, window, tile_sizes, luts, status, frame_tile;
+    DevBuf tiles, norms, analysis, slots, frame_bytes, frame_off, scan_tmp, window, tile_sizes, luts, status, frame_tile,
+        hdr_tab;
+    int hdr_tab_n = -1, hdr_tab_sr = -1;  // cached frame-header table (fast encode path)
     bool force_generic = false;  // testing: route every job through the generic kernels
     int ablate = 0;              // diagnostics: FRS_ABLATE bitmask (outputs invalid when set)
     // host staging (pinned)
