@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--queries", type=int, default=1000, help="C5 bbox-extract queries (0: skip)")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                     help="tools/pmc_traffic.py output of a rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE pass of this bench")
     return ap.parse_args()
@@ -60,16 +61,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    device = local_rank
     if world > 1:
         import torch
         import torch.distributed as tdist
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl")  # RCCL over xGMI
+        # one rank per GPU; on a box with fewer GPUs than ranks (rehearsal only) ranks share devices
+        device = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(device)
+        tdist.init_process_group(args.backend)  # "nccl" = RCCL over xGMI
         dist = tdist
 
     from flac_raster_amd import _native
 
-    ctx = _native.Context(local_rank)
+    ctx = _native.Context(device)
     T = args.tile
     W = args.width
     full_h = args.height * world
@@ -88,23 +92,27 @@ def main():
     arena = ctx.alloc(ctx.arena_bound(desc))
     ctx.sync()
 
-    sizes_dev = None
+    coll = None
     if dist is not None:
         import torch
-        sizes_dev = torch.zeros(world, trows * ((W + T - 1) // T) // world + (W + T - 1) // T * 2,
-                                dtype=torch.int64, device=f"cuda:{local_rank}")
+        coll = torch.device("cpu") if args.backend == "gloo" else torch.device(f"cuda:{device}")
+        tcols = (W + T - 1) // T
+        slot = (trows + world - 1) // world * tcols  # tiles of the largest slab
 
     def step():
         off, mn, mx, bps = ctx.encode_tiles_device(raster.ptr, desc, arena)
         if dist is not None:
             import torch
-            # spatial-index exchange: every rank's per-tile byte sizes -> global offsets (RCCL all-gather)
-            mine = torch.zeros(sizes_dev.shape[1], dtype=torch.int64, device=sizes_dev.device)
-            sz = torch.from_numpy(np.diff(off)).to(sizes_dev.device)
+            # spatial-index exchange: every rank's per-tile byte sizes -> global byte offsets (RCCL all-gather)
+            mine = torch.zeros(slot, dtype=torch.int64, device=coll)
+            sz = torch.from_numpy(np.diff(off)).to(coll)
             mine[: sz.numel()] = sz
             gathered = [torch.empty_like(mine) for _ in range(world)]
             dist.all_gather(gathered, mine)
-            torch.cuda.synchronize()
+            global_off = torch.cumsum(torch.cat(gathered), 0)  # padded slots hold 0 bytes
+            if coll.type == "cuda":
+                torch.cuda.synchronize()
+            del global_off
         return off, mn, mx
 
     for _ in range(args.warmup):
@@ -129,10 +137,10 @@ def main():
     elapsed = t1 - t0
     if dist is not None:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        px = torch.tensor([rows * W], dtype=torch.int64, device=f"cuda:{local_rank}")
+        px = torch.tensor([rows * W], dtype=torch.int64, device=coll)
         dist.all_reduce(px)
         total_px = int(px.item())
     else:
@@ -165,7 +173,8 @@ def main():
         "vs_baseline": None,
         "dtype": "int16",
         "data": "synthetic (on-device DEM recipe of SURVEY.md 8d, seed 1234)",
-        "config": {"workload": "C4 create-streaming encode", "raster": f"{full_h}x{W}x{B} int16",
+        "config": {"workload": ("C4 " if (args.height, W, B, T) == (40000, 40000, 4, 512) else "") +
+                   "create-streaming encode (band 1, device-resident) + C5 bbox extract", "raster": f"{full_h}x{W}x{B} int16",
                    "tile_size": T, "tiles_per_rank": int(ntiles), "blocksize": 4096, "compression_level": 5,
                    "parallelism": f"tile-rows sharded x{world}", "compressed_bytes_rank0": comp_bytes},
         "kernels_ms": {k: round(v, 4) for k, v in kernels.items()},
