@@ -1371,10 +1371,9 @@ __global__ void __launch_bounds__(256) k_analyze_v2(const typename Elem<DT>::T *
                                                    const int16_t *luts, const float *__restrict__ window,
                                                    SubAnalysis *out, const int32_t *__restrict__ ftile) {
     using T = typename Elem<DT>::T;
-    __shared__ float swin[kMaxBlock];
+    const float *__restrict__ swin = window;  // uniform index in every lane: scalar (SMEM) loads
     __shared__ int16_t slut[4][kLutCap];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int i = threadIdx.x; i < P.blocksize; i += blockDim.x) swin[i] = window[i];
     const int64_t f = ((int64_t)blockIdx.x * 4 + wave) * 64 + lane;
     const bool live = f < P.nframes;
     const int64_t fq = live ? f : P.nframes - 1;  // dead lanes re-read the last frame (no out-of-tile loads)
@@ -1421,18 +1420,20 @@ __global__ void __launch_bounds__(256) k_analyze_v2(const typename Elem<DT>::T *
     };
     for (int c = 0; c < kMaxBlock / 64; c++) {
         const int i0 = c * 64;
+        Chunk64<DT> chc;
+        chc.load(base, P.row_stride, g.w, crow, ccol, vec, 64);
+        advance();
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
         float xf[64];
-        {
-            Chunk64<DT> chc;
-            chc.load(base, P.row_stride, g.w, crow, ccol, vec, 64);
-            advance();
-            norm_chunk<DT>(chc, tn, lut, [&](int j, int32_t x) {
+        norm_chunk<DT>(chc, tn, lut, [&](int j, int32_t x) {
+            if ((j >> 5) == half) {
                 or_acc |= (uint32_t)x;
                 xf[j] = (float)x;
-            });
-        }
+            }
+        });
 #pragma unroll
-        for (int b = 0; b < 8; b++) {
+        for (int b = half * 4; b < half * 4 + 4; b++) {
             double cur[8];
 #pragma unroll
             for (int j = 0; j < 8; j++) cur[j] = (double)(xf[b * 8 + j] * swin[i0 + b * 8 + j]);
@@ -1446,6 +1447,7 @@ __global__ void __launch_bounds__(256) k_analyze_v2(const typename Elem<DT>::T *
             }
 #pragma unroll
             for (int j = 0; j < 8; j++) prev[j] = cur[j];
+        }
         }
     }
     if (!live) return;
