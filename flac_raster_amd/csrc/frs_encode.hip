@@ -1215,7 +1215,8 @@ __device__ inline int32_t norm_fast(typename Elem<DT>::T x, const TileNorm &tn, 
 
 // normalise 64 elements of a chunk into int32 (mode is wave-uniform in the callers' common case; the
 // switch sits outside the unrolled element loop so the loop body is branch-free)
-template <int DT> struct Chunk64;
+template <int DT, int N> struct ChunkN;
+template <int DT> using Chunk64 = ChunkN<DT, 64>;
 
 // normalise the 64 elements of a chunk (mode is wave-uniform in the encode kernel; the switch sits
 // outside the unrolled element loop so the loop body is branch-free).  emit(j, x) in order j = 0..63.
@@ -1274,15 +1275,16 @@ __device__ inline uint32_t udiv_inv(uint32_t n, uint32_t d, double inv) {
     return q;
 }
 
-// 64 consecutive elements of a frame, kept packed in 32-bit words (int16: 32 words; uint8: 16 words).
+// N (32 or 64) consecutive elements of a frame, kept packed in 32-bit words (int16, N = 64: 32 words).
 // vec: 16-byte loads of one row segment; otherwise an element gather with a row cursor.
-template <int DT> struct Chunk64 {
+template <int DT, int N> struct ChunkN {
     using T = typename Elem<DT>::T;
-    static constexpr int kWords = (int)(64 * sizeof(T) / 4);
+    static constexpr int kWords = (int)(N * sizeof(T) / 4);
+    static_assert(kWords % 4 == 0, "chunk = whole 16-byte loads");
     uint32_t w[kWords];
     __device__ inline void unpack(T *out) const {
 #pragma unroll
-        for (int j = 0; j < 64; j++) out[j] = get(j);
+        for (int j = 0; j < N; j++) out[j] = get(j);
     }
     __device__ inline T get(int j) const {  // j must be a compile-time constant after unrolling
         if constexpr (sizeof(T) == 1) return (T)((w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
@@ -1365,92 +1367,9 @@ __device__ inline void norm_block8(const Chunk64<DT> &ch, int b, const TileNorm 
     }
 }
 
-template <int DT>
-__global__ void __launch_bounds__(256) k_analyze_v2(const typename Elem<DT>::T *raster, EncodeParams P,
-                                                   const TileGeom *tiles, const TileNorm *norms,
-                                                   const int16_t *luts, const float *__restrict__ window,
-                                                   SubAnalysis *out, const int32_t *__restrict__ ftile) {
-    using T = typename Elem<DT>::T;
-    const float *__restrict__ swin = window;  // uniform index in every lane: scalar (SMEM) loads
-    __shared__ int16_t slut[4][kLutCap];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t f = ((int64_t)blockIdx.x * 4 + wave) * 64 + lane;
-    const bool live = f < P.nframes;
-    const int64_t fq = live ? f : P.nframes - 1;  // dead lanes re-read the last frame (no out-of-tile loads)
-    const int t = ftile[fq];
-    const TileGeom g = tiles[t];
-    const int64_t s0 = (fq - g.frame_base) * P.blocksize;
-    const int64_t tile_px = (int64_t)g.h * g.w;
-    const int n = live ? (int)min((int64_t)P.blocksize, tile_px - s0) : 0;
-    TileNorm tn = norms[t];
-    // LUT: one per wave when the wave's frames share a tile; other LUT tiles take the exact division
-    const int t0 = __shfl(t, 0);
-    const bool uni = __all(t == t0);
-    const bool wave_lut = uni && tn.mode == kNormLut;
-    if (wave_lut) {
-        const int64_t R = tn.imax - tn.imin;
-        const int16_t *src = luts + (int64_t)t0 * kLutCap;
-        for (int64_t d = lane; d <= R; d += 64) slut[wave][d] = src[d];
-    }
-    __syncthreads();
-    const int16_t *lut = wave_lut ? slut[wave] : luts + (int64_t)t * kLutCap;
-    const T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
-    const bool vec = P.vec_ok && (g.w % 64) == 0;
-
-    uint32_t or_acc = 0;
-    double acc[kMaxLpc + 1];
-#pragma unroll
-    for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
-    double prev[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) prev[j] = 0.0;
-
-    // fast path: every frame is a full block (host guarantees), 64 chunks of 64 samples per lane; a
-    // row/column cursor walks the tile (no per-chunk division); the next chunk's loads are issued before
-    // the current chunk's FMAs
-    const uint32_t r0 = udiv_inv((uint32_t)s0, (uint32_t)g.w, 1.0 / (double)g.w);
-    int64_t crow = r0;
-    int ccol = (int)((uint32_t)s0 - r0 * (uint32_t)g.w);
-    auto advance = [&]() {
-        ccol += 64;
-        while (ccol >= g.w) {
-            ccol -= g.w;
-            crow++;
-        }
-    };
-    for (int c = 0; c < kMaxBlock / 64; c++) {
-        const int i0 = c * 64;
-        Chunk64<DT> chc;
-        chc.load(base, P.row_stride, g.w, crow, ccol, vec, 64);
-        advance();
-#pragma unroll
-        for (int half = 0; half < 2; half++) {
-        float xf[64];
-        norm_chunk<DT>(chc, tn, lut, [&](int j, int32_t x) {
-            if ((j >> 5) == half) {
-                or_acc |= (uint32_t)x;
-                xf[j] = (float)x;
-            }
-        });
-#pragma unroll
-        for (int b = half * 4; b < half * 4 + 4; b++) {
-            double cur[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) cur[j] = (double)(xf[b * 8 + j] * swin[i0 + b * 8 + j]);
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-#pragma unroll
-                for (int l = 0; l <= kMaxLpc; l++) {
-                    const double other = (j - l >= 0) ? cur[j - l] : prev[8 + j - l];
-                    acc[l] = fma(cur[j], other, acc[l]);
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 8; j++) prev[j] = cur[j];
-        }
-        }
-    }
-    if (!live) return;
+// wasted bits, LPC order choice (expected bits), Levinson coefficients and quantisation of one frame from its
+// windowed autocorrelation sums (stream_encoder.c process_subframe_ / lpc.c; shared by k_analyze_v2/v3)
+__device__ inline SubAnalysis analysis_finish(const double *acc, uint32_t or_acc, int n, const EncodeParams &P) {
     SubAnalysis A;
     A.n = n;
     int w = or_acc ? __builtin_ctz(or_acc) : 0;
@@ -1549,7 +1468,216 @@ __global__ void __launch_bounds__(256) k_analyze_v2(const typename Elem<DT>::T *
             }
         }
     }
-    out[f] = A;
+    return A;
+}
+
+template <int DT>
+__global__ void __launch_bounds__(256) k_analyze_v2(const typename Elem<DT>::T *raster, EncodeParams P,
+                                                   const TileGeom *tiles, const TileNorm *norms,
+                                                   const int16_t *luts, const float *__restrict__ window,
+                                                   SubAnalysis *out, const int32_t *__restrict__ ftile) {
+    using T = typename Elem<DT>::T;
+    const float *__restrict__ swin = window;  // uniform index in every lane: scalar (SMEM) loads
+    __shared__ int16_t slut[4][kLutCap];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t f = ((int64_t)blockIdx.x * 4 + wave) * 64 + lane;
+    const bool live = f < P.nframes;
+    const int64_t fq = live ? f : P.nframes - 1;  // dead lanes re-read the last frame (no out-of-tile loads)
+    const int t = ftile[fq];
+    const TileGeom g = tiles[t];
+    const int64_t s0 = (fq - g.frame_base) * P.blocksize;
+    const int64_t tile_px = (int64_t)g.h * g.w;
+    const int n = live ? (int)min((int64_t)P.blocksize, tile_px - s0) : 0;
+    TileNorm tn = norms[t];
+    // LUT: one per wave when the wave's frames share a tile; other LUT tiles take the exact division
+    const int t0 = __shfl(t, 0);
+    const bool uni = __all(t == t0);
+    const bool wave_lut = uni && tn.mode == kNormLut;
+    if (wave_lut) {
+        const int64_t R = tn.imax - tn.imin;
+        const int16_t *src = luts + (int64_t)t0 * kLutCap;
+        for (int64_t d = lane; d <= R; d += 64) slut[wave][d] = src[d];
+    }
+    __syncthreads();
+    const int16_t *lut = wave_lut ? slut[wave] : luts + (int64_t)t * kLutCap;
+    const T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
+    const bool vec = P.vec_ok && (g.w % 64) == 0;
+
+    uint32_t or_acc = 0;
+    double acc[kMaxLpc + 1];
+#pragma unroll
+    for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
+    double prev[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) prev[j] = 0.0;
+
+    // fast path: every frame is a full block (host guarantees), 64 chunks of 64 samples per lane; a
+    // row/column cursor walks the tile (no per-chunk division); the next chunk's loads are issued before
+    // the current chunk's FMAs
+    const uint32_t r0 = udiv_inv((uint32_t)s0, (uint32_t)g.w, 1.0 / (double)g.w);
+    int64_t crow = r0;
+    int ccol = (int)((uint32_t)s0 - r0 * (uint32_t)g.w);
+    auto advance = [&]() {
+        ccol += 64;
+        while (ccol >= g.w) {
+            ccol -= g.w;
+            crow++;
+        }
+    };
+    for (int c = 0; c < kMaxBlock / 64; c++) {
+        const int i0 = c * 64;
+        Chunk64<DT> chc;
+        chc.load(base, P.row_stride, g.w, crow, ccol, vec, 64);
+        advance();
+#pragma unroll
+        for (int half = 0; half < 2; half++) {
+        float xf[64];
+        norm_chunk<DT>(chc, tn, lut, [&](int j, int32_t x) {
+            if ((j >> 5) == half) {
+                or_acc |= (uint32_t)x;
+                xf[j] = (float)x;
+            }
+        });
+#pragma unroll
+        for (int b = half * 4; b < half * 4 + 4; b++) {
+            double cur[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) cur[j] = (double)(xf[b * 8 + j] * swin[i0 + b * 8 + j]);
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+#pragma unroll
+                for (int l = 0; l <= kMaxLpc; l++) {
+                    const double other = (j - l >= 0) ? cur[j - l] : prev[8 + j - l];
+                    acc[l] = fma(cur[j], other, acc[l]);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) prev[j] = cur[j];
+        }
+        }
+    }
+    if (!live) return;
+    out[f] = analysis_finish(acc, or_acc, n, P);
+}
+
+// ------------------------------------------------------------------------------ k_analyze_v3
+// Same per-frame arithmetic as k_analyze_v2 (lane = frame, libFLAC's sequential fp64 autocorrelation), laid
+// out for occupancy and memory-level parallelism: a wave takes up to 64 frames of ONE tile (host wave table),
+// so the normaliser is wave-uniform and chosen once (LUT in LDS read by ds_read / zeros / fast division /
+// exact division) instead of a per-sample switch; each lane loads its next 64 samples as one 128-byte line
+// (8 x 16 B; 16 samples in the fp64-division class) and normalises them 8 at a time straight into doubles.
+constexpr int kAnaKindLds = 0, kAnaKindZero = 1, kAnaKindFastDiv = 2, kAnaKindGeneric = 3;
+
+template <int DT, int KIND>
+__device__ inline int32_t ana_norm(typename Elem<DT>::T x, const TileNorm &tn, const int16_t *slut,
+                                   const int16_t *glut) {
+    if constexpr (KIND == kAnaKindLds) {
+        return (int32_t)slut[(int32_t)x - (int32_t)tn.imin];
+    } else if constexpr (KIND == kAnaKindZero) {
+        return 0;
+    } else if constexpr (KIND == kAnaKindFastDiv) {
+        const double a = (double)(2 * ((int32_t)x - (int32_t)tn.imin));
+        const double q0 = a * tn.rinv;
+        const double r = fma(-q0, tn.den, a);
+        const double q1 = fma(r, tn.rinv, q0);
+        return (int32_t)(int16_t)(int32_t)((q1 - 1.0) * 32767.0);
+    } else {
+        return norm_fast<DT>(x, tn, glut);
+    }
+}
+
+template <int DT, int KIND, int kAnaChunk>
+__device__ inline void ana_autoc(const typename Elem<DT>::T *base, const EncodeParams &P, const TileGeom &g,
+                                 int64_t s0, const TileNorm &tn, const int16_t *slut, const int16_t *glut,
+                                 const float *__restrict__ swin, bool vec, double *acc, uint32_t &or_acc) {
+    using Ch = ChunkN<DT, kAnaChunk>;
+    const uint32_t r0 = udiv_inv((uint32_t)s0, (uint32_t)g.w, 1.0 / (double)g.w);
+    int64_t crow = r0;
+    int ccol = (int)((uint32_t)s0 - r0 * (uint32_t)g.w);
+    double prev[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) prev[j] = 0.0;
+    for (int c = 0; c < kMaxBlock / kAnaChunk; c++) {
+        const int i0 = c * kAnaChunk;
+        Ch ch;
+        ch.load(base, P.row_stride, g.w, crow, ccol, vec, kAnaChunk);
+        ccol += kAnaChunk;
+        while (ccol >= g.w) {
+            ccol -= g.w;
+            crow++;
+        }
+#pragma unroll
+        for (int b = 0; b < kAnaChunk / 8; b++) {
+            double cur[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int32_t x = ana_norm<DT, KIND>(ch.get(8 * b + j), tn, slut, glut);
+                or_acc |= (uint32_t)x;
+                cur[j] = (double)((float)x * swin[i0 + 8 * b + j]);  // lpc.c window_data: float product
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+#pragma unroll
+                for (int l = 0; l <= kMaxLpc; l++) acc[l] = fma(cur[j], (j - l >= 0) ? cur[j - l] : prev[8 + j - l], acc[l]);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; j++) prev[j] = cur[j];
+        }
+    }
+}
+
+// Two launches of one kernel body keep the common case lean: SLOW = false takes the tiles normalised by LUT (or
+// zeros) -- ~120 VGPRs, 4 waves/SIMD; SLOW = true takes the fast-division / exact-division tiles, whose fp64
+// normalisation needs more registers.  A wave of the other class returns at once.
+template <int DT, bool SLOW>
+__global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *raster, EncodeParams P,
+                                                   const TileGeom *tiles, const TileNorm *norms,
+                                                   const int16_t *luts, const float *__restrict__ window,
+                                                   SubAnalysis *out, const int2 *__restrict__ wtab, int nwaves) {
+    __shared__ int16_t slut[SLOW ? 1 : 4][SLOW ? 1 : kLutCap];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wv = blockIdx.x * 4 + wave;
+    if (wv >= nwaves) return;
+    const int2 wt = wtab[wv];  // (tile, first frame of the tile handled by this wave)
+    const int t = wt.x;
+    const TileNorm tn = norms[t];
+    const int mode = tn.mode;  // wave-uniform: one tile per wave
+    const bool lean = mode == kNormLut || mode == kNormZero;
+    if (lean == SLOW) return;
+    const TileGeom g = tiles[t];
+    const bool live = wt.y + lane < g.nframes;
+    const int64_t fk = live ? wt.y + lane : g.nframes - 1;  // dead lanes re-read the tile's last frame
+    const int64_t f = g.frame_base + fk;
+    const int64_t s0 = fk * P.blocksize;
+    const int64_t tile_px = (int64_t)g.h * g.w;
+    const int n = live ? (int)min((int64_t)P.blocksize, tile_px - s0) : 0;
+    const typename Elem<DT>::T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
+    constexpr int kChunk = SLOW ? 16 : 64;  // samples per lane load (SLOW: fewer VGPRs beside the fp64 division)
+    const bool vec = P.vec_ok && (g.w % kChunk) == 0;
+    const int16_t *glut = luts + (int64_t)t * kLutCap;
+    double acc[kMaxLpc + 1];
+#pragma unroll
+    for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
+    uint32_t or_acc = 0;
+    if constexpr (!SLOW) {
+        int16_t *wl = slut[wave];
+        if (mode == kNormLut) {
+            const int64_t R = tn.imax - tn.imin;
+            for (int64_t d = lane; d <= R; d += 64) wl[d] = glut[d];
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's LUT stores have landed (each wave reads only its own)
+            __builtin_amdgcn_wave_barrier();
+            ana_autoc<DT, kAnaKindLds, kChunk>(base, P, g, s0, tn, wl, glut, window, vec, acc, or_acc);
+        } else {
+            ana_autoc<DT, kAnaKindZero, kChunk>(base, P, g, s0, tn, wl, glut, window, vec, acc, or_acc);
+        }
+    } else {
+        if (mode == kNormFastDiv)
+            ana_autoc<DT, kAnaKindFastDiv, kChunk>(base, P, g, s0, tn, nullptr, glut, window, vec, acc, or_acc);
+        else
+            ana_autoc<DT, kAnaKindGeneric, kChunk>(base, P, g, s0, tn, nullptr, glut, window, vec, acc, or_acc);
+    }
+    if (!live) return;
+    out[f] = analysis_finish(acc, or_acc, n, P);
 }
 
 // ---- wave helpers (64 lanes)
@@ -2722,10 +2850,27 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         FRS_HIP(ctx->frame_tile.ensure(sizeof(int32_t) * nframes));
         k_frame_tile<<<ntiles, 64, 0, st>>>(dtiles, ntiles, ctx->frame_tile.as<int32_t>());
         prof_begin(ctx, "analyze", &ev);
-        k_analyze_v2<DT><<<(unsigned)((nframes + 255) / 256), 256, 0, st>>>(raster, P, dtiles, dnorms,
-                                                                             ctx->luts.as<int16_t>(),
-                                                                             ctx->window.as<float>(), dana,
-                                                                             ctx->frame_tile.as<int32_t>());
+        if (P.ablate & 256) {  // diagnostics: the previous analysis kernel (A/B)
+            k_analyze_v2<DT><<<(unsigned)((nframes + 255) / 256), 256, 0, st>>>(
+                raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(), ctx->window.as<float>(), dana,
+                ctx->frame_tile.as<int32_t>());
+        } else {
+            // wave table: (tile, first frame) per wave, up to 64 frames of one tile each
+            std::vector<int2> wt;
+            wt.reserve((size_t)(nframes / 64 + ntiles));
+            for (int ti = 0; ti < ntiles; ti++)
+                for (int k0 = 0; k0 < tiles[ti].nframes; k0 += 64) wt.push_back(make_int2(ti, k0));
+            const int nwaves = (int)wt.size();
+            FRS_HIP(ctx->wave_tab.ensure(sizeof(int2) * wt.size()));
+            FRS_HIP(hipMemcpyAsync(ctx->wave_tab.ptr, wt.data(), sizeof(int2) * wt.size(), hipMemcpyHostToDevice, st));
+            const unsigned wgrid = (unsigned)((nwaves + 3) / 4);
+            k_analyze_v3<DT, false><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
+                                                           ctx->window.as<float>(), dana, ctx->wave_tab.as<int2>(),
+                                                           nwaves);
+            k_analyze_v3<DT, true><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
+                                                          ctx->window.as<float>(), dana, ctx->wave_tab.as<int2>(),
+                                                          nwaves);
+        }
         prof_end(ctx, "analyze", ev);
         uint64_t *dstatus = ctx->status.as<uint64_t>();
         int *ticket = reinterpret_cast<int *>(dstatus + nframes);
