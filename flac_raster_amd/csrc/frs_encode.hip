@@ -2046,11 +2046,20 @@ __device__ inline void resolve_and_store(const EncodeParams &P, PendingFrame &pf
         const uint32_t n16 = ((uint32_t)fbytes - a0) >> 4;
         const uint32_t r = a0 & 3, sb = a0 >> 2;
         uint4 *d16 = reinterpret_cast<uint4 *>(dst + a0);
+        // words sb .. sb + 4 of chunk ci from two 16-B aligned LDS reads (ds_read_b128: consecutive lanes hit
+        // consecutive banks; five dword reads at a 4-word lane stride were 4-way bank conflicts)
+        const uint4 *fb4 = reinterpret_cast<const uint4 *>(fbuf);
         for (uint32_t ci = (uint32_t)lane; ci < n16; ci += 64) {
-            const uint32_t s = sb + 4 * ci;
-            const uint32_t w0 = __builtin_bswap32(fbuf[s]), w1 = __builtin_bswap32(fbuf[s + 1]);
-            const uint32_t w2 = __builtin_bswap32(fbuf[s + 2]), w3 = __builtin_bswap32(fbuf[s + 3]);
-            const uint32_t w4 = __builtin_bswap32(fbuf[s + 4]);
+            const uint4 A4 = fb4[ci], B4 = fb4[ci + 1];
+            uint32_t v0, v1, v2, v3, v4;
+            switch (sb) {  // wave-uniform
+            case 0: v0 = A4.x; v1 = A4.y; v2 = A4.z; v3 = A4.w; v4 = B4.x; break;
+            case 1: v0 = A4.y; v1 = A4.z; v2 = A4.w; v3 = B4.x; v4 = B4.y; break;
+            case 2: v0 = A4.z; v1 = A4.w; v2 = B4.x; v3 = B4.y; v4 = B4.z; break;
+            default: v0 = A4.w; v1 = B4.x; v2 = B4.y; v3 = B4.z; v4 = B4.w; break;
+            }
+            const uint32_t w0 = __builtin_bswap32(v0), w1 = __builtin_bswap32(v1), w2 = __builtin_bswap32(v2);
+            const uint32_t w3 = __builtin_bswap32(v3), w4 = __builtin_bswap32(v4);
             uint4 o4;
             o4.x = __builtin_amdgcn_alignbyte(w1, w0, r);
             o4.y = __builtin_amdgcn_alignbyte(w2, w1, r);
@@ -2539,7 +2548,8 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     if (ok && !(P.ablate & 2)) {
         // slice-by-4 over 32-bit words, one contiguous word range per lane, combined with x^(8m) factors
         const uint32_t nfw = body >> 2, tail = body & 3;
-        const uint32_t cw = (nfw + 63) >> 6;
+        // odd words per lane: lane bases cw apart fall in 32 distinct LDS banks (cw = 32 would be 32-way)
+        const uint32_t cw = ((nfw + 63) >> 6) | 1u;
         const uint32_t wb = min(nfw, (uint32_t)lane * cw), we = min(nfw, wb + cw);
         uint32_t c = 0;
         for (uint32_t i = wb; i < we; i++) {
