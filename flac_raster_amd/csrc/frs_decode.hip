@@ -13,6 +13,8 @@
 // that the subframes end exactly at the CRC footer.
 #include <hipcub/hipcub.hpp>
 
+#include <type_traits>
+
 #include "frs_internal.h"
 
 namespace frs {
@@ -666,10 +668,386 @@ __global__ void __launch_bounds__(64) k_decode_frames(const uint8_t *blob, const
                      blocksize, nvalid, nullptr, nullptr);
 }
 
-// One wave per frame: the frame's bytes are staged in LDS by the whole wave (coalesced dword loads), then
-// lane 0 decodes from LDS (bit refills are LDS reads instead of dependent global loads).  Frames larger
-// than the stage are decoded straight from global memory.
+// ------------------------------------------------------------------ wave-uniform (scalar-unit) frame decoder
+// A subframe's Rice codes are a sequential bit walk and its LPC restore a nonlinear recurrence, so one frame is
+// serial work.  It runs here on the scalar unit: every value is wave-uniform (SGPRs: s_flbit_i32_b64,
+// s_lshl_b64, s_mul_i32 at scalar latency) instead of lane 0's dependent VALU chain.  Bitstream words reach the
+// scalar unit through a VGPR window (lane i = stage word wbase + i, one ds_read per 64 words) and v_readlane;
+// decoded samples leave through v_writelane into a VGPR stored by one coalesced write per 64 samples.
 constexpr int kDecStageWords = 6144;  // 24 KB
+
+struct WaveBits {
+    const uint32_t *stage;  // LDS: big-endian (byte-swapped) dwords of the blob from byte 4 * wb
+    uint32_t win;           // stage[wbase + lane]
+    uint32_t wbase, wi;     // window base and next word to take (stage word indices)
+    uint32_t wlim;          // words staged
+    uint64_t c;             // left-aligned bit cache
+    int n;                  // valid bits in c
+    int lane;
+    __device__ inline uint32_t word(uint32_t i) {
+        if (i - wbase >= 64u) {
+            wbase = i & ~63u;
+            win = stage[min(wbase + (uint32_t)lane, wlim)];
+        }
+        return (uint32_t)__builtin_amdgcn_readlane((int)win, (int)(i - wbase));
+    }
+    __device__ inline void refill() {
+        while (n <= 32) refill1();
+    }
+    __device__ inline void refill1() {  // one word (callers guarantee 0 < n <= 32)
+        c |= (uint64_t)word(wi++) << (32 - n);
+        n += 32;
+    }
+    __device__ inline void init(const uint32_t *st, uint32_t nwords, uint32_t bitpos, int ln) {
+        stage = st;
+        wlim = nwords;
+        lane = ln;
+        wbase = 0u - 64u;
+        wi = bitpos >> 5;
+        c = (uint64_t)word(wi++) << 32;
+        n = 32;
+        const int off = (int)(bitpos & 31);
+        c <<= off;
+        n -= off;
+        refill();
+    }
+    __device__ inline uint32_t bits(int k) {  // k <= 32; n > 32 on entry
+        if (k == 0) return 0;
+        const uint32_t v = (uint32_t)(c >> (64 - k));
+        c <<= k;
+        n -= k;
+        refill();
+        return v;
+    }
+    __device__ inline int32_t sbits(int k) {
+        const uint32_t v = bits(k);
+        return (k == 0 || k == 32) ? (int32_t)v : ((int32_t)(v << (32 - k)) >> (32 - k));
+    }
+    __device__ inline uint32_t pos() const { return wi * 32 - (uint32_t)n; }
+    // zeros before the next 1 (the 1 is consumed); false past `lim` bits (corrupt data)
+    __device__ inline bool unary(uint32_t &q, uint32_t lim) {
+        q = 0;
+        while (c == 0) {  // the cache holds n (> 32) zero bits
+            q += (uint32_t)n;
+            n = 0;
+            refill();
+            if (pos() > lim) return false;
+        }
+        const int z = __builtin_clzll(c);  // < n: the cache's bits below n are zero
+        q += (uint32_t)z;
+        c = (z + 1 >= 64) ? 0 : (c << (z + 1));
+        n -= z + 1;
+        refill();
+        return true;
+    }
+};
+
+// ------------------------------------------------------------------ two-wave pipelined frame decoder
+// A lone wave issues one instruction every ~6 (SALU) to ~8 (VALU) cycles (tools/micro/issue_rates.hip), so a
+// frame's decode time is its serial instruction count.  k_decode_frames_pipe splits that count over two waves of
+// one work-group (same CU): wave 0 parses the frame on the scalar unit and Rice-decodes the residuals into LDS,
+// 64 at a time, publishing progress; wave 1 restores the samples behind it -- the LPC recurrence as a v_dot2
+// chain over the eight newest samples held as packed int16 pairs -- and writes them to LDS, copied to the PCM
+// output at the end.  Mono 16-bit FIXED / LPC (order <= 8, 32-bit-safe prediction) / CONSTANT / VERBATIM
+// subframes; anything else falls back to decode_one_frame on wave 0, lane 0.
+typedef short dec_v2s16 __attribute__((ext_vector_type(2)));
+__device__ inline int32_t dec_dot2(uint32_t a, uint32_t b, int32_t c) {  // v_dot2_i32_i16
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(dec_v2s16, a), __builtin_bit_cast(dec_v2s16, b), c, false);
+}
+constexpr int kPipeFallback = 1, kPipeDone = 2, kPipeRestore = 3, kPipeError = 4;
+struct PipeInfo {
+    int32_t state;       // 0 while parsing, then kPipe*
+    int32_t progress;    // residuals published in resbuf (samples [o, progress) are ready)
+    int32_t valid;       // producer's verdict at the end: 1 = frame ends at its CRC footer
+    int32_t finished;    // producer done (valid final)
+    int32_t o, shift, w, bs;
+    int32_t cq[8];
+    int32_t wu[8];
+};
+
+__device__ inline void lds_publish(volatile int32_t *p, int32_t v) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's earlier LDS writes have landed
+    *p = v;
+}
+__device__ inline int32_t lds_poll(volatile int32_t *p) { return *p; }
+
+__global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob, const int64_t *soff, int ns,
+                                                           const int64_t *poff, const int64_t *cpos,
+                                                           const int64_t *ends, const int64_t *fbase,
+                                                           const int64_t *frame_cand, int64_t nframes, int channels,
+                                                           int stream_bps, int32_t *pcm, int blocksize, int *nvalid) {
+    __shared__ uint32_t stage[kDecStageWords + 4];
+    __shared__ int32_t resbuf[kDecResMax];
+    __shared__ uint32_t xout[kDecResMax / 2];  // restored samples as int16 pairs
+    __shared__ PipeInfo info;
+    const int64_t fi = blockIdx.x;
+    if (fi >= nframes) return;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t ci = frame_cand[fi];
+    const int64_t fpos = cpos[ci], fend_known = ends[ci];
+    const int s = stream_of(soff, ns, fpos);
+    const int64_t send = soff[s + 1];
+    const int64_t wb = fpos >> 2, we = (fend_known + 3) >> 2;
+    const bool staged = we - wb <= kDecStageWords;
+    if (staged)  // big-endian words: the scalar bit reader needs no byte swap
+        for (int64_t k = threadIdx.x; k < we - wb + 4; k += 128)
+            stage[k] = __builtin_bswap32(load_word_guarded(blob, wb + k, send));
+    if (threadIdx.x == 0) {
+        info.state = 0;
+        info.progress = 0;
+        info.finished = 0;
+        info.valid = 0;
+    }
+    __syncthreads();
+    const int64_t nsamp = poff[s + 1] - poff[s];
+    const int64_t kk = fi - fbase[s];
+    const int64_t first = kk * blocksize;
+    int32_t *out = pcm + (poff[s] + first);
+    volatile PipeInfo *vi = &info;
+    if (wave == 0) {
+        // ================= producer: parse + Rice decode (wave-uniform, scalar unit)
+        auto finish = [&](int st, int valid) {
+            if (lane == 0) {
+                info.valid = valid;
+                lds_publish(&vi->finished, 1);
+                if (st) lds_publish(&vi->state, st);
+            }
+        };
+        if (!staged) {
+            finish(kPipeFallback, 0);
+            if (lane == 0)
+                decode_one_frame(blob, blob, 0, soff, ns, poff, cpos, ends, fbase, frame_cand, fi, channels,
+                                 stream_bps, pcm, blocksize, nvalid, resbuf, nullptr);
+            return;
+        }
+        const FrameHdr cd = parse_header(blob, fpos, send, channels, stream_bps);
+        if (!cd.ok || cd.frame_no != kk || cd.bs > blocksize || first + cd.bs > nsamp) {
+            finish(kPipeError, 0);
+            return;
+        }
+        const int bs = __builtin_amdgcn_readfirstlane(cd.bs);
+        const uint32_t lim = (uint32_t)((fend_known - 4 * wb) * 8);
+        WaveBits br;
+        br.init(stage, (uint32_t)(we - wb + 3), (uint32_t)((fpos + cd.hdr_len - 4 * wb) * 8), lane);
+        br.bits(1);
+        const int t = (int)br.bits(6);
+        int w = 0;
+        if (br.bits(1)) {
+            uint32_t q;
+            if (!br.unary(q, lim)) { finish(kPipeError, 0); return; }
+            w = (int)q + 1;
+        }
+        const int sbps = __builtin_amdgcn_readfirstlane(cd.bps) - w;
+        auto fallback = [&]() {
+            finish(kPipeFallback, 0);
+            for (int64_t k = lane; k < we - wb + 4; k += 64) stage[k] = __builtin_bswap32(stage[k]);  // back to LE
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0)
+                decode_one_frame(blob, reinterpret_cast<const uint8_t *>(stage), wb * 4, soff, ns, poff, cpos, ends,
+                                 fbase, frame_cand, fi, channels, stream_bps, pcm, blocksize, nvalid, resbuf, stage);
+        };
+        if (cd.bps > 16 || sbps <= 0) { fallback(); return; }
+        auto end_ok = [&]() { return (int64_t)((br.pos() + 7) >> 3) + 4 * wb + 2 == fend_known; };
+        if (t == 0) {  // CONSTANT
+            const int32_t v = br.sbits(sbps);
+            for (int i = lane; i < bs; i += 64) out[i] = (int32_t)((uint32_t)v << w);
+            const int ok = end_ok();
+            if (ok && lane == 0) atomicAdd(nvalid, 1);
+            finish(kPipeDone, ok);
+            return;
+        }
+        if (t == 1) {  // VERBATIM: samples straight out, 64 per coalesced store
+            uint32_t vo = 0;
+            for (int i = 0; i < bs; i++) {
+                const int32_t x = br.sbits(sbps);
+                vo = lane == (i & 63) ? ((uint32_t)x << w) : vo;
+                if ((i & 63) == 63 || i == bs - 1) {
+                    const int b0 = i & ~63;
+                    if (b0 + lane <= i) out[b0 + lane] = (int32_t)vo;
+                }
+            }
+            const int ok = end_ok();
+            if (ok && lane == 0) atomicAdd(nvalid, 1);
+            finish(kPipeDone, ok);
+            return;
+        }
+        if (!((t >= 8 && t <= 12) || (t >= 32 && t <= 39))) { fallback(); return; }
+        const bool lpc = t >= 32;
+        const int o = lpc ? t - 31 : t - 8;
+        if (o > bs) { finish(kPipeError, 0); return; }
+        int32_t wu[8], cq[8];
+#pragma unroll
+        for (int m = 0; m < 8; m++) {
+            wu[m] = 0;
+            cq[m] = 0;
+        }
+#pragma unroll
+        for (int m = 0; m < 8; m++)
+            if (m < o) wu[m] = br.sbits(sbps);
+        int shift = 0, prec = 3;
+        if (lpc) {
+            prec = (int)br.bits(4) + 1;
+            if (prec == 16) { finish(kPipeError, 0); return; }
+            shift = br.sbits(5);
+            if (shift < 0) { finish(kPipeError, 0); return; }
+#pragma unroll
+            for (int m = 0; m < 8; m++)
+                if (m < o) cq[m] = br.sbits(prec);
+        } else {
+            if (o >= 1) cq[0] = o == 1 ? 1 : o == 2 ? 2 : o == 3 ? 3 : 4;
+            if (o >= 2) cq[1] = o == 2 ? -1 : o == 3 ? -3 : -6;
+            if (o >= 3) cq[2] = o == 3 ? 1 : 4;
+            if (o >= 4) cq[3] = -1;
+        }
+        int lg = 0;
+        while ((1 << lg) < o) lg++;
+        // 16-bit samples and coefficients for the v_dot2 restore, 32-bit-safe prediction
+        if (!(sbps <= 16 && prec <= 16 && prec + sbps + lg <= 31)) { fallback(); return; }
+        const int method = (int)br.bits(2);
+        if (method > 1) { finish(kPipeError, 0); return; }
+        const int po = (int)br.bits(4);
+        if ((bs >> po) < o || (bs & ((1 << po) - 1))) { finish(kPipeError, 0); return; }
+        if (lane == 0) {
+            info.o = o;
+            info.shift = shift;
+            info.w = w;
+            info.bs = bs;
+#pragma unroll
+            for (int m = 0; m < 8; m++) {
+                info.cq[m] = cq[m];
+                info.wu[m] = wu[m];
+            }
+            lds_publish(&vi->state, kPipeRestore);
+        }
+        const int pb = method == 0 ? 4 : 5, esc = (1 << pb) - 1;
+        const int psz = bs >> po;
+        uint32_t vr = 0, vu = 0;
+        uint64_t vesc = 0;  // lanes of the current 64-sample group filled by an escaped partition
+        int i = o;
+        bool bad = false;
+        // residuals of the 64-sample group ending at sample `last` into resbuf, then publish them
+        auto flush = [&](int last) {
+            const uint32_t zz = (vu >> 1) ^ (uint32_t)(-(int32_t)(vu & 1));
+            resbuf[(last & ~63) + lane] = (int32_t)(((vesc >> lane) & 1) ? vr : zz);
+            vesc = 0;
+            if (lane == 0 && last + 1 < bs) lds_publish(&vi->progress, last + 1);
+        };
+        for (int p = 0; p < (1 << po) && !bad; p++) {
+            const int kp = (int)br.bits(pb);
+            const int pe = (p + 1) * psz;
+            if (kp == esc) {
+                const int nb = (int)br.bits(5);
+                for (; i < pe; i++) {
+                    const int32_t r = nb ? br.sbits(nb) : 0;
+                    vr = lane == (i & 63) ? (uint32_t)r : vr;
+                    vesc |= 1ull << (i & 63);
+                    if ((i & 63) == 63) flush(i);
+                }
+            } else {
+                const int k1 = kp + 1;
+                const uint32_t kmask = (1u << kp) - 1u;
+                // one Rice code from the cache: zeros z, stop bit, kp low bits; false on corrupt data
+                auto code = [&](uint32_t &u) -> bool {
+                    const int z = __builtin_clzll(br.c | 1);
+                    const int tot = z + k1;
+                    if (tot < br.n) {  // the whole code is in the cache
+                        u = ((uint32_t)z << kp) | ((uint32_t)(br.c >> (64 - tot)) & kmask);
+                        br.c <<= tot;
+                        br.n -= tot;
+                        if (br.n <= 32) br.refill1();
+                        return true;
+                    }
+                    uint32_t q;
+                    if (!br.unary(q, lim)) return false;
+                    u = (q << kp) | br.bits(kp);
+                    return true;
+                };
+                for (; i < pe; i++) {
+                    uint32_t u;
+                    if (!code(u)) {
+                        bad = true;
+                        break;
+                    }
+                    vu = lane == (i & 63) ? u : vu;  // zig-zag codes; decoded 64 at a time on the vector unit
+                    if ((i & 63) == 63) flush(i);
+                }
+            }
+        }
+        if (!bad && (bs & 63)) flush(bs - 1);  // the last partial group
+        const int ok = !bad && end_ok();
+        if (lane == 0) {
+            info.valid = ok;
+            lds_publish(&vi->progress, bad ? -1 : bs);
+            lds_publish(&vi->finished, 1);
+        }
+        return;
+    }
+    // ================= consumer (wave 1): LPC / FIXED restore behind the producer
+    int st;
+    while ((st = lds_poll(&vi->state)) == 0) __builtin_amdgcn_s_sleep(1);
+    if (st != kPipeRestore) return;  // handled by the producer
+    const int o = info.o, shift = info.shift, w = info.w, bs = info.bs;
+    // coefficient pairs C[k] = (c[2k+1] << 16 | c[2k] & 0xffff): dot2 with history pair H[k] = (x[i-2k-2], x[i-2k-1])
+    uint32_t C[4], H[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 4; k++) C[k] = ((uint32_t)info.cq[2 * k + 1] << 16) | ((uint32_t)info.cq[2 * k] & 0xFFFFu);
+    // warm-up samples: x[0..o-1]; H after them holds x[o-8..o-1]
+    int32_t wu[8];
+#pragma unroll
+    for (int m = 0; m < 8; m++) wu[m] = info.wu[m];
+#pragma unroll
+    for (int m = 0; m < 8; m++)
+        if (m < o) {
+            H[3] = __builtin_amdgcn_alignbit(H[3], H[2], 16);
+            H[2] = __builtin_amdgcn_alignbit(H[2], H[1], 16);
+            H[1] = __builtin_amdgcn_alignbit(H[1], H[0], 16);
+            H[0] = (H[0] << 16) | ((uint32_t)wu[m] & 0xFFFFu);
+        }
+#pragma unroll
+    for (int m = 0; m < 8; m++)
+        if (m < o && lane == 0) reinterpret_cast<int16_t *>(xout)[m] = (int16_t)wu[m];
+    int avail = 0;
+    uint32_t vr = 0;
+    bool failed = false;
+    for (int i = o; i < bs; i++) {
+        if (i >= avail || (i & 63) == 0 || i == o) {
+            if (i >= avail) {
+                int pg;
+                while ((pg = lds_poll(&vi->progress)) <= i && pg >= 0) __builtin_amdgcn_s_sleep(1);
+                if (pg < 0) {
+                    failed = true;
+                    break;
+                }
+                avail = pg;
+            }
+            vr = (uint32_t)resbuf[(i & ~63) + lane];
+        }
+        const int32_t r = __builtin_amdgcn_readlane((int)vr, i & 63);
+        int32_t pred = dec_dot2(H[3], C[3], 0);
+        pred = dec_dot2(H[2], C[2], pred);
+        pred = dec_dot2(H[1], C[1], pred);
+        pred = dec_dot2(H[0], C[0], pred);
+        const int32_t x = r + (pred >> shift);
+        H[3] = __builtin_amdgcn_alignbit(H[3], H[2], 16);
+        H[2] = __builtin_amdgcn_alignbit(H[2], H[1], 16);
+        H[1] = __builtin_amdgcn_alignbit(H[1], H[0], 16);
+        H[0] = (H[0] << 16) | ((uint32_t)x & 0xFFFFu);
+        if (i & 1) xout[i >> 1] = __builtin_amdgcn_alignbit(H[0], H[0], 16);  // (x[i] << 16) | x[i-1]
+    }
+    if (!failed && (bs & 1)) xout[bs >> 1] = H[0] & 0xFFFFu;
+    while (lds_poll(&vi->finished) == 0) __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+    if (failed || !info.valid) return;
+    const int16_t *x16 = reinterpret_cast<const int16_t *>(xout);
+    for (int i = lane; i < bs; i += 64) out[i] = (int32_t)((uint32_t)(int32_t)x16[i] << w);
+    if (lane == 0) atomicAdd(nvalid, 1);
+}
+
+// One wave per frame: the frame's bytes are staged in LDS by the whole wave (coalesced dword loads), then lane 0
+// decodes from LDS (bit refills are LDS reads instead of dependent global loads).  Frames larger than the stage
+// are decoded straight from global memory.  Multi-channel and wide streams (and FRS_ABLATE 1024).
 __global__ void __launch_bounds__(64) k_decode_frames_wave(const uint8_t *blob, const int64_t *soff, int ns,
                                                           const int64_t *poff, const int64_t *cpos,
                                                           const int64_t *ends, const int64_t *fbase,
@@ -814,10 +1192,16 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         k_chain<<<(nstreams + 63) / 64, 64, 0, st>>>(dsoff, nstreams, cpos, ncand, ends, dfbase, dchain, bad);
         prof_end(ctx, "decode_span", ev);
         prof_begin(ctx, "decode_frames", &ev);
-        k_decode_frames_wave<<<(unsigned)frames, 64, 0, st>>>(blob_dev, dsoff, nstreams,
-                                                                      ctx->dec_poff.as<int64_t>(), cpos, ends, dfbase,
-                                                                      dchain, frames, channels, bps, pcm_dev, blocksize,
-                                                                      nvalid);
+        if (channels == 1 && bps <= 16 && blocksize <= kDecResMax && !(ctx->ablate & 1024))
+            k_decode_frames_pipe<<<(unsigned)frames, 128, 0, st>>>(blob_dev, dsoff, nstreams,
+                                                                   ctx->dec_poff.as<int64_t>(), cpos, ends, dfbase,
+                                                                   dchain, frames, channels, bps, pcm_dev, blocksize,
+                                                                   nvalid);
+        else
+            k_decode_frames_wave<<<(unsigned)frames, 64, 0, st>>>(blob_dev, dsoff, nstreams,
+                                                                  ctx->dec_poff.as<int64_t>(), cpos, ends, dfbase,
+                                                                  dchain, frames, channels, bps, pcm_dev, blocksize,
+                                                                  nvalid);
         prof_end(ctx, "decode_frames", ev);
     }
     int hv[3] = {0, 0, 0};

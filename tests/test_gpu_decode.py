@@ -1,0 +1,45 @@
+"""GPU decode parity: the mono 16-bit fast decoder (k_decode_frames_pipe: scalar-unit Rice decode + v_dot2 LPC
+restore in two waves) and the lane-0 decoder must both return exactly the oracle's decode of the same frames,
+for every subframe type the encoder emits (CONSTANT, VERBATIM, FIXED, LPC, wasted bits) and partial frames."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _bands():
+    rng = np.random.default_rng(77)
+    H, W = 512, 768
+    y, x = np.meshgrid(np.linspace(0, 20, H), np.linspace(0, 20, W), indexing="ij")
+    dem = (1000 + 300 * np.sin(x * 0.8) * np.cos(y * 0.3) + 150 * np.sin(1.2 * x) * np.sin(1.1 * y)
+           + 50 * rng.random((H, W))).astype(np.int16)
+    dem[:64, :128] = dem[0, 0]                                     # constant frames
+    noise = rng.integers(-32768, 32767, size=(256, 256), dtype=np.int16)  # verbatim-heavy
+    steps = (np.arange(320 * 200).reshape(320, 200) // 7 % 50 * 64).astype(np.uint16)  # wasted bits
+    odd = (700 + 40 * np.sin(np.linspace(0, 30, 300 * 333)).reshape(300, 333)
+           + rng.normal(0, 3, (300, 333))).astype(np.int16)  # partial frames, rows crossing frames
+    return [("dem", dem, 256), ("noise", noise, 128), ("steps", steps, 160), ("odd", odd, 128)]
+
+
+@pytest.mark.parametrize("ablate", ["0", "1024"])  # 1024: force the lane-0 decoder
+def test_decode_matches_oracle(gpu_ctx, ablate, monkeypatch):
+    from flac_raster_amd import _native
+    monkeypatch.setenv("FRS_ABLATE", ablate)
+    dctx = _native.Context(0)
+    for name, band, tile in _bands():
+        H, W = band.shape
+        d = gpu_ctx.make_desc(H, W, band.dtype, tile_h=tile, tile_w=tile, sample_rate=44100, bits_per_sample=16)
+        arena, off, mn, mx, bps = gpu_ctx.encode_tiles_host(band, d)
+        counts = []
+        for r0 in range(0, H, tile):
+            for c0 in range(0, W, tile):
+                counts.append(min(tile, H - r0) * min(tile, W - c0))
+        pcm = dctx.decode_frames_host(arena, off, counts, channels=1, bps=16)
+        for t, n in enumerate(counts):
+            frames = arena[off[t]:off[t + 1]].tobytes()
+            ref = O.decode_frames(frames, 1, 16, n)
+            got = pcm[int(np.sum(counts[:t])):int(np.sum(counts[:t + 1]))]
+            assert np.array_equal(got, ref), (name, t)
+    dctx.close()
