@@ -283,9 +283,18 @@ def cpu_baseline(ctx, raster, rows, W, T, off, arena, args):
     nt = len(o_off) - 1
     gpu = arena.download(int(off[nt]), 0)
     parity = bool(np.array_equal(o_off, off[: nt + 1]) and gpu.tobytes() == o_arena.tobytes())
-    return {"value": round(h * W / dt / 1e6, 2), "unit": "Mpixels/s", "cores": args.cpu_threads, "kind": "port",
-            "sample": f"{nt} band-1 tiles ({h}x{W} px) of the benchmark raster, oracle/flac_oracle.c",
-            "seconds": round(dt, 3), "bit_exact_vs_gpu": parity}
+    res = {"value": round(h * W / dt / 1e6, 2), "unit": "Mpixels/s", "cores": args.cpu_threads, "kind": "port",
+           "sample": f"{nt} band-1 tiles ({h}x{W} px) of the benchmark raster, oracle/flac_oracle.c",
+           "seconds": round(dt, 3), "bit_exact_vs_gpu": parity}
+    # the same sample on the box's CPU share (OpenMP over tiles; OMP_NUM_THREADS is the share on the GPU box)
+    mt = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    if args.cpu_threads == 1 and mt > 1:
+        t0 = time.perf_counter()
+        m_arena, m_off, _, _ = O.encode_tiles(band, T, threads=mt)
+        dt_mt = time.perf_counter() - t0
+        res["multi_thread"] = {"value": round(h * W / dt_mt / 1e6, 2), "cores": mt, "seconds": round(dt_mt, 3),
+                               "bit_exact_vs_gpu": bool(m_arena.tobytes() == o_arena.tobytes())}
+    return res
 
 
 if __name__ == "__main__":
