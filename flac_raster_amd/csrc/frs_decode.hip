@@ -724,6 +724,15 @@ struct WaveBits {
         return (k == 0 || k == 32) ? (int32_t)v : ((int32_t)(v << (32 - k)) >> (32 - k));
     }
     __device__ inline uint32_t pos() const { return wi * 32 - (uint32_t)n; }
+    __device__ inline void seek(uint32_t bitpos) {
+        wi = bitpos >> 5;
+        c = (uint64_t)word(wi++) << 32;
+        n = 32;
+        const int off = (int)(bitpos & 31);
+        c <<= off;
+        n -= off;
+        refill();
+    }
     // zeros before the next 1 (the 1 is consumed); false past `lim` bits (corrupt data)
     __device__ inline bool unary(uint32_t &q, uint32_t lim) {
         q = 0;
@@ -776,7 +785,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                                                            const int64_t *ends, const int64_t *fbase,
                                                            const int64_t *frame_cand, int64_t nframes, int channels,
                                                            int stream_bps, int32_t *pcm, int blocksize, int *nvalid) {
-    __shared__ uint32_t stage[kDecStageWords + 4];
+    __shared__ uint32_t stage[kDecStageWords + 8];  // + the window step's look-ahead words
     __shared__ int32_t resbuf[kDecResMax];
     __shared__ uint32_t xout[kDecResMax / 2];  // restored samples as int16 pairs
     __shared__ PipeInfo info;
@@ -790,7 +799,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     const int64_t wb = fpos >> 2, we = (fend_known + 3) >> 2;
     const bool staged = we - wb <= kDecStageWords;
     if (staged)  // big-endian words: the scalar bit reader needs no byte swap
-        for (int64_t k = threadIdx.x; k < we - wb + 4; k += 128)
+        for (int64_t k = threadIdx.x; k < we - wb + 8; k += 128)
             stage[k] = __builtin_bswap32(load_word_guarded(blob, wb + k, send));
     if (threadIdx.x == 0) {
         info.state = 0;
@@ -922,59 +931,96 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
         }
         const int pb = method == 0 ? 4 : 5, esc = (1 << pb) - 1;
         const int psz = bs >> po;
-        uint32_t vr = 0, vu = 0;
-        uint64_t vesc = 0;  // lanes of the current 64-sample group filled by an escaped partition
         int i = o;
         bool bad = false;
-        // residuals of the 64-sample group ending at sample `last` into resbuf, then publish them
-        auto flush = [&](int last) {
-            const uint32_t zz = (vu >> 1) ^ (uint32_t)(-(int32_t)(vu & 1));
-            resbuf[(last & ~63) + lane] = (int32_t)(((vesc >> lane) & 1) ? vr : zz);
-            vesc = 0;
-            if (lane == 0 && last + 1 < bs) lds_publish(&vi->progress, last + 1);
+        uint32_t P = br.pos();  // stage bit of the next field
+        auto publish = [&]() {
+            if (lane == 0) lds_publish(&vi->progress, i);
         };
         for (int p = 0; p < (1 << po) && !bad; p++) {
+            br.seek(P);
             const int kp = (int)br.bits(pb);
-            const int pe = (p + 1) * psz;
-            if (kp == esc) {
+            int left = psz - (p == 0 ? o : 0);
+            if (kp == esc) {  // escaped partition: fixed-width residuals (rare; lane 0 stores them)
                 const int nb = (int)br.bits(5);
-                for (; i < pe; i++) {
+                for (int j = 0; j < left; j++, i++) {
                     const int32_t r = nb ? br.sbits(nb) : 0;
-                    vr = lane == (i & 63) ? (uint32_t)r : vr;
-                    vesc |= 1ull << (i & 63);
-                    if ((i & 63) == 63) flush(i);
+                    if (lane == 0) resbuf[i] = r;
                 }
-            } else {
-                const int k1 = kp + 1;
-                const uint32_t kmask = (1u << kp) - 1u;
-                // one Rice code from the cache: zeros z, stop bit, kp low bits; false on corrupt data
-                auto code = [&](uint32_t &u) -> bool {
-                    const int z = __builtin_clzll(br.c | 1);
+                P = br.pos();
+                publish();
+                continue;
+            }
+            P = br.pos();
+            const int k1 = kp + 1;
+            // Window step: lane j decodes the Rice codes that would start at bits P + j and P + 64 + j (from
+            // big-endian stage words); the scalar unit then walks the chain of actual code starts through those
+            // 128 candidates (one v_readlane per code) and the lanes on the chain store their residuals in order.
+            while (left > 0) {
+                if (P > lim) {
+                    bad = true;
+                    break;
+                }
+                const uint32_t b = P + (uint32_t)lane, wi = b >> 5, sh = b & 31u;
+                const uint32_t w0 = stage[wi], w1 = stage[wi + 1], w2 = stage[wi + 2], w3 = stage[wi + 3],
+                               w4 = stage[wi + 4];
+                auto cand = [&](uint32_t x0, uint32_t x1, uint32_t x2, int base, uint32_t &u) -> int {
+                    const uint32_t hi = sh ? __builtin_amdgcn_alignbit(x0, x1, 32u - sh) : x0;
+                    const uint32_t lo = sh ? __builtin_amdgcn_alignbit(x1, x2, 32u - sh) : x1;
+                    const uint64_t win = ((uint64_t)hi << 32) | lo;
+                    const int z = win ? __builtin_clzll(win) : 64;
                     const int tot = z + k1;
-                    if (tot < br.n) {  // the whole code is in the cache
-                        u = ((uint32_t)z << kp) | ((uint32_t)(br.c >> (64 - tot)) & kmask);
-                        br.c <<= tot;
-                        br.n -= tot;
-                        if (br.n <= 32) br.refill1();
-                        return true;
-                    }
-                    uint32_t q;
-                    if (!br.unary(q, lim)) return false;
-                    u = (q << kp) | br.bits(kp);
-                    return true;
+                    const uint32_t low = (kp && tot <= 64) ? (uint32_t)((win << (z + 1)) >> (64 - kp)) : 0u;
+                    u = ((uint32_t)z << kp) | low;
+                    return tot <= 64 ? base + lane + tot : 255;  // next code start (relative to P) or "long"
                 };
-                for (; i < pe; i++) {
-                    uint32_t u;
-                    if (!code(u)) {
+                uint32_t ua, ub;
+                const int na = cand(w0, w1, w2, 0, ua), nb2 = cand(w2, w3, w4, 64, ub);
+                const int nxt = na | (nb2 << 16);  // candidates at P + lane (low half) and P + 64 + lane (high)
+                uint64_t ma = 0, mb = 0;
+                int cur = 0, cnt = 0;
+                bool lng = false;
+                while (cnt < left && cur < 128) {
+                    const int nx = (__builtin_amdgcn_readlane(nxt, cur & 63) >> ((cur >> 6) << 4)) & 0xFFFF;
+                    if (nx == 255) {  // the code at cur runs past its 64-bit window
+                        lng = true;
+                        break;
+                    }
+                    if (cur < 64) ma |= 1ull << cur;
+                    else mb |= 1ull << (cur - 64);
+                    cnt++;
+                    cur = nx;
+                }
+                const uint64_t below = (1ull << lane) - 1ull;
+                if ((ma >> lane) & 1ull) {
+                    const int idx = __builtin_popcountll(ma & below);
+                    resbuf[i + idx] = (int32_t)((ua >> 1) ^ (uint32_t)(-(int32_t)(ua & 1)));
+                }
+                if ((mb >> lane) & 1ull) {
+                    const int idx = __builtin_popcountll(ma) + __builtin_popcountll(mb & below);
+                    resbuf[i + idx] = (int32_t)((ub >> 1) ^ (uint32_t)(-(int32_t)(ub & 1)));
+                }
+                const int i0 = i;
+                i += cnt;
+                left -= cnt;
+                P += (uint32_t)cur;
+                if (lng) {  // a long unary run: one code through the scalar reader
+                    br.seek(P);
+                    uint32_t q;
+                    if (!br.unary(q, lim)) {
                         bad = true;
                         break;
                     }
-                    vu = lane == (i & 63) ? u : vu;  // zig-zag codes; decoded 64 at a time on the vector unit
-                    if ((i & 63) == 63) flush(i);
+                    const uint32_t uu = (q << kp) | br.bits(kp);
+                    if (lane == 0) resbuf[i] = (int32_t)((uu >> 1) ^ (uint32_t)(-(int32_t)(uu & 1)));
+                    i++;
+                    left--;
+                    P = br.pos();
                 }
+                if ((i0 >> 6) != (i >> 6) || left == 0) publish();  // per 64-sample group (and partition end)
             }
         }
-        if (!bad && (bs & 63)) flush(bs - 1);  // the last partial group
+        br.seek(P);  // the frame's end check reads br.pos()
         const int ok = !bad && end_ok();
         if (lane == 0) {
             info.valid = ok;
