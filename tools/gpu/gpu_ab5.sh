@@ -1,0 +1,12 @@
+#!/bin/bash
+# Alternating A/B of variants/libhead.so and variants/libnew.so (bench encode step incl. host overhead).
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+rm -rf gpurun_out/ab5; mkdir -p gpurun_out/ab5
+for r in 1 2 3; do
+  for n in head new; do
+    FRS_LIB_PATH=$PWD/variants/lib$n.so timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu --queries 0 >> gpurun_out/ab5/$n.log 2>&1 || exit 1
+  done
+done
+echo done
