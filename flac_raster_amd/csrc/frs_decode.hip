@@ -161,7 +161,7 @@ __device__ inline uint32_t dec_gfmul(uint32_t a, uint32_t b) {
 
 __global__ void __launch_bounds__(64) k_span_crc_wave(const uint8_t *blob, const int64_t *soff, int ns,
                                                      const int64_t *cpos, const int *ncand, int64_t max_frame,
-                                                     int64_t *ends) {
+                                                     int64_t *ends, int32_t *nexti) {
     __shared__ uint32_t stage[kSpanWords + 1];
     __shared__ uint16_t t4[4][256];
     __shared__ uint16_t xlo[256];
@@ -186,6 +186,7 @@ __global__ void __launch_bounds__(64) k_span_crc_wave(const uint8_t *blob, const
     const int64_t send = soff[s + 1];
     const int64_t lim = min(send, p + max_frame);
     int64_t result = -1;
+    int32_t rnext = -1;  // candidate index at the span's end, -2 = the stream's end
     for (int j = i + 1;; j++) {
         int64_t e = (j < nc) ? cpos[j] : send;
         if (e > send) e = send;
@@ -204,7 +205,9 @@ __global__ void __launch_bounds__(64) k_span_crc_wave(const uint8_t *blob, const
                     const uint32_t a = b + off0;
                     return (stage[a >> 2] >> (8 * (a & 3))) & 0xFFu;
                 };
-                const uint32_t ch = ((nb + 63) / 64 + 3) & ~3u;  // bytes per lane, multiple of 4
+                // bytes per lane: a multiple of 4 whose word count is odd (lane bases in distinct LDS banks)
+                uint32_t ch = ((nb + 63) / 64 + 3) & ~3u;
+                if (!((ch >> 2) & 1u)) ch += 4;
                 const uint32_t b0 = min(nb, (uint32_t)lane * ch), b1 = min(nb, b0 + ch);
                 uint32_t c = 0, b = b0;
                 for (; b + 4 <= b1; b += 4) {
@@ -224,6 +227,7 @@ __global__ void __launch_bounds__(64) k_span_crc_wave(const uint8_t *blob, const
                 __builtin_amdgcn_wave_barrier();
                 if (crc == got) {
                     result = e;
+                    rnext = (j < nc && cpos[j] < send) ? j : -2;
                     break;
                 }
             } else {  // rare: a span longer than the stage
@@ -232,13 +236,17 @@ __global__ void __launch_bounds__(64) k_span_crc_wave(const uint8_t *blob, const
                 const uint32_t got = ((uint32_t)blob[e - 2] << 8) | blob[e - 1];
                 if (c == got) {
                     result = e;
+                    rnext = (j < nc && cpos[j] < send) ? j : -2;
                     break;
                 }
             }
         }
         if (e >= send) break;
     }
-    if (lane == 0) ends[i] = result;
+    if (lane == 0) {
+        ends[i] = result;
+        nexti[i] = rnext;
+    }
 }
 
 __device__ inline int find_pos(const int64_t *cpos, int n, int64_t p) {
@@ -270,6 +278,60 @@ __global__ void k_chain(const int64_t *soff, int ns, const int64_t *cpos, const 
         cur = ends[idx];
     }
     if (cur != soff[s + 1]) atomicAdd(bad, 1);
+}
+
+// k_chain with the span links in LDS: one work-group per stream loads the stream's candidate -> next-candidate
+// links (k_span_crc_wave's nexti) and lane 0 walks them, one LDS read per frame instead of a binary search of
+// global memory per frame.  Streams with more candidates than the LDS table take the global walk.
+constexpr int kChainLds = 4096;
+__device__ inline int lower_bound_pos(const int64_t *cpos, int n, int64_t p) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (cpos[mid] < p) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+__global__ void __launch_bounds__(64) k_chain_lds(const int64_t *soff, int ns, const int64_t *cpos, const int *ncand,
+                                                 const int32_t *nexti, const int64_t *fbase, int64_t *frame_cand,
+                                                 int *bad) {
+    __shared__ int32_t nx[kChainLds];
+    __shared__ int32_t rng[2];
+    const int s = blockIdx.x;
+    if (s >= ns) return;
+    const int lane = threadIdx.x;
+    const int nc = *ncand;
+    if (lane == 0) {
+        rng[0] = ns == 1 ? 0 : lower_bound_pos(cpos, nc, soff[s]);
+        rng[1] = ns == 1 ? nc : lower_bound_pos(cpos, nc, soff[s + 1]);
+    }
+    __syncthreads();
+    const int c0 = rng[0], c1 = rng[1];
+    const bool in_lds = c1 - c0 <= kChainLds;
+    if (in_lds)
+        for (int k = lane; k < c1 - c0; k += 64) nx[k] = nexti[c0 + k];
+    __syncthreads();
+    if (lane != 0) return;
+    const int64_t nf = fbase[s + 1] - fbase[s];
+    if (c0 >= c1 || cpos[c0] != soff[s]) {
+        atomicAdd(bad, 1);
+        return;
+    }
+    int idx = c0;
+    for (int64_t k = 0; k < nf; k++) {
+        frame_cand[fbase[s] + k] = idx;
+        const int n = in_lds ? nx[idx - c0] : nexti[idx];
+        if (k + 1 < nf) {
+            if (n < 0) {
+                atomicAdd(bad, 1);
+                return;
+            }
+            idx = n;
+        } else if (n != -2) {
+            atomicAdd(bad, 1);
+        }
+    }
 }
 
 constexpr int kDecResMax = 4096;  // residual buffer (LDS) of the fast subframe path
@@ -1231,11 +1293,15 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     prof_end(ctx, "decode", ev);
     if (hc > 0) {
         prof_begin(ctx, "decode_span", &ev);
-        if (max_frame < (int64_t)4096 * 256)  // x^(8m) table range
-            k_span_crc_wave<<<hc, 64, 0, st>>>(blob_dev, dsoff, nstreams, cpos, ncand, max_frame, ends);
-        else
+        if (max_frame < (int64_t)4096 * 256) {  // x^(8m) table range
+            FRS_HIP(ctx->dec_next.ensure(sizeof(int32_t) * (size_t)hc + 64));
+            int32_t *nexti = ctx->dec_next.as<int32_t>();
+            k_span_crc_wave<<<hc, 64, 0, st>>>(blob_dev, dsoff, nstreams, cpos, ncand, max_frame, ends, nexti);
+            k_chain_lds<<<nstreams, 64, 0, st>>>(dsoff, nstreams, cpos, ncand, nexti, dfbase, dchain, bad);
+        } else {
             k_span_crc<<<(hc + 63) / 64, 64, 0, st>>>(blob_dev, dsoff, nstreams, flags, cpos, ncand, max_frame, ends);
-        k_chain<<<(nstreams + 63) / 64, 64, 0, st>>>(dsoff, nstreams, cpos, ncand, ends, dfbase, dchain, bad);
+            k_chain<<<(nstreams + 63) / 64, 64, 0, st>>>(dsoff, nstreams, cpos, ncand, ends, dfbase, dchain, bad);
+        }
         prof_end(ctx, "decode_span", ev);
         prof_begin(ctx, "decode_frames", &ev);
         if (channels == 1 && bps <= 16 && blocksize <= kDecResMax && !(ctx->ablate & 1024))

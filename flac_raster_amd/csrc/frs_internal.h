@@ -52,7 +52,7 @@ struct frs_ctx {
     // host staging (pinned)
     DevBuf raster_stage, arena_stage;  // device copies for the host-pointer entry points
     // decode scratch
-    DevBuf dec_cand, dec_count, dec_blob, dec_pcm, dec_soff, dec_poff;
+    DevBuf dec_cand, dec_count, dec_blob, dec_pcm, dec_soff, dec_poff, dec_next;
     // profiling
     bool prof = false;
     std::map<std::string, ProfEntry> prof_tab;
