@@ -33,7 +33,8 @@ sys.path.insert(0, str(ROOT))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E peak 8.0 TB/s
 METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"] if (ROOT / "BASELINE.json").exists() else \
     "Mpixels/sec encode (create-streaming) + bbox-extract ms, 1/2/4/8 GPU; bit-exact vs ref"
-KERNEL_SYMBOL = {"encode": "frs::k_encode_v3<3>", "analyze": "frs::k_analyze_v3<3, false>", "stats": "frs::k_tile_stats_vec<3>"}
+KERNEL_SYMBOL = {"encode": "frs::k_encode_v3<3>", "analyze": "frs::k_analyze_v3<3, false, true>",
+                 "stats": "frs::k_tile_stats_vec<3>"}
 
 
 def parse():
@@ -150,9 +151,11 @@ def main():
     kernels = {k: v for k, v in kernels.items() if v > 0}
     comp_bytes = int(off[-1])
     px_rank = rows * W
-    # algorithmic bytes per launch: stats reads 2 B/px; analyze reads 2 B/px; encode reads
-    # 2 B/px and writes the frames; compact reads + writes the frames.
-    algo = {"stats": 2 * px_rank, "analyze": 2 * px_rank, "encode": 2 * px_rank + comp_bytes,
+    # algorithmic bytes per launch: stats reads 2 B/px; analyze reads 2 B/px (4 B/px when the tile
+    # stats are fused into it: min/max pass + autocorrelation pass); encode reads 2 B/px and writes the frames;
+    # compact reads + writes the frames.
+    fused = "stats" not in kernels
+    algo = {"stats": 2 * px_rank, "analyze": (4 if fused else 2) * px_rank, "encode": 2 * px_rank + comp_bytes,
             "compact": 2 * comp_bytes}
     dom = max((k for k in kernels if kernels[k] > 0), key=lambda k: kernels[k])
     dom_ms = kernels[dom]

@@ -17,6 +17,8 @@
 
 #include <type_traits>
 
+#include <cstring>
+
 #include "frs_internal.h"
 
 namespace frs {
@@ -227,10 +229,9 @@ __global__ void __launch_bounds__(256) k_tile_stats_vec(const typename Elem<DT>:
     }
 }
 
-template <int DT> __global__ void k_tile_finalize(TileNorm *norms, int ntiles, int norm_mode, int scale_bits) {
-    int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= ntiles) return;
-    TileNorm n = norms[t];
+// normalisation parameters of a tile from its min/max (converter.py:88-110): data_min/data_max, the range in
+// the dtype, and the fast-path mode (LUT / zeros / fast division / exact division)
+template <int DT> __device__ inline void tile_norm_finalize(TileNorm &n, int norm_mode, int scale_bits) {
     using T = typename Elem<DT>::T;
     n.mode = kNormSlow;
     n.rinv = 0.0;
@@ -253,6 +254,13 @@ template <int DT> __global__ void k_tile_finalize(TileNorm *norms, int ntiles, i
             n.rinv = 1.0 / n.den;
         }
     }
+}
+
+template <int DT> __global__ void k_tile_finalize(TileNorm *norms, int ntiles, int norm_mode, int scale_bits) {
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntiles) return;
+    TileNorm n = norms[t];
+    tile_norm_finalize<DT>(n, norm_mode, scale_bits);
     norms[t] = n;
 }
 
@@ -1253,18 +1261,21 @@ __device__ inline void norm_chunk(const Chunk64<DT> &ch, const TileNorm &tn, con
     }
 }
 
+// LUT entry d = x - min of a kNormLut tile (exact double path: numpy 2.0*(x-min)/(max-min)-1.0, *32767)
+template <int DT> __device__ inline int16_t lut_entry(const TileNorm &tn, int64_t d) {
+    using T = typename Elem<DT>::T;
+    const T dd = (T)d;
+    const double v = ((2.0 * (double)dd) / tn.den - 1.0) * 32767.0;
+    return (int16_t)cast_f64_i32_x86(v);
+}
+
 template <int DT>
 __global__ void __launch_bounds__(256) k_build_lut(const TileNorm *norms, int16_t *luts) {
     const int t = blockIdx.x;
     const TileNorm tn = norms[t];
     if (tn.mode != kNormLut) return;
-    using T = typename Elem<DT>::T;
     const int64_t R = tn.imax - tn.imin;
-    for (int64_t d = threadIdx.x; d <= R; d += blockDim.x) {
-        const T dd = (T)d;
-        const double v = ((2.0 * (double)dd) / tn.den - 1.0) * 32767.0;  // numpy: 2.0*(x-min)/(max-min)-1.0, *32767
-        luts[(int64_t)t * kLutCap + d] = (int16_t)cast_f64_i32_x86(v);
-    }
+    for (int64_t d = threadIdx.x; d <= R; d += blockDim.x) luts[(int64_t)t * kLutCap + d] = lut_entry<DT>(tn, d);
 }
 
 // n / d for n < 2^32 via a double reciprocal (inv = 1.0 / d): the estimate is off by at most one, fixed up
@@ -1626,35 +1637,102 @@ __device__ inline void ana_autoc(const typename Elem<DT>::T *base, const EncodeP
     }
 }
 
+// min/max of a whole tile by one wave (16-bit samples, 16-B aligned rows): 16-B loads, kStatsLoads in flight per lane,
+// packed 16-bit min/max; the tile's vectors are dealt out lane-major (vector i to lane i % 64), lanes past the
+// end re-read vector 0.  Returns the keys (elem_key order) in lo/hi, wave-uniform.
+constexpr int kStatsLoads = 16;
+template <int DT>
+__device__ inline void wave_tile_minmax(const typename Elem<DT>::T *base, int64_t row_stride, const TileGeom &g,
+                                        int lane, int64_t &lo, int64_t &hi) {
+    using T = typename Elem<DT>::T;
+    static_assert(sizeof(T) == 2, "16-bit samples");
+    using V = std::conditional_t<std::is_signed_v<T>, v2i16, v2u16>;
+    using E16 = std::conditional_t<std::is_signed_v<T>, short, unsigned short>;
+    V vmin = (V)(std::is_signed_v<T> ? (E16)32767 : (E16)65535), vmax = (V)(std::is_signed_v<T> ? (E16)-32768 : (E16)0);
+    const int nvec = g.w / 8;  // 16-B vectors per row
+    const int total = g.h * nvec;
+    const int dq = 64 / nvec, dr = 64 - dq * nvec;  // advance of a lane's (row, vector) per 64 vectors
+    int row = lane / nvec, v = lane - row * nvec;
+    const char *b = reinterpret_cast<const char *>(base);
+    const int64_t rs = row_stride * 2;
+    const int iters = (total + 64 * kStatsLoads - 1) / (64 * kStatsLoads);
+    for (int it = 0; it < iters; it++) {
+        uint4 q[kStatsLoads];
+#pragma unroll
+        for (int u = 0; u < kStatsLoads; u++) {
+            const bool ok = row < g.h;
+            q[u] = *reinterpret_cast<const uint4 *>(b + (ok ? row * rs + v * 16 : 0));
+            v += dr;
+            row += dq;
+            if (v >= nvec) {
+                v -= nvec;
+                row++;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kStatsLoads; u++) {
+            const uint32_t w4[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const V x = __builtin_bit_cast(V, w4[k]);
+                vmin = __builtin_elementwise_min(vmin, x);
+                vmax = __builtin_elementwise_max(vmax, x);
+            }
+        }
+    }
+    int32_t l = min((int32_t)vmin.x, (int32_t)vmin.y), h = max((int32_t)vmax.x, (int32_t)vmax.y);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        l = min(l, __shfl_xor(l, o));
+        h = max(h, __shfl_xor(h, o));
+    }
+    lo = l;
+    hi = h;
+}
+
 // Two launches of one kernel body keep the common case lean: SLOW = false takes the tiles normalised by LUT (or
 // zeros) -- ~120 VGPRs, 4 waves/SIMD; SLOW = true takes the fast-division / exact-division tiles, whose fp64
 // normalisation needs more registers.  A wave of the other class returns at once.
-template <int DT, bool SLOW>
+// STATS = true (SLOW = false, 16-bit samples, every tile one wave): the wave first computes its tile's min/max
+// and normalisation parameters (k_tile_stats_vec + k_tile_finalize) and builds the tile's LUT (k_build_lut) in
+// LDS and in global memory for the encoder -- the tile is read twice, but the separate stats pass and its
+// launches are gone.  A slow-class tile only gets its parameters written here; the SLOW launch analyses it.
+template <int DT, bool SLOW, bool STATS = false>
 __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *raster, EncodeParams P,
-                                                   const TileGeom *tiles, const TileNorm *norms,
-                                                   const int16_t *luts, const float *__restrict__ window,
+                                                   const TileGeom *tiles, TileNorm *norms,
+                                                   int16_t *luts, const float *__restrict__ window,
                                                    SubAnalysis *out, const int2 *__restrict__ wtab, int nwaves) {
+    static_assert(!(SLOW && STATS), "stats are fused into the lean launch only");
     __shared__ int16_t slut[SLOW ? 1 : 4][SLOW ? 1 : kLutCap];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wv = blockIdx.x * 4 + wave;
     if (wv >= nwaves) return;
     const int2 wt = wtab[wv];  // (tile, first frame of the tile handled by this wave)
     const int t = wt.x;
-    const TileNorm tn = norms[t];
+    const TileGeom g = tiles[t];
+    const typename Elem<DT>::T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
+    int16_t *glut = luts + (int64_t)t * kLutCap;
+    TileNorm tn;
+    if constexpr (STATS) {
+        if constexpr (sizeof(typename Elem<DT>::T) == 2 && !Elem<DT>::is_float) {
+            wave_tile_minmax<DT>(base, P.row_stride, g, lane, tn.imin, tn.imax);
+            tile_norm_finalize<DT>(tn, P.norm_mode, P.scale_bits);
+            if (lane == 0) norms[t] = tn;
+        }
+    } else {
+        tn = norms[t];
+    }
     const int mode = tn.mode;  // wave-uniform: one tile per wave
     const bool lean = mode == kNormLut || mode == kNormZero;
     if (lean == SLOW) return;
-    const TileGeom g = tiles[t];
     const bool live = wt.y + lane < g.nframes;
     const int64_t fk = live ? wt.y + lane : g.nframes - 1;  // dead lanes re-read the tile's last frame
     const int64_t f = g.frame_base + fk;
     const int64_t s0 = fk * P.blocksize;
     const int64_t tile_px = (int64_t)g.h * g.w;
     const int n = live ? (int)min((int64_t)P.blocksize, tile_px - s0) : 0;
-    const typename Elem<DT>::T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
     constexpr int kChunk = SLOW ? 16 : 64;  // samples per lane load (SLOW: fewer VGPRs beside the fp64 division)
     const bool vec = P.vec_ok && (g.w % kChunk) == 0;
-    const int16_t *glut = luts + (int64_t)t * kLutCap;
     double acc[kMaxLpc + 1];
 #pragma unroll
     for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
@@ -1663,7 +1741,15 @@ __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *
         int16_t *wl = slut[wave];
         if (mode == kNormLut) {
             const int64_t R = tn.imax - tn.imin;
-            for (int64_t d = lane; d <= R; d += 64) wl[d] = glut[d];
+            if constexpr (STATS) {
+                for (int64_t d = lane; d <= R; d += 64) {
+                    const int16_t e = lut_entry<DT>(tn, d);
+                    wl[d] = e;
+                    glut[d] = e;
+                }
+            } else {
+                for (int64_t d = lane; d <= R; d += 64) wl[d] = glut[d];
+            }
             __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's LUT stores have landed (each wave reads only its own)
             __builtin_amdgcn_wave_barrier();
             ana_autoc<DT, kAnaKindLds, kChunk>(base, P, g, s0, tn, wl, glut, window, vec, acc, or_acc);
@@ -2621,11 +2707,20 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
     if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
 }
 
-__global__ void k_fast_finish(const int64_t *frame_off, const uint64_t *status, const TileGeom *tiles, int ntiles,
-                              int64_t nframes, int64_t *tile_off) {
+// results of the fast path packed for one D2H copy: tile offsets [ntiles + 1], (dmin, dmax) per tile, error flags
+__global__ void k_fast_finish(const int64_t *frame_off, const uint64_t *status, const TileGeom *tiles,
+                              const TileNorm *norms, const int *err_flag, int ntiles, int64_t nframes, int64_t *pack) {
     int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < ntiles) tile_off[t] = frame_off[tiles[t].frame_base];
-    if (t == ntiles) tile_off[t] = (int64_t)(status[nframes - 1] & kValMask);
+    double *mm = reinterpret_cast<double *>(pack + ntiles + 1);
+    if (t < ntiles) {
+        pack[t] = frame_off[tiles[t].frame_base];
+        mm[2 * t] = norms[t].dmin;
+        mm[2 * t + 1] = norms[t].dmax;
+    }
+    if (t == ntiles) {
+        pack[t] = (int64_t)(status[nframes - 1] & kValMask);
+        pack[3 * (int64_t)ntiles + 1] = *err_flag;
+    }
 }
 
 // ------------------------------------------------------------------------------------- host side
@@ -2791,6 +2886,12 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     FRS_HIP(ctx->frame_bytes.ensure(sizeof(int64_t) * (nframes + 1) + 64));
     FRS_HIP(ctx->frame_off.ensure(sizeof(int64_t) * (nframes + 1)));
     FRS_HIP(ctx->tile_sizes.ensure(sizeof(int64_t) * (ntiles + 1) + 64));
+    // pinned staging: tiles | wave table | packed results (the previous call has synchronised, so it is free)
+    const size_t pin_tiles = 0, pin_wt = (sizeof(TileGeom) * ntiles + 255) & ~(size_t)255;
+    const size_t wt_cap = (size_t)(nframes / 64 + ntiles + 1);
+    const size_t pin_res = (pin_wt + sizeof(int2) * wt_cap + 255) & ~(size_t)255;
+    const size_t res_bytes = sizeof(int64_t) * (3 * (size_t)ntiles + 2);
+    FRS_HIP(ctx->pin.ensure(pin_res + res_bytes));
     if (ctx->window_bs != d->blocksize) {
         std::vector<float> win(d->blocksize, 1.0f);
         // FLAC__window_tukey(0.5) computed in double with the host libm cos, stored as float (window.c)
@@ -2807,7 +2908,9 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         FRS_HIP(hipStreamSynchronize(st));
         ctx->window_bs = d->blocksize;
     }
-    FRS_HIP(hipMemcpyAsync(ctx->tiles.ptr, tiles.data(), sizeof(TileGeom) * ntiles, hipMemcpyHostToDevice, st));
+    memcpy(ctx->pin.at<TileGeom>(pin_tiles), tiles.data(), sizeof(TileGeom) * ntiles);
+    FRS_HIP(hipMemcpyAsync(ctx->tiles.ptr, ctx->pin.at<TileGeom>(pin_tiles), sizeof(TileGeom) * ntiles,
+                           hipMemcpyHostToDevice, st));
     int *err_flag = reinterpret_cast<int *>(ctx->frame_bytes.as<int64_t>() + nframes + 1);
     FRS_HIP(hipMemsetAsync(err_flag, 0, sizeof(int), st));
 
@@ -2817,46 +2920,55 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     SubAnalysis *dana = ctx->analysis.as<SubAnalysis>();
 
     hipEvent_t ev;
-    // 1. tile stats
-    prof_begin(ctx, "stats", &ev);
-    k_stats_init<<<(ntiles + 255) / 256, 256, 0, st>>>(dnorms, ntiles);
+    // fast path: mono 16-bit streams whose frames are all full 4096-sample blocks
+    bool all_full = true, one_wave_tiles = true;
+    for (const TileGeom &tg : tiles) {
+        all_full = all_full && (((int64_t)tg.h * tg.w) % d->blocksize == 0);
+        one_wave_tiles = one_wave_tiles && tg.nframes <= 64;
+    }
+    const bool fast = !ctx->force_generic && P.bps == 16 && P.nch == 1 && P.norm_mode == 0 && d->blocksize == 4096 &&
+                      all_full && !Elem<DT>::is_float;
     bool stats_vec = false;
     if constexpr (sizeof(T) <= 2 && !Elem<DT>::is_float) {
         const int64_t es = (int64_t)sizeof(T);
         const uintptr_t b = reinterpret_cast<uintptr_t>(raster_dev) + (uintptr_t)(d->band0 * d->band_stride * es);
         stats_vec = (b % 16 == 0) && ((d->row_stride * es) % 16 == 0) && ((d->band_stride * es) % 16 == 0) &&
                     ((d->tile_w * es) % 16 == 0) && ((d->width * es) % 16 == 0);
+    }
+    // Tile stats on the fast path (16-bit samples, 16-B aligned rows, one wave per tile): fused into the analysis
+    // launch (k_analyze_v3<DT, false, true>: min/max, parameters and LUT per wave).  Otherwise (and with
+    // FRS_ABLATE 4096) the stats kernels run before the analysis.
+    const bool fuse_stats = fast && stats_vec && sizeof(T) == 2 && one_wave_tiles && !(P.ablate & (4096 | 256));
+    // 1. tile stats
+    if (!fuse_stats) {
+        prof_begin(ctx, "stats", &ev);
+        k_stats_init<<<(ntiles + 255) / 256, 256, 0, st>>>(dnorms, ntiles);
         if (stats_vec) {
+            const int64_t es = (int64_t)sizeof(T);
             const int64_t px = (int64_t)d->tile_h * d->tile_w * d->nbands;
             // ~256 KB per work-group, at least ~2048 work-groups overall
             int splits = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)d->tile_h * d->nbands, px * es / (256 << 10)));
             while ((int64_t)splits * ntiles < 2048 && splits < d->tile_h * d->nbands) splits++;
             dim3 grid(splits, ntiles);
-            k_tile_stats_vec<DT><<<grid, 256, 0, st>>>(reinterpret_cast<const T *>(raster_dev), P, ctx->tiles.as<TileGeom>(),
-                                                       ctx->norms.as<TileNorm>(), splits);
+            if constexpr (sizeof(T) <= 2 && !Elem<DT>::is_float)
+                k_tile_stats_vec<DT><<<grid, 256, 0, st>>>(raster, P, dtiles, dnorms, splits);
+        } else {
+            int64_t rows = (int64_t)d->tile_h * d->nbands;
+            int splits = (int)std::min<int64_t>(rows, std::max<int64_t>(1, (int64_t)4096 / ntiles));
+            if (splits < 1) splits = 1;
+            dim3 grid(splits, ntiles);
+            k_tile_stats<DT><<<grid, 256, 0, st>>>(raster, P, dtiles, dnorms, splits);
         }
+        k_tile_finalize<DT><<<(ntiles + 255) / 256, 256, 0, st>>>(dnorms, ntiles, P.norm_mode, P.scale_bits);
+        prof_end(ctx, "stats", ev);
     }
-    if (!stats_vec) {
-        int64_t rows = (int64_t)d->tile_h * d->nbands;
-        int splits = (int)std::min<int64_t>(rows, std::max<int64_t>(1, (int64_t)4096 / ntiles));
-        if (splits < 1) splits = 1;
-        dim3 grid(splits, ntiles);
-        k_tile_stats<DT><<<grid, 256, 0, st>>>(raster, P, dtiles, dnorms, splits);
-    }
-    k_tile_finalize<DT><<<(ntiles + 255) / 256, 256, 0, st>>>(dnorms, ntiles, P.norm_mode, P.scale_bits);
-    prof_end(ctx, "stats", ev);
-    // fast path: mono 16-bit streams whose frames are all full 4096-sample blocks
-    bool all_full = true;
-    for (const TileGeom &tg : tiles) all_full = all_full && (((int64_t)tg.h * tg.w) % d->blocksize == 0);
-    const bool fast = !ctx->force_generic && P.bps == 16 && P.nch == 1 && P.norm_mode == 0 && d->blocksize == 4096 &&
-                      all_full && !Elem<DT>::is_float;
     if constexpr (!Elem<DT>::is_float) if (fast) {
         const int es = (int)sizeof(T);
         P.vec_ok = ((d->row_stride * es) % 16 == 0) && (d->tile_w % 64 == 0) &&
                    ((reinterpret_cast<uintptr_t>(raster_dev) + (size_t)d->band0 * d->band_stride * es) % 16 == 0);
         FRS_HIP(ctx->luts.ensure(sizeof(int16_t) * (size_t)kLutCap * ntiles));
         FRS_HIP(ctx->status.ensure(sizeof(uint64_t) * (nframes + 1) + 64));
-        k_build_lut<DT><<<ntiles, 256, 0, st>>>(dnorms, ctx->luts.as<int16_t>());
+        if (!fuse_stats) k_build_lut<DT><<<ntiles, 256, 0, st>>>(dnorms, ctx->luts.as<int16_t>());
         FRS_HIP(ctx->frame_tile.ensure(sizeof(int32_t) * nframes));
         k_frame_tile<<<ntiles, 64, 0, st>>>(dtiles, ntiles, ctx->frame_tile.as<int32_t>());
         prof_begin(ctx, "analyze", &ev);
@@ -2866,17 +2978,23 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                 ctx->frame_tile.as<int32_t>());
         } else {
             // wave table: (tile, first frame) per wave, up to 64 frames of one tile each
-            std::vector<int2> wt;
-            wt.reserve((size_t)(nframes / 64 + ntiles));
+            int2 *wt = ctx->pin.at<int2>(pin_wt);
+            int nwaves = 0;
             for (int ti = 0; ti < ntiles; ti++)
-                for (int k0 = 0; k0 < tiles[ti].nframes; k0 += 64) wt.push_back(make_int2(ti, k0));
-            const int nwaves = (int)wt.size();
-            FRS_HIP(ctx->wave_tab.ensure(sizeof(int2) * wt.size()));
-            FRS_HIP(hipMemcpyAsync(ctx->wave_tab.ptr, wt.data(), sizeof(int2) * wt.size(), hipMemcpyHostToDevice, st));
+                for (int k0 = 0; k0 < tiles[ti].nframes; k0 += 64) wt[nwaves++] = make_int2(ti, k0);
+            FRS_HIP(ctx->wave_tab.ensure(sizeof(int2) * nwaves));
+            FRS_HIP(hipMemcpyAsync(ctx->wave_tab.ptr, wt, sizeof(int2) * nwaves, hipMemcpyHostToDevice, st));
             const unsigned wgrid = (unsigned)((nwaves + 3) / 4);
-            k_analyze_v3<DT, false><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
-                                                           ctx->window.as<float>(), dana, ctx->wave_tab.as<int2>(),
-                                                           nwaves);
+            if (fuse_stats) {
+                if constexpr (sizeof(T) == 2)
+                    k_analyze_v3<DT, false, true><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
+                                                                         ctx->window.as<float>(), dana,
+                                                                         ctx->wave_tab.as<int2>(), nwaves);
+            } else {
+                k_analyze_v3<DT, false><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
+                                                               ctx->window.as<float>(), dana, ctx->wave_tab.as<int2>(),
+                                                               nwaves);
+            }
             k_analyze_v3<DT, true><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
                                                           ctx->window.as<float>(), dana, ctx->wave_tab.as<int2>(),
                                                           nwaves);
@@ -2971,19 +3089,21 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
             const unsigned long long z[4] = {0, 0, 0, 0};
             FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lb_stats), z, sizeof(z), 0, hipMemcpyHostToDevice, st));
         }
-        k_fast_finish<<<(ntiles + 1 + 255) / 256, 256, 0, st>>>(ctx->frame_off.as<int64_t>(), dstatus, dtiles, ntiles,
-                                                               nframes, ctx->tile_sizes.as<int64_t>());
-        std::vector<TileNorm> hn(ntiles);
-        int errv = 0;
-        FRS_HIP(hipMemcpyAsync(tile_off, ctx->tile_sizes.ptr, sizeof(int64_t) * (ntiles + 1), hipMemcpyDeviceToHost, st));
-        FRS_HIP(hipMemcpyAsync(hn.data(), dnorms, sizeof(TileNorm) * ntiles, hipMemcpyDeviceToHost, st));
-        FRS_HIP(hipMemcpyAsync(&errv, err_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+        FRS_HIP(ctx->host_pack.ensure(res_bytes));
+        int64_t *dpack = ctx->host_pack.as<int64_t>();
+        k_fast_finish<<<(ntiles + 1 + 255) / 256, 256, 0, st>>>(ctx->frame_off.as<int64_t>(), dstatus, dtiles, dnorms,
+                                                               err_flag, ntiles, nframes, dpack);
+        const int64_t *hpack = ctx->pin.at<int64_t>(pin_res);
+        FRS_HIP(hipMemcpyAsync(ctx->pin.at<int64_t>(pin_res), dpack, res_bytes, hipMemcpyDeviceToHost, st));
         FRS_HIP(hipStreamSynchronize(st));
         prof_collect(ctx);
+        memcpy(tile_off, hpack, sizeof(int64_t) * (ntiles + 1));
+        const double *mm = reinterpret_cast<const double *>(hpack + ntiles + 1);
         for (int t = 0; t < ntiles; t++) {
-            tile_min[t] = hn[t].dmin;
-            tile_max[t] = hn[t].dmax;
+            tile_min[t] = mm[2 * t];
+            tile_max[t] = mm[2 * t + 1];
         }
+        const int errv = (int)hpack[3 * (int64_t)ntiles + 1];
         if (errv & 16) {
             ctx->err = "arena too small";
             return FRS_E_NOSPACE;

@@ -33,6 +33,29 @@ struct DevBuf {
     template <typename T> T *as() const { return reinterpret_cast<T *>(ptr); }
 };
 
+// pinned host staging (small per-call H2D tables and the packed D2H results of the fast encode path): one
+// allocation reused across calls, so the copies are DMA transfers instead of staged pageable copies
+struct HostPin {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t need) {
+        if (need <= bytes) return hipSuccess;
+        if (ptr) hipHostFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+        size_t want = need + need / 8 + 4096;
+        hipError_t e = hipHostMalloc(&ptr, want, hipHostMallocDefault);
+        if (e == hipSuccess) bytes = want;
+        return e;
+    }
+    void release() {
+        if (ptr) hipHostFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+    template <typename T> T *at(size_t off) const { return reinterpret_cast<T *>(static_cast<char *>(ptr) + off); }
+};
+
 struct ProfEntry {
     double total_ms = 0.0;
     int count = 0;
@@ -51,6 +74,8 @@ struct frs_ctx {
     int ablate = 0;              // diagnostics: FRS_ABLATE bitmask (outputs invalid when set)
     // host staging (pinned)
     DevBuf raster_stage, arena_stage;  // device copies for the host-pointer entry points
+    HostPin pin;                       // pinned staging of the fast encode path (tiles, wave table, results)
+    DevBuf host_pack;                  // device side of the packed fast-path results
     // decode scratch
     DevBuf dec_cand, dec_count, dec_blob, dec_pcm, dec_soff, dec_poff, dec_next;
     // profiling

@@ -150,3 +150,32 @@ def test_fast_path_scale_and_noise(gpu_ctx, kind, shape, tile):
     o_arena, o_off, o_mn, o_mx = O.encode_tiles(band, tile, threads=8)
     assert list(off) == list(o_off)
     assert arena.tobytes() == o_arena.tobytes()
+
+
+@pytest.mark.parametrize("dtype,lo,hi,tile", [
+    (np.int16, 900, 1800, 512),      # LUT tiles
+    (np.uint16, 0, 40000, 256),      # fast-division tiles (the SLOW analysis launch)
+    (np.int16, -30000, 30000, 128),  # wrapping range (exact division)
+])
+def test_fast_path_stats_modes(dtype, lo, hi, tile, monkeypatch):
+    """The fast path's tile stats run fused into the analysis launch (one wave per tile; default) or as separate
+    kernels before it (FRS_ABLATE 4096): both must give the oracle's bytes, also on a second call."""
+    from flac_raster_amd import _native
+    rng = np.random.default_rng(99)
+    H, W = 768, 1280
+    y, x = np.meshgrid(np.linspace(0, 1, H), np.linspace(0, 1, W), indexing="ij")
+    band = np.clip(lo + (hi - lo) * (0.5 + 0.45 * np.sin(7 * x) * np.cos(3 * y))
+                   + rng.normal(0, (hi - lo) * 0.01 + 0.3, (H, W)), lo, hi).astype(dtype)
+    band[:tile, :tile] = band[0, 0]
+    o_arena, o_off, o_mn, o_mx = O.encode_tiles(band, tile, threads=8)
+    for ablate in ("0", "4096"):
+        monkeypatch.setenv("FRS_ABLATE", ablate)
+        ctx = _native.Context(0)
+        try:
+            for _ in range(2):  # second call reuses the side stream, events and scratch
+                arena, off, mn, mx, bps = _gpu_tiles(ctx, band, tile)
+                assert list(off) == list(o_off), ablate
+                assert arena.tobytes() == o_arena.tobytes(), ablate
+                assert list(mn) == list(o_mn) and list(mx) == list(o_mx), ablate
+        finally:
+            ctx.close()
