@@ -1981,12 +1981,28 @@ struct EncV3Shared {
     int lut_tile;
 };
 
+// Bank-aware layout of a wave's frame buffer.  Word w of the frame lives at row (w mod C), column (w / C) of a
+// 64-column matrix, C = ceil(words / 64) <= 34 chosen per frame: phys(w) = (w mod C) * 64 + w / C, so the LDS
+// bank is the column.  Lane L's codes fill roughly column L, so the 64 lanes' concurrent bit-writer atomics
+// land in distinct banks whatever each lane's progress (in the plain layout they hit banks
+// (base_L + progress_L) mod 32: a birthday-problem 3-4 way conflict).  w / C = (w * ceil(2^20 / C)) >> 20,
+// exact for w < 2400 and C <= 34 (checked exhaustively), so phys costs a 24-bit multiply, a shift and a mad.
+struct FbMap {
+    uint32_t c, magic, k;  // C, ceil(2^20 / C), 64 C - 1
+    __device__ inline uint32_t col(uint32_t w) const { return __umul24(w, magic) >> 20; }
+    __device__ inline uint32_t operator()(uint32_t w) const { return (w << 6) - __umul24(col(w), k); }
+};
+__device__ inline FbMap fb_map(uint32_t words) {  // words the frame may touch (<= kFrameWordsV3)
+    const uint32_t c = max(1u, (words + 63) >> 6);
+    return FbMap{c, ((1u << 20) + c - 1) / c, 64 * c - 1};
+}
+
 // bit writer without branches: the (up to 32-bit) code at [pos, pos + nbits) straddles at most 2 words
-__device__ inline void lds_put_bits2(uint32_t *buf, uint32_t pos, uint32_t val, int nbits) {
+__device__ inline void lds_put_bits2(uint32_t *buf, const FbMap &M, uint32_t pos, uint32_t val, int nbits) {
     const uint32_t wi = pos >> 5;
     const uint64_t v = (uint64_t)val << (64 - (int)(pos & 31) - nbits);
-    atomicOr(&buf[wi], (uint32_t)(v >> 32));
-    atomicOr(&buf[wi + 1], (uint32_t)v);
+    atomicOr(&buf[M(wi)], (uint32_t)(v >> 32));
+    atomicOr(&buf[M(wi + 1)], (uint32_t)v);
 }
 
 // opaque register barrier: stops the compiler from carrying 64 residuals across passes (CSE) and
@@ -2004,12 +2020,13 @@ __device__ inline uint32_t sad_u32(uint32_t a, uint32_t b, uint32_t c) {
 }
 
 // OR a left-aligned code (its first bit in bit 31) into the bit buffer at bit position pos
-__device__ inline void lds_put_left(uint32_t *buf, uint32_t pos, uint32_t codeL) {
+__device__ inline void lds_put_left(uint32_t *buf, const FbMap &M, uint32_t pos, uint32_t codeL) {
     const uint32_t hi = __builtin_amdgcn_alignbit(0u, codeL, pos);  // codeL >> (pos & 31)
     const uint32_t lo = __builtin_amdgcn_alignbit(codeL, 0u, pos);  // codeL << (32 - (pos & 31)); 0 if aligned
-    uint32_t *w = buf + (pos >> 5);
-    atomicOr(w, hi);
-    atomicOr(w + 1, lo);
+    // phys(wi + 1) = phys(wi) + 64 - (col(wi + 1) - col(wi)) * (64 C - 1); the + 64 folds into the ds offset
+    const uint32_t wi = pos >> 5, t = __umul24(wi, M.magic), base = wi << 6;
+    atomicOr(buf + (base - __umul24(t >> 20, M.k)), hi);
+    atomicOr(buf + (base - __umul24((t + M.magic) >> 20, M.k)) + 64, lo);
 }
 
 __device__ inline uint32_t zigzag(int32_t r) { return ((uint32_t)r << 1) ^ (uint32_t)(r >> 31); }
@@ -2018,6 +2035,7 @@ struct PendingFrame {  // a frame whose bytes sit in the wave's bit buffer, offs
     int64_t f = -1;
     uint64_t fbytes = 0;
     bool ok = true;
+    FbMap map{1, 1u << 20, 63};  // the frame's buffer layout
 };
 
 __device__ inline void sample_rate_code(int sr, int &src, int &srx) {  // RFC 9639 9.1.2
@@ -2120,44 +2138,47 @@ __device__ inline void resolve_and_store(const EncodeParams &P, PendingFrame &pf
             __hip_atomic_store(&status[f], kFlagIncl | (prefix + fbytes), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         frame_off[f] = (int64_t)prefix;
     }
-    const uint32_t used_words = ok ? (uint32_t)((fbytes + 3) >> 2) + 2 : (uint32_t)kFrameWordsV3;
+    const FbMap M = pf.map;
     if ((int64_t)(prefix + fbytes) > arena_cap) {
         if (l0) atomicOr(err, 16);
     } else if (!(P.ablate & 16) && fbytes) {
         // ---- store [prefix, prefix + fbytes): bytes up to 16-B alignment, 16-B chunks, byte tail
         uint8_t *dst = arena + prefix;
         const uint32_t a0 = min((uint32_t)fbytes, (uint32_t)((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15));
-        auto byte_at = [&](uint32_t b) -> uint8_t { return (uint8_t)(fbuf[b >> 2] >> (24 - 8 * (b & 3))); };
+        auto byte_at = [&](uint32_t b) -> uint8_t { return (uint8_t)(fbuf[M(b >> 2)] >> (24 - 8 * (b & 3))); };
         if ((uint32_t)lane < a0) dst[lane] = byte_at((uint32_t)lane);
         const uint32_t n16 = ((uint32_t)fbytes - a0) >> 4;
         const uint32_t r = a0 & 3, sb = a0 >> 2;
         uint4 *d16 = reinterpret_cast<uint4 *>(dst + a0);
-        // words sb .. sb + 4 of chunk ci from two 16-B aligned LDS reads (ds_read_b128: consecutive lanes hit
-        // consecutive banks; five dword reads at a 4-word lane stride were 4-way bank conflicts)
-        const uint4 *fb4 = reinterpret_cast<const uint4 *>(fbuf);
-        for (uint32_t ci = (uint32_t)lane; ci < n16; ci += 64) {
-            const uint4 A4 = fb4[ci], B4 = fb4[ci + 1];
-            uint32_t v0, v1, v2, v3, v4;
-            switch (sb) {  // wave-uniform
-            case 0: v0 = A4.x; v1 = A4.y; v2 = A4.z; v3 = A4.w; v4 = B4.x; break;
-            case 1: v0 = A4.y; v1 = A4.z; v2 = A4.w; v3 = B4.x; v4 = B4.y; break;
-            case 2: v0 = A4.z; v1 = A4.w; v2 = B4.x; v3 = B4.y; v4 = B4.z; break;
-            default: v0 = A4.w; v1 = B4.x; v2 = B4.y; v3 = B4.z; v4 = B4.w; break;
-            }
-            const uint32_t w0 = __builtin_bswap32(v0), w1 = __builtin_bswap32(v1), w2 = __builtin_bswap32(v2);
-            const uint32_t w3 = __builtin_bswap32(v3), w4 = __builtin_bswap32(v4);
+        // 16-B chunk ci = words sb + 4 ci .. sb + 4 ci + 4.  Lane L takes the chunks of column L (ci = L C/4 + j),
+        // so at each step the 64 lanes read one buffer row: consecutive banks
+        auto chunk = [&](uint32_t ci) {
+            const uint32_t wq = sb + 4 * ci;
+            const uint32_t w0 = __builtin_bswap32(fbuf[M(wq)]), w1 = __builtin_bswap32(fbuf[M(wq + 1)]);
+            const uint32_t w2 = __builtin_bswap32(fbuf[M(wq + 2)]), w3 = __builtin_bswap32(fbuf[M(wq + 3)]);
+            const uint32_t w4 = __builtin_bswap32(fbuf[M(wq + 4)]);
             uint4 o4;
             o4.x = __builtin_amdgcn_alignbyte(w1, w0, r);
             o4.y = __builtin_amdgcn_alignbyte(w2, w1, r);
             o4.z = __builtin_amdgcn_alignbyte(w3, w2, r);
             o4.w = __builtin_amdgcn_alignbyte(w4, w3, r);
             d16[ci] = o4;
-        }
+        };
+        // the chunks whose first word lies in column L: at each step the lanes read rows within 3 of each
+        // other in their own columns, i.e. distinct banks
+        const uint32_t c0 = (uint32_t)lane * M.c, c1 = c0 + M.c;
+        const uint32_t ci0 = c0 > sb ? (c0 - sb + 3) >> 2 : 0u, ci1 = c1 > sb ? min(n16, (c1 - sb + 3) >> 2) : 0u;
+        for (uint32_t ci = ci0; ci < ci1; ci++) chunk(ci);
         const uint32_t tb = a0 + 16 * n16 + (uint32_t)lane;
         if (tb < (uint32_t)fbytes) dst[tb] = byte_at(tb);
     }
-    // leave the bit buffer zeroed for this wave's next frame (LDS ops of one wave complete in order)
-    for (uint32_t i = (uint32_t)lane; i < used_words; i += 64) fbuf[i] = 0;
+    // leave the bit buffer zeroed for this wave's next frame (LDS ops of one wave complete in order): the C rows
+    // of the frame's matrix, or the whole buffer after a failed frame
+    if (ok) {
+        for (uint32_t i = 0; i < M.c; i++) fbuf[(i << 6) | (uint32_t)lane] = 0;
+    } else {
+        for (uint32_t i = (uint32_t)lane; i < (uint32_t)kFrameWordsV3; i += 64) fbuf[i] = 0;
+    }
     pf.f = -1;
 }
 
@@ -2534,6 +2555,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     }
     const uint32_t body = (end_bits + 7) >> 3;  // bytes before the CRC-16 footer
     const uint64_t fbytes = ok ? (uint64_t)body + 2 : 0;
+    const FbMap M = fb_map(((end_bits + 23) >> 5) + 2);  // words written: body, CRC-16 (byte aligned), one spare
     if (l0) {  // publish our aggregate
         const uint64_t v = (f == 0 ? kFlagIncl : kFlagAgg) | fbytes;
         __hip_atomic_store(&status[f], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2545,15 +2567,15 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     // ---- phase B: every bit of this frame into the (zeroed) buffer, then the CRC-16
     if (l0 && tab) {
         // 13 header bytes at most; the 4th word's low byte holds the length (byte 15: never a header byte)
-        fbuf[0] = hrow.x;
-        fbuf[1] = hrow.y;
-        fbuf[2] = hrow.z;
-        fbuf[3] = hrow.w & 0xFFFFFF00u;
+        fbuf[M(0)] = hrow.x;
+        fbuf[M(1)] = hrow.y;
+        fbuf[M(2)] = hrow.z;
+        fbuf[M(3)] = hrow.w & 0xFFFFFF00u;
     }
     if (l0) {
         uint32_t hbits = 0, c8 = 0;
         auto put8 = [&](uint32_t b) {
-            lds_put_bits2(fbuf, hbits, b, 8);
+            lds_put_bits2(fbuf, M, hbits, b, 8);
             c8 = S.crc8[c8 ^ b];
             hbits += 8;
         };
@@ -2576,35 +2598,35 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         put8(c8);  // CRC-8 (the table lookup of the last call is unused)
         }
         const int typecode = type == 0 ? 0 : type == 1 ? 1 : type == 2 ? 8 + of : 32 + ol - 1;
-        lds_put_bits2(fbuf, hdr_bits, (uint32_t)(typecode << 1) | (w ? 1u : 0u), 8);
-        if (w) lds_put_bits2(fbuf, hdr_bits + 8 + (uint32_t)(w - 1), 1, 1);
+        lds_put_bits2(fbuf, M, hdr_bits, (uint32_t)(typecode << 1) | (w ? 1u : 0u), 8);
+        if (w) lds_put_bits2(fbuf, M, hdr_bits + 8 + (uint32_t)(w - 1), 1, 1);
         const uint32_t smask = (1u << sbps) - 1u;
-        if (type == 0) lds_put_bits2(fbuf, pos0, (uint32_t)X(0) & smask, sbps);
+        if (type == 0) lds_put_bits2(fbuf, M, pos0, (uint32_t)X(0) & smask, sbps);
         if (type >= 2) {
             uint32_t q = pos0;
 #pragma unroll
             for (int i = 0; i < kMaxLpc; i++)
-                if (i < o) lds_put_bits2(fbuf, q + (uint32_t)i * sbps, (uint32_t)X(i) & smask, sbps);
+                if (i < o) lds_put_bits2(fbuf, M, q + (uint32_t)i * sbps, (uint32_t)X(i) & smask, sbps);
             q += (uint32_t)o * sbps;
             if (type == 3) {
-                lds_put_bits2(fbuf, q, (uint32_t)(A.lpc_prec - 1), 4);
-                lds_put_bits2(fbuf, q + 4, (uint32_t)lshift & 31u, 5);
+                lds_put_bits2(fbuf, M, q, (uint32_t)(A.lpc_prec - 1), 4);
+                lds_put_bits2(fbuf, M, q + 4, (uint32_t)lshift & 31u, 5);
 #pragma unroll
                 for (int i = 0; i < kMaxLpc; i++)
                     if (i < o)
-                        lds_put_bits2(fbuf, q + 9 + (uint32_t)i * A.lpc_prec,
+                        lds_put_bits2(fbuf, M, q + 9 + (uint32_t)i * A.lpc_prec,
                                       (uint32_t)A.q[i] & ((1u << A.lpc_prec) - 1u), A.lpc_prec);
                 q += 9 + (uint32_t)o * A.lpc_prec;
             }
-            lds_put_bits2(fbuf, q, (uint32_t)po, 6);  // RICE (00) + partition order (4 bits)
+            lds_put_bits2(fbuf, M, q, (uint32_t)po, 6);  // RICE (00) + partition order (4 bits)
         }
     }
-    if (type >= 2 && ok && (lane & (lanes_per - 1)) == 0) lds_put_bits2(fbuf, run - 4u, (uint32_t)k, 4);
+    if (type >= 2 && ok && (lane & (lanes_per - 1)) == 0) lds_put_bits2(fbuf, M, run - 4u, (uint32_t)k, 4);
     if (type == 1) {
         const uint32_t p0 = pos + (uint32_t)(64 * lane) * (uint32_t)sbps;
         const uint32_t shl = 32u - (uint32_t)sbps;
 #pragma unroll
-        for (int j = 0; j < 64; j++) lds_put_left(fbuf, p0 + (uint32_t)j * sbps, (uint32_t)X(j) << shl);
+        for (int j = 0; j < 64; j++) lds_put_left(fbuf, M, p0 + (uint32_t)j * sbps, (uint32_t)X(j) << shl);
     } else if (type >= 2 && ok && !(P.ablate & 4)) {
         // code = stop bit + k low bits, left-aligned: (u << (31 - k)) with the stop bit forced on
         const uint32_t sh = 31u - (uint32_t)k, oneL = 0x80000000u, lowL = (k ? (0xFFFFFFFFu >> (32 - k)) : 0u) << sh;
@@ -2623,7 +2645,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
                     codeL = 0;
                     adv = 0;
                 }
-                lds_put_left(fbuf, run + q, codeL);
+                lds_put_left(fbuf, M, run + q, codeL);
                 run += adv;
             }
         }
@@ -2634,18 +2656,19 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     if (ok && !(P.ablate & 2)) {
         // slice-by-4 over 32-bit words, one contiguous word range per lane, combined with x^(8m) factors
         const uint32_t nfw = body >> 2, tail = body & 3;
-        // odd words per lane: lane bases cw apart fall in 32 distinct LDS banks (cw = 32 would be 32-way)
-        const uint32_t cw = ((nfw + 63) >> 6) | 1u;
-        const uint32_t wb = min(nfw, (uint32_t)lane * cw), we = min(nfw, wb + cw);
+        // lane L takes column L of the buffer (words L C .. L C + C - 1), so at each step the lanes read one row:
+        // consecutive banks
+        const uint32_t wb = min(nfw, (uint32_t)lane * M.c), we = min(nfw, wb + M.c);
         uint32_t c = 0;
-        for (uint32_t i = wb; i < we; i++) {
-            const uint32_t word = fbuf[i];
+        const uint32_t *colp = fbuf + lane;
+        for (uint32_t i = wb; i < we; i++, colp += 64) {
+            const uint32_t word = *colp;
             c = (uint32_t)S.crc4[3][((c >> 8) ^ (word >> 24)) & 0xFF] ^ S.crc4[2][((c & 0xFF) ^ (word >> 16)) & 0xFF] ^
                 S.crc4[1][(word >> 8) & 0xFF] ^ S.crc4[0][word & 0xFF];
         }
         uint32_t end = we * 4;
-        if (lane == (int)((nfw - 1) / cw)) {
-            const uint32_t word = fbuf[nfw];
+        if (lane == (int)M.col(nfw - 1)) {
+            const uint32_t word = fbuf[M(nfw)];
             for (uint32_t b = 0; b < tail; b++) {
                 const uint32_t byte = (word >> (24 - 8 * b)) & 0xFF;
                 c = ((c << 8) & 0xFFFFu) ^ S.crc4[0][((c >> 8) ^ byte) & 0xFF];
@@ -2654,11 +2677,12 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         }
         const uint32_t m = body - end;
         crc = dpp_wave_xor_u32(gf_mulmod(gf_mulmod(c, S.xlo[m & 63]), S.xhi[m >> 6]));
-        if (l0) lds_put_bits2(fbuf, body << 3, crc, 16);
+        if (l0) lds_put_bits2(fbuf, M, body << 3, crc, 16);
     }
     prev.f = f;
     prev.fbytes = fbytes;
     prev.ok = ok;
+    prev.map = M;
 }
 
 template <int DT>
