@@ -1986,15 +1986,19 @@ struct EncV3Shared {
 // bank is the column.  Lane L's codes fill roughly column L, so the 64 lanes' concurrent bit-writer atomics
 // land in distinct banks whatever each lane's progress (in the plain layout they hit banks
 // (base_L + progress_L) mod 32: a birthday-problem 3-4 way conflict).  w / C = (w * ceil(2^20 / C)) >> 20,
-// exact for w < 2400 and C <= 34 (checked exhaustively), so phys costs a 24-bit multiply, a shift and a mad.
+// exact for w < 2400 and C <= 34, and the column of bit position b is mulhi(b, ceil(2^32 / 32 C)), exact for
+// b < 2^17 (both checked exhaustively), so phys costs a multiply and a 24-bit mad.
 struct FbMap {
-    uint32_t c, magic, k;  // C, ceil(2^20 / C), 64 C - 1
+    uint32_t c, magic, k, bmagic;  // C, ceil(2^20 / C), 64 C - 1, ceil(2^32 / 32 C)
     __device__ inline uint32_t col(uint32_t w) const { return __umul24(w, magic) >> 20; }
-    __device__ inline uint32_t operator()(uint32_t w) const { return (w << 6) - __umul24(col(w), k); }
+    __device__ inline uint32_t operator()(uint32_t w) const {
+        return (uint32_t)__mul24((int)col(w), -(int)k) + (w << 6);
+    }
+    __device__ inline uint32_t bitcol(uint32_t b) const { return __umulhi(b, bmagic); }
 };
 __device__ inline FbMap fb_map(uint32_t words) {  // words the frame may touch (<= kFrameWordsV3)
     const uint32_t c = max(1u, (words + 63) >> 6);
-    return FbMap{c, ((1u << 20) + c - 1) / c, 64 * c - 1};
+    return FbMap{c, ((1u << 20) + c - 1) / c, 64 * c - 1, (uint32_t)((0x100000000ull + 32 * c - 1) / (32 * c))};
 }
 
 // bit writer without branches: the (up to 32-bit) code at [pos, pos + nbits) straddles at most 2 words
@@ -2023,10 +2027,10 @@ __device__ inline uint32_t sad_u32(uint32_t a, uint32_t b, uint32_t c) {
 __device__ inline void lds_put_left(uint32_t *buf, const FbMap &M, uint32_t pos, uint32_t codeL) {
     const uint32_t hi = __builtin_amdgcn_alignbit(0u, codeL, pos);  // codeL >> (pos & 31)
     const uint32_t lo = __builtin_amdgcn_alignbit(codeL, 0u, pos);  // codeL << (32 - (pos & 31)); 0 if aligned
-    // phys(wi + 1) = phys(wi) + 64 - (col(wi + 1) - col(wi)) * (64 C - 1); the + 64 folds into the ds offset
-    const uint32_t wi = pos >> 5, t = __umul24(wi, M.magic), base = wi << 6;
-    atomicOr(buf + (base - __umul24(t >> 20, M.k)), hi);
-    atomicOr(buf + (base - __umul24((t + M.magic) >> 20, M.k)) + 64, lo);
+    // phys(wi + 1) = (wi << 6) - col(wi + 1) (64 C - 1) + 64; the + 64 folds into the ds offset
+    const uint32_t base = (pos >> 5) << 6;
+    atomicOr(buf + ((uint32_t)__mul24((int)M.bitcol(pos), -(int)M.k) + base), hi);
+    atomicOr(buf + ((uint32_t)__mul24((int)M.bitcol(pos + 32), -(int)M.k) + base) + 64, lo);
 }
 
 __device__ inline uint32_t zigzag(int32_t r) { return ((uint32_t)r << 1) ^ (uint32_t)(r >> 31); }
@@ -2168,7 +2172,22 @@ __device__ inline void resolve_and_store(const EncodeParams &P, PendingFrame &pf
         // other in their own columns, i.e. distinct banks
         const uint32_t c0 = (uint32_t)lane * M.c, c1 = c0 + M.c;
         const uint32_t ci0 = c0 > sb ? (c0 - sb + 3) >> 2 : 0u, ci1 = c1 > sb ? min(n16, (c1 - sb + 3) >> 2) : 0u;
-        for (uint32_t ci = ci0; ci < ci1; ci++) chunk(ci);
+        // chunks before the column's last lie wholly in column L: rows r .. r + 4 at phys r * 64 + L
+        if (ci0 < ci1) {
+            const uint32_t *cp = fbuf + M(sb + 4 * ci0);
+            for (uint32_t ci = ci0; ci + 1 < ci1; ci++, cp += 256) {
+                const uint32_t w0 = __builtin_bswap32(cp[0]), w1 = __builtin_bswap32(cp[64]);
+                const uint32_t w2 = __builtin_bswap32(cp[128]), w3 = __builtin_bswap32(cp[192]);
+                const uint32_t w4 = __builtin_bswap32(cp[256]);
+                uint4 o4;
+                o4.x = __builtin_amdgcn_alignbyte(w1, w0, r);
+                o4.y = __builtin_amdgcn_alignbyte(w2, w1, r);
+                o4.z = __builtin_amdgcn_alignbyte(w3, w2, r);
+                o4.w = __builtin_amdgcn_alignbyte(w4, w3, r);
+                d16[ci] = o4;
+            }
+            chunk(ci1 - 1);
+        }
         const uint32_t tb = a0 + 16 * n16 + (uint32_t)lane;
         if (tb < (uint32_t)fbytes) dst[tb] = byte_at(tb);
     }
