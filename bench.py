@@ -31,6 +31,9 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E peak 8.0 TB/s
+# VALU issue peak: 1024 SIMDs x 2.4 GHz x 1/2 wave64 instruction per cycle (MI355X_MICROARCH.md: a wave64 VALU
+# instruction issues over 2 cycles, 32 lanes/cycle; = the 157.3 TFLOPS FP32 vector peak / 128 FLOP)
+VALU_PEAK_GINST_S = 1024 * 2.4 * 0.5
 METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"] if (ROOT / "BASELINE.json").exists() else \
     "Mpixels/sec encode (create-streaming) + bbox-extract ms, 1/2/4/8 GPU; bit-exact vs ref"
 KERNEL_SYMBOL = {"encode": "frs::k_encode_v3<3>", "analyze": "frs::k_analyze_v3<3, false, true>",
@@ -185,6 +188,12 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic_for(args.traffic_json, dom, px_rank)},
     }
+    valu = pmc_for(args.traffic_json, dom, px_rank, "valu_insts")
+    if valu:  # the integer encoder is issue-bound, not HBM-bound: its VALU instruction rate vs the issue peak
+        rate = valu / (dom_ms * 1e-3) / 1e9
+        result["roofline"]["issue"] = {"valu_insts": round(valu), "achieved": round(rate, 1),
+                                       "peak": VALU_PEAK_GINST_S, "unit": "G wave-instr/s",
+                                       "frac": round(rate / VALU_PEAK_GINST_S, 4)}
 
     if rank == 0 and args.queries > 0:
         result["bbox_extract"] = bbox_extract(ctx, raster, arena, off, mn, mx, rows, W, T, args.queries)
@@ -258,8 +267,8 @@ def bbox_extract(ctx, raster, arena, off, tmin, tmax, rows, W, T, nq):
             "kernels_ms": kern, "lossless_spot_checks": checked, "lossless": lossless}
 
 
-def traffic_for(path, kernel, px):
-    """HBM bytes per launch of `kernel` from a committed PMC summary (tools/pmc_traffic.py) measured on this
+def pmc_for(path, kernel, px, field):
+    """Per-launch PMC figure `field` of `kernel` from a committed summary (tools/pmc_traffic.py) measured on this
     same workload (C4 slab of `px` pixels); None when absent or taken on another workload."""
     try:
         d = json.loads(Path(path).read_text())
@@ -268,7 +277,13 @@ def traffic_for(path, kernel, px):
     if d.get("pixels_per_launch") not in (None, px):
         return None
     k = d.get("kernels", {}).get(KERNEL_SYMBOL.get(kernel, kernel))
-    return None if k is None else round(k["bytes"])
+    return None if k is None or field not in k else k[field]
+
+
+def traffic_for(path, kernel, px):
+    """HBM bytes per launch of `kernel` (FETCH_SIZE x2 + WRITE_SIZE passes)."""
+    b = pmc_for(path, kernel, px, "bytes")
+    return None if b is None else round(b)
 
 
 def cpu_baseline(ctx, raster, rows, W, T, off, arena, args):

@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
 """HBM traffic per kernel launch from rocprofv3 --pmc passes (run_counter_collection.csv).
 
-Usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json [--label TEXT] [--pixels PIXELS_PER_LAUNCH]
+Usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json [--label TEXT] [--pixels PIXELS_PER_LAUNCH] [--valu DIR]
 
 FETCH_SIZE and WRITE_SIZE are in KB per dispatch (summed over TCC instances here).  On gfx950 FETCH_SIZE
 counts half the bytes of wide streaming reads, so it is doubled (MI355X_MICROARCH.md, "HBM [CDNA4]");
 WRITE_SIZE is taken as is.  The JSON maps kernel short names to mean bytes per launch, and bench.py copies
-the dominant kernel's figure into roofline.traffic.
+the dominant kernel's figure into roofline.traffic.  --valu DIR (a `--pmc SQ_INSTS_VALU` pass) adds the mean
+wave-level VALU instructions per launch, which bench.py turns into roofline.issue (VALU issue rate vs peak).
 """
 import csv
 import json
@@ -42,10 +43,14 @@ def main():
         rd = 2 * fr.get(k, 0.0) * 1024
         wb = wr.get(k, 0.0) * 1024
         kernels[k] = {"read_bytes": rd, "write_bytes": wb, "bytes": rd + wb}
+    if "--valu" in sys.argv:
+        for k, v in per_dispatch(sys.argv[sys.argv.index("--valu") + 1], "SQ_INSTS_VALU").items():
+            kernels.setdefault(k, {})["valu_insts"] = v
     json.dump({"label": label, "pixels_per_launch": pixels, "fetch_correction": 2.0, "kernels": kernels},
               open(dst, "w"), indent=1)
     for k, v in kernels.items():
-        print(f"{k}: read {v['read_bytes'] / 1e9:.3f} GB write {v['write_bytes'] / 1e9:.3f} GB")
+        print(f"{k}: read {v.get('read_bytes', 0) / 1e9:.3f} GB write {v.get('write_bytes', 0) / 1e9:.3f} GB "
+              f"valu {v.get('valu_insts', 0):.4g}")
 
 
 if __name__ == "__main__":
