@@ -847,7 +847,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                                                            const int64_t *ends, const int64_t *fbase,
                                                            const int64_t *frame_cand, int64_t nframes, int channels,
                                                            int stream_bps, int32_t *pcm, int blocksize, int *nvalid) {
-    __shared__ uint32_t stage[kDecStageWords + 8];  // + the window step's look-ahead words
+    __shared__ uint32_t stage[kDecStageWords + 12];  // + the window step's look-ahead words
     __shared__ int32_t resbuf[kDecResMax];
     __shared__ uint32_t xout[kDecResMax / 2];  // restored samples as int16 pairs
     __shared__ PipeInfo info;
@@ -861,7 +861,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     const int64_t wb = fpos >> 2, we = (fend_known + 3) >> 2;
     const bool staged = we - wb <= kDecStageWords;
     if (staged)  // big-endian words: the scalar bit reader needs no byte swap
-        for (int64_t k = threadIdx.x; k < we - wb + 8; k += 128)
+        for (int64_t k = threadIdx.x; k < we - wb + 12; k += 128)
             stage[k] = __builtin_bswap32(load_word_guarded(blob, wb + k, send));
     if (threadIdx.x == 0) {
         info.state = 0;
@@ -1015,18 +1015,23 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
             }
             P = br.pos();
             const int k1 = kp + 1;
-            // Window step: lane j decodes the Rice codes that would start at bits P + j and P + 64 + j (from
-            // big-endian stage words); the scalar unit then walks the chain of actual code starts through those
-            // 128 candidates (one v_readlane per code) and the lanes on the chain store their residuals in order.
+            // Window step over 256 bits: lane j decodes the Rice codes that would start at bits P + j + 64q
+            // (q = 0..3, from big-endian stage words); the scalar unit walks the chain of actual code starts through
+            // those 256 candidates (one v_readlane per code) and records the m-th start in lane m of `posv`
+            // (one v_cndmask); lane m then fetches its residual from the candidate's lane by ds_bpermute and the
+            // window's residuals leave in one contiguous LDS store.  A 256-bit window holds ~16 codes of a
+            // 15-bit/sample frame, so the per-window fixed cost (stage reads, candidate decode, store) is paid half
+            // as often as with a 128-bit window.
             while (left > 0) {
                 if (P > lim) {
                     bad = true;
                     break;
                 }
                 const uint32_t b = P + (uint32_t)lane, wi = b >> 5, sh = b & 31u;
-                const uint32_t w0 = stage[wi], w1 = stage[wi + 1], w2 = stage[wi + 2], w3 = stage[wi + 3],
-                               w4 = stage[wi + 4];
-                auto cand = [&](uint32_t x0, uint32_t x1, uint32_t x2, int base, uint32_t &u) -> int {
+                uint32_t wv[9];
+#pragma unroll
+                for (int m = 0; m < 9; m++) wv[m] = stage[wi + m];
+                auto cand = [&](uint32_t x0, uint32_t x1, uint32_t x2, uint32_t &u) -> uint32_t {
                     const uint32_t hi = sh ? __builtin_amdgcn_alignbit(x0, x1, 32u - sh) : x0;
                     const uint32_t lo = sh ? __builtin_amdgcn_alignbit(x1, x2, 32u - sh) : x1;
                     const uint64_t win = ((uint64_t)hi << 32) | lo;
@@ -1034,33 +1039,36 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                     const int tot = z + k1;
                     const uint32_t low = (kp && tot <= 64) ? (uint32_t)((win << (z + 1)) >> (64 - kp)) : 0u;
                     u = ((uint32_t)z << kp) | low;
-                    return tot <= 64 ? base + lane + tot : 255;  // next code start (relative to P) or "long"
+                    return tot <= 64 ? (uint32_t)tot : 0xFFu;  // code length, or "long"
                 };
-                uint32_t ua, ub;
-                const int na = cand(w0, w1, w2, 0, ua), nb2 = cand(w2, w3, w4, 64, ub);
-                const int nxt = na | (nb2 << 16);  // candidates at P + lane (low half) and P + 64 + lane (high)
-                uint64_t ma = 0, mb = 0;
-                int cur = 0, cnt = 0;
+                uint32_t uq[4];
+                // code lengths of the candidates at P + lane + 64q packed as byte q (0xff: longer than 64 bits)
+                const uint32_t la = cand(wv[0], wv[1], wv[2], uq[0]), lb = cand(wv[2], wv[3], wv[4], uq[1]);
+                const uint32_t lc = cand(wv[4], wv[5], wv[6], uq[2]), ld = cand(wv[6], wv[7], wv[8], uq[3]);
+                const int lens = (int)(la | (lb << 8) | (lc << 16) | (ld << 24));
+                const int cap = left < 64 ? left : 64;
+                int cur = 0, cnt = 0, posv = 0;
                 bool lng = false;
-                while (cnt < left && cur < 128) {
-                    const int nx = (__builtin_amdgcn_readlane(nxt, cur & 63) >> ((cur >> 6) << 4)) & 0xFFFF;
-                    if (nx == 255) {  // the code at cur runs past its 64-bit window
+                // the walk: one v_readlane + byte extract per code, one taken branch per code
+                for (;;) {
+                    const int len = (__builtin_amdgcn_readlane(lens, cur & 63) >> ((cur >> 3) & 24)) & 0xFF;
+                    if (len == 0xFF) {  // the code at cur runs past its 64-bit window
                         lng = true;
                         break;
                     }
-                    if (cur < 64) ma |= 1ull << cur;
-                    else mb |= 1ull << (cur - 64);
+                    posv = lane == cnt ? cur : posv;  // v_cndmask off the walk's dependency chain
                     cnt++;
-                    cur = nx;
+                    cur += len;
+                    if ((cnt >= cap) | (cur >= 256)) break;
                 }
-                const uint64_t below = (1ull << lane) - 1ull;
-                if ((ma >> lane) & 1ull) {
-                    const int idx = __builtin_popcountll(ma & below);
-                    resbuf[i + idx] = (int32_t)((ua >> 1) ^ (uint32_t)(-(int32_t)(ua & 1)));
-                }
-                if ((mb >> lane) & 1ull) {
-                    const int idx = __builtin_popcountll(ma) + __builtin_popcountll(mb & below);
-                    resbuf[i + idx] = (int32_t)((ub >> 1) ^ (uint32_t)(-(int32_t)(ub & 1)));
+                {
+                    const int src = (posv & 63) << 2, q = (posv >> 6) & 3;
+                    const uint32_t g0 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)uq[0]);
+                    const uint32_t g1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)uq[1]);
+                    const uint32_t g2 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)uq[2]);
+                    const uint32_t g3 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)uq[3]);
+                    const uint32_t u = q == 0 ? g0 : q == 1 ? g1 : q == 2 ? g2 : g3;
+                    if (lane < cnt) resbuf[i + lane] = (int32_t)((u >> 1) ^ (uint32_t)(-(int32_t)(u & 1)));
                 }
                 const int i0 = i;
                 i += cnt;
@@ -1116,22 +1124,10 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     for (int m = 0; m < 8; m++)
         if (m < o && lane == 0) reinterpret_cast<int16_t *>(xout)[m] = (int16_t)wu[m];
     int avail = 0;
-    uint32_t vr = 0;
     bool failed = false;
-    for (int i = o; i < bs; i++) {
-        if (i >= avail || (i & 63) == 0 || i == o) {
-            if (i >= avail) {
-                int pg;
-                while ((pg = lds_poll(&vi->progress)) <= i && pg >= 0) __builtin_amdgcn_s_sleep(1);
-                if (pg < 0) {
-                    failed = true;
-                    break;
-                }
-                avail = pg;
-            }
-            vr = (uint32_t)resbuf[(i & ~63) + lane];
-        }
-        const int32_t r = __builtin_amdgcn_readlane((int)vr, i & 63);
+    // one sample of the recurrence: x = r + (sum q.x >> shift), the four dot2 over (newest, older) pairs with the
+    // oldest pairs first so only the last one waits on x[i-1]; the history pairs then shift by one sample
+    auto restore = [&](int32_t r, int i, bool odd) {
         int32_t pred = dec_dot2(H[3], C[3], 0);
         pred = dec_dot2(H[2], C[2], pred);
         pred = dec_dot2(H[1], C[1], pred);
@@ -1140,9 +1136,49 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
         H[3] = __builtin_amdgcn_alignbit(H[3], H[2], 16);
         H[2] = __builtin_amdgcn_alignbit(H[2], H[1], 16);
         H[1] = __builtin_amdgcn_alignbit(H[1], H[0], 16);
-        H[0] = (H[0] << 16) | ((uint32_t)x & 0xFFFFu);
-        if (i & 1) xout[i >> 1] = __builtin_amdgcn_alignbit(H[0], H[0], 16);  // (x[i] << 16) | x[i-1]
+        H[0] = __builtin_amdgcn_perm(H[0], (uint32_t)x, 0x05040100u);  // (H0 << 16) | (x & 0xffff)
+        if (odd) xout[i >> 1] = __builtin_amdgcn_alignbit(H[0], H[0], 16);  // (x[i] << 16) | x[i-1]
+    };
+    // wait until the producer has published residuals up to `need` (it publishes per 64-sample group, at
+    // partition ends and bs at the end; -1 on a bad frame)
+    auto wait_for = [&](int need) -> bool {
+        if (avail >= need) return true;
+        int pg;
+        while ((pg = lds_poll(&vi->progress)) < need && pg >= 0) __builtin_amdgcn_s_sleep(1);
+        __asm__ volatile("" ::: "memory");  // resbuf reads stay behind the poll
+        if (pg < 0) return false;
+        avail = pg;
+        return true;
+    };
+    // per-sample path with run-time lane selects: the head up to the first 64-sample boundary and any tail
+    auto generic = [&](int lo, int hi) {
+        uint32_t vr = 0;
+        for (int i = lo; i < hi; i++) {
+            if (i == lo || (i & 63) == 0) {
+                if (!wait_for(min((i & ~63) + 64, bs))) {
+                    failed = true;
+                    return;
+                }
+                vr = (uint32_t)resbuf[(i & ~63) + lane];
+            }
+            restore(__builtin_amdgcn_readlane((int)vr, i & 63), i, (i & 1) != 0);
+        }
+    };
+    const int head = min(bs, (o + 63) & ~63);
+    generic(o, head);
+    int i = head;
+    // whole 64-sample groups, fully unrolled: residual j of the group by v_readlane with an immediate lane index,
+    // no per-sample branches or scalar index arithmetic
+    for (; !failed && i + 64 <= bs; i += 64) {
+        if (!wait_for(i + 64)) {
+            failed = true;
+            break;
+        }
+        const int vr = resbuf[i + lane];
+#pragma unroll
+        for (int j = 0; j < 64; j++) restore(__builtin_amdgcn_readlane(vr, j), i + j, (j & 1) != 0);
     }
+    if (!failed && i < bs) generic(i, bs);
     if (!failed && (bs & 1)) xout[bs >> 1] = H[0] & 0xFFFFu;
     while (lds_poll(&vi->finished) == 0) __builtin_amdgcn_s_sleep(1);
     __builtin_amdgcn_s_waitcnt(0xC07F);
