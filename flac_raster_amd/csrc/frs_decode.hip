@@ -1018,8 +1018,8 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
             // Window step over 256 bits: lane j decodes the Rice codes that would start at bits P + j + 64q
             // (q = 0..3, from big-endian stage words); the scalar unit walks the chain of actual code starts through
             // those 256 candidates (one v_readlane per code) and records the m-th start in lane m of `posv`
-            // (one v_cndmask); lane m then fetches its residual from the candidate's lane by ds_bpermute and the
-            // window's residuals leave in one contiguous LDS store.  A 256-bit window holds ~16 codes of a
+            // (one v_cndmask); lane m then decodes the value of the code at that start and the window's residuals
+            // leave in one contiguous LDS store.  A 256-bit window holds ~16 codes of a
             // 15-bit/sample frame, so the per-window fixed cost (stage reads, candidate decode, store) is paid half
             // as often as with a 128-bit window.
             while (left > 0) {
@@ -1031,20 +1031,20 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                 uint32_t wv[9];
 #pragma unroll
                 for (int m = 0; m < 9; m++) wv[m] = stage[wi + m];
-                auto cand = [&](uint32_t x0, uint32_t x1, uint32_t x2, uint32_t &u) -> uint32_t {
-                    const uint32_t hi = sh ? __builtin_amdgcn_alignbit(x0, x1, 32u - sh) : x0;
-                    const uint32_t lo = sh ? __builtin_amdgcn_alignbit(x1, x2, 32u - sh) : x1;
-                    const uint64_t win = ((uint64_t)hi << 32) | lo;
-                    const int z = win ? __builtin_clzll(win) : 64;
-                    const int tot = z + k1;
-                    const uint32_t low = (kp && tot <= 64) ? (uint32_t)((win << (z + 1)) >> (64 - kp)) : 0u;
-                    u = ((uint32_t)z << kp) | low;
+                auto window64 = [&](uint32_t x0, uint32_t x1, uint32_t x2, uint32_t sft) -> uint64_t {
+                    const uint32_t hi = sft ? __builtin_amdgcn_alignbit(x0, x1, 32u - sft) : x0;
+                    const uint32_t lo = sft ? __builtin_amdgcn_alignbit(x1, x2, 32u - sft) : x1;
+                    return ((uint64_t)hi << 32) | lo;
+                };
+                auto cand = [&](uint32_t x0, uint32_t x1, uint32_t x2) -> uint32_t {
+                    const uint64_t win = window64(x0, x1, x2, sh);
+                    const int tot = (win ? __builtin_clzll(win) : 64) + k1;
                     return tot <= 64 ? (uint32_t)tot : 0xFFu;  // code length, or "long"
                 };
-                uint32_t uq[4];
-                // code lengths of the candidates at P + lane + 64q packed as byte q (0xff: longer than 64 bits)
-                const uint32_t la = cand(wv[0], wv[1], wv[2], uq[0]), lb = cand(wv[2], wv[3], wv[4], uq[1]);
-                const uint32_t lc = cand(wv[4], wv[5], wv[6], uq[2]), ld = cand(wv[6], wv[7], wv[8], uq[3]);
+                // code lengths of the candidates at P + lane + 64q packed as byte q (0xff: longer than 64 bits);
+                // the values are decoded after the walk, only at the chain's code starts
+                const uint32_t la = cand(wv[0], wv[1], wv[2]), lb = cand(wv[2], wv[3], wv[4]);
+                const uint32_t lc = cand(wv[4], wv[5], wv[6]), ld = cand(wv[6], wv[7], wv[8]);
                 const int lens = (int)(la | (lb << 8) | (lc << 16) | (ld << 24));
                 const int cap = left < 64 ? left : 64;
                 int cur = 0, cnt = 0, posv = 0;
@@ -1062,12 +1062,11 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                     if ((cnt >= cap) | (cur >= 256)) break;
                 }
                 {
-                    const int src = (posv & 63) << 2, q = (posv >> 6) & 3;
-                    const uint32_t g0 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)uq[0]);
-                    const uint32_t g1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)uq[1]);
-                    const uint32_t g2 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)uq[2]);
-                    const uint32_t g3 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)uq[3]);
-                    const uint32_t u = q == 0 ? g0 : q == 1 ? g1 : q == 2 ? g2 : g3;
+                    const uint32_t bc = P + (uint32_t)posv, wc = bc >> 5;  // lane m: the m-th code of the window
+                    const uint64_t win = window64(stage[wc], stage[wc + 1], stage[wc + 2], bc & 31u);
+                    const int z = win ? __builtin_clzll(win) : 64;
+                    const uint32_t low = kp ? (uint32_t)((win << (z + 1)) >> (64 - kp)) : 0u;
+                    const uint32_t u = ((uint32_t)z << kp) | low;
                     if (lane < cnt) resbuf[i + lane] = (int32_t)((u >> 1) ^ (uint32_t)(-(int32_t)(u & 1)));
                 }
                 const int i0 = i;
