@@ -737,6 +737,9 @@ __global__ void __launch_bounds__(64) k_decode_frames(const uint8_t *blob, const
 // scalar unit through a VGPR window (lane i = stage word wbase + i, one ds_read per 64 words) and v_readlane;
 // decoded samples leave through v_writelane into a VGPR stored by one coalesced write per 64 samples.
 constexpr int kDecStageWords = 6144;  // 24 KB
+// Rice window of the pipelined producer: kRiceWinQ candidates per lane (64 * kRiceWinQ bit positions); jump tables
+// hold the window plus the fixed points a code can end on past it (< 64 bits further)
+constexpr int kRiceWinQ = 16, kRiceWinBits = 64 * kRiceWinQ, kJumpN = kRiceWinBits + 128;
 
 struct WaveBits {
     const uint32_t *stage;  // LDS: big-endian (byte-swapped) dwords of the blob from byte 4 * wb
@@ -847,11 +850,11 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                                                            const int64_t *ends, const int64_t *fbase,
                                                            const int64_t *frame_cand, int64_t nframes, int channels,
                                                            int stream_bps, int32_t *pcm, int blocksize, int *nvalid) {
-    __shared__ uint32_t stage[kDecStageWords + 20];  // + the window step's look-ahead words
+    __shared__ uint32_t stage[kDecStageWords + 2 * kRiceWinQ + 4];  // + the window step's look-ahead words
     __shared__ int32_t resbuf[kDecResMax];
     __shared__ uint32_t xout[kDecResMax / 2];  // restored samples as int16 pairs
     __shared__ PipeInfo info;
-    __shared__ uint16_t jt[6][640];  // producer's Rice-window jump tables (512 candidates + fixed points)
+    __shared__ uint16_t jt[6][kJumpN];  // producer's Rice-window jump tables (window + fixed points)
     const int64_t fi = blockIdx.x;
     if (fi >= nframes) return;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -862,7 +865,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     const int64_t wb = fpos >> 2, we = (fend_known + 3) >> 2;
     const bool staged = we - wb <= kDecStageWords;
     if (staged)  // big-endian words: the scalar bit reader needs no byte swap
-        for (int64_t k = threadIdx.x; k < we - wb + 20; k += 128)
+        for (int64_t k = threadIdx.x; k < we - wb + 2 * kRiceWinQ + 4; k += 128)
             stage[k] = __builtin_bswap32(load_word_guarded(blob, wb + k, send));
     if (threadIdx.x == 0) {
         info.state = 0;
@@ -1002,8 +1005,8 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
         };
 #pragma unroll
         for (int k = 0; k < 6; k++) {  // jump-table entries past the window are fixed points
-            jt[k][512 + lane] = (uint16_t)(512 + lane);
-            jt[k][576 + lane] = (uint16_t)(576 + lane);
+            jt[k][kRiceWinBits + lane] = (uint16_t)(kRiceWinBits + lane);
+            jt[k][kRiceWinBits + 64 + lane] = (uint16_t)(kRiceWinBits + 64 + lane);
         }
         for (int p = 0; p < (1 << po) && !bad; p++) {
             br.seek(P);
@@ -1021,22 +1024,21 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
             }
             P = br.pos();
             const int k1 = kp + 1;
-            // Window step over 512 bits: lane j decodes the Rice codes that would start at bits P + j + 64q
-            // (q = 0..7, from big-endian stage words); the chain of actual code starts through those 512 candidates
+            // Window step over kRiceWinBits = 1024 bits: lane j decodes the Rice codes that would start at bits
+            // P + j + 64q (q < kRiceWinQ, from big-endian stage words); the chain of actual code starts through them
             // is resolved by pointer jumping over LDS tables (lane m lands on the m-th start in six reads, no
             // per-code scalar loop); lane m then decodes the value of the code at that start and the window's residuals
-            // leave in one contiguous LDS store.  A 512-bit window holds ~33 codes of a
-            // 15-bit/sample frame, so the per-window fixed cost (stage reads, candidate decode, store) is paid a
-            // quarter as often as with a 128-bit window.
+            // leave in one contiguous LDS store.  A 1024-bit window holds ~64 codes (the lane
+            // cap) of a 15-bit/sample frame: measured per tile 0.221 / 0.204 / 0.192 ms at 512 / 768 / 1024 bits.
             while (left > 0) {
                 if (P > lim) {
                     bad = true;
                     break;
                 }
                 const uint32_t b = P + (uint32_t)lane, wi = b >> 5, sh = b & 31u;
-                uint32_t wv[17];
+                uint32_t wv[2 * kRiceWinQ + 1];
 #pragma unroll
-                for (int m = 0; m < 17; m++) wv[m] = stage[wi + m];
+                for (int m = 0; m < 2 * kRiceWinQ + 1; m++) wv[m] = stage[wi + m];
                 auto window64 = [&](uint32_t x0, uint32_t x1, uint32_t x2, uint32_t sft) -> uint64_t {
                     const uint32_t hi = sft ? __builtin_amdgcn_alignbit(x0, x1, 32u - sft) : x0;
                     const uint32_t lo = sft ? __builtin_amdgcn_alignbit(x1, x2, 32u - sft) : x1;
@@ -1049,15 +1051,15 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                 };
                 // code lengths of the candidates at P + lane + 64q packed as byte q (0xff: longer than 64 bits);
                 // the values are decoded after the walk, only at the chain's code starts
-                uint32_t lq[8];
+                uint32_t lq[kRiceWinQ];
 #pragma unroll
-                for (int q = 0; q < 8; q++) lq[q] = cand(wv[2 * q], wv[2 * q + 1], wv[2 * q + 2]);
+                for (int q = 0; q < kRiceWinQ; q++) lq[q] = cand(wv[2 * q], wv[2 * q + 1], wv[2 * q + 2]);
                 // chain by pointer jumping: jt[k][c] = the code start 2^k codes after candidate c (absorbing at a
                 // long code and past the window), so lane m finds the m-th code start in six dependent LDS reads
                 const int cap = left < 64 ? left : 64;
-                int jq[8];
+                int jq[kRiceWinQ];
 #pragma unroll
-                for (int q = 0; q < 8; q++) {
+                for (int q = 0; q < kRiceWinQ; q++) {
                     const int c = lane + 64 * q;
                     jq[q] = lq[q] == 0xFFu ? c : c + (int)lq[q];
                     jt[0][c] = (uint16_t)jq[q];
@@ -1065,9 +1067,9 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
 #pragma unroll
                 for (int k = 0; k < 5; k++) {
 #pragma unroll
-                    for (int q = 0; q < 8; q++) jq[q] = jt[k][jq[q]];
+                    for (int q = 0; q < kRiceWinQ; q++) jq[q] = jt[k][jq[q]];
 #pragma unroll
-                    for (int q = 0; q < 8; q++) jt[k + 1][lane + 64 * q] = (uint16_t)jq[q];
+                    for (int q = 0; q < kRiceWinQ; q++) jt[k + 1][lane + 64 * q] = (uint16_t)jq[q];
                 }
                 int posv = 0;
 #pragma unroll
@@ -1076,13 +1078,13 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                     posv = ((lane >> k) & 1) ? nx : posv;
                 }
                 const int nxt = jt[0][posv];
-                const uint64_t chain = __ballot(posv < 512 && nxt != posv && lane < cap);  // lanes 0..cnt-1
+                const uint64_t chain = __ballot(posv < kRiceWinBits && nxt != posv && lane < cap);  // lanes 0..cnt-1
                 const int cnt = __builtin_popcountll(chain);
                 int cur;
                 bool lng = false;
                 if (cnt < cap) {  // stopped at a long code (inside the window) or past the window
                     cur = __builtin_amdgcn_readlane(posv, cnt);
-                    lng = cur < 512;
+                    lng = cur < kRiceWinBits;
                 } else {
                     cur = __builtin_amdgcn_readlane(nxt, cnt - 1);
                 }
