@@ -1,6 +1,7 @@
 """GPU decode parity: the mono 16-bit fast decoder (k_decode_frames_pipe: scalar-unit Rice decode + v_dot2 LPC
 restore in two waves) and the lane-0 decoder must both return exactly the oracle's decode of the same frames,
-for every subframe type the encoder emits (CONSTANT, VERBATIM, FIXED, LPC, wasted bits) and partial frames."""
+for every subframe type the encoder emits (CONSTANT, VERBATIM, FIXED, LPC, wasted bits), partial frames,
+Rice windows that hit the 64-code cap and codes longer than a 64-bit candidate window."""
 import numpy as np
 import pytest
 
@@ -20,7 +21,15 @@ def _bands():
     steps = (np.arange(320 * 200).reshape(320, 200) // 7 % 50 * 64).astype(np.uint16)  # wasted bits
     odd = (700 + 40 * np.sin(np.linspace(0, 30, 300 * 333)).reshape(300, 333)
            + rng.normal(0, 3, (300, 333))).astype(np.int16)  # partial frames, rows crossing frames
-    return [("dem", dem, 256), ("noise", noise, 128), ("steps", steps, 160), ("odd", odd, 128)]
+    # Rice-window edge cases of the pipelined decoder: near-flat data (Rice parameter 0-1, so a 1024-bit window
+    # holds more than its 64-code cap) and a smooth field with sparse spikes (unary runs longer than 64 bits:
+    # the producer's "long code" path through the scalar reader)
+    flat = (100 + rng.integers(-1, 2, size=(256, 256))).astype(np.int16)
+    flat[::5, :] = 100
+    spiky = (500 + 20 * np.sin(np.linspace(0, 12, 256 * 256)).reshape(256, 256)).astype(np.int16)
+    spiky.flat[rng.choice(spiky.size, 40, replace=False)] = rng.choice([-30000, 30000], 40).astype(np.int16)
+    return [("dem", dem, 256), ("noise", noise, 128), ("steps", steps, 160), ("odd", odd, 128),
+            ("flat", flat, 256), ("spiky", spiky, 256)]
 
 
 @pytest.mark.parametrize("ablate", ["0", "1024"])  # 1024: force the lane-0 decoder
