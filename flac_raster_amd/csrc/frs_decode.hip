@@ -160,8 +160,12 @@ __device__ inline uint32_t dec_gfmul(uint32_t a, uint32_t b) {
 }
 
 __global__ void __launch_bounds__(64) k_span_crc_wave(const uint8_t *blob, const int64_t *soff, int ns,
-                                                     const int64_t *cpos, const int *ncand, int64_t max_frame,
-                                                     int64_t *ends, int32_t *nexti) {
+                                                     const int64_t *cpos, const int *ncand, int cand_cap,
+                                                     int64_t max_frame, int64_t *ends, int32_t *nexti) {
+    // launched before the host knows the candidate count (no mid-query sync): idle work-groups leave at once and
+    // the rest stride over the candidates; an overflowing selection is reported by the host, not walked here
+    const int nc = *ncand;
+    if ((int)blockIdx.x >= nc || nc > cand_cap) return;
     __shared__ uint32_t stage[kSpanWords + 1];
     __shared__ uint16_t t4[4][256];
     __shared__ uint16_t xlo[256];
@@ -178,74 +182,73 @@ __global__ void __launch_bounds__(64) k_span_crc_wave(const uint8_t *blob, const
         xlo[k] = d_xpow_lo[k];
     }
     __syncthreads();
-    const int nc = *ncand;
-    const int i = blockIdx.x;
-    if (i >= nc) return;
-    const int64_t p = cpos[i];
-    const int s = stream_of(soff, ns, p);
-    const int64_t send = soff[s + 1];
-    const int64_t lim = min(send, p + max_frame);
-    int64_t result = -1;
-    int32_t rnext = -1;  // candidate index at the span's end, -2 = the stream's end
-    for (int j = i + 1;; j++) {
-        int64_t e = (j < nc) ? cpos[j] : send;
-        if (e > send) e = send;
-        if (e > lim) break;
-        if (e >= p + 7) {
-            const int64_t wb = p >> 2, we = (e + 3) >> 2;  // aligned words covering [p, e)
-            const int64_t nwords = we - wb;
-            uint32_t crc = 0;
-            if (nwords <= kSpanWords) {
-                for (int64_t k = lane; k < nwords; k += 64) stage[k] = load_word_guarded(blob, wb + k, send);
-                __builtin_amdgcn_s_waitcnt(0xC07F);
-                __builtin_amdgcn_wave_barrier();
-                const uint32_t nb = (uint32_t)(e - 2 - p);  // bytes covered by the CRC
-                const uint32_t off0 = (uint32_t)(p & 3);    // byte offset of p in stage
-                auto byte_at = [&](uint32_t b) -> uint32_t {  // b relative to p
-                    const uint32_t a = b + off0;
-                    return (stage[a >> 2] >> (8 * (a & 3))) & 0xFFu;
-                };
-                // bytes per lane: a multiple of 4 whose word count is odd (lane bases in distinct LDS banks)
-                uint32_t ch = ((nb + 63) / 64 + 3) & ~3u;
-                if (!((ch >> 2) & 1u)) ch += 4;
-                const uint32_t b0 = min(nb, (uint32_t)lane * ch), b1 = min(nb, b0 + ch);
-                uint32_t c = 0, b = b0;
-                for (; b + 4 <= b1; b += 4) {
-                    const uint32_t a = b + off0;
-                    const uint32_t lo = stage[a >> 2], hi = stage[(a >> 2) + 1];
-                    const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, a & 3);  // bytes b..b+3, LE
-                    c = (uint32_t)t4[3][((c >> 8) ^ (w & 0xFF)) & 0xFF] ^ t4[2][((c & 0xFF) ^ ((w >> 8) & 0xFF)) & 0xFF] ^
-                        t4[1][(w >> 16) & 0xFF] ^ t4[0][w >> 24];
-                }
-                for (; b < b1; b++) c = ((c << 8) & 0xFFFFu) ^ t4[0][((c >> 8) ^ byte_at(b)) & 0xFF];
-                const uint32_t m = nb - b1;  // bytes after this lane's chunk
-                c = dec_gfmul(dec_gfmul(c, xlo[m & 255]), d_xpow_hi[m >> 8]);
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) c ^= __shfl_xor(c, o);
-                crc = c;
-                const uint32_t got = (byte_at(nb) << 8) | byte_at(nb + 1);
-                __builtin_amdgcn_wave_barrier();
-                if (crc == got) {
-                    result = e;
-                    rnext = (j < nc && cpos[j] < send) ? j : -2;
-                    break;
-                }
-            } else {  // rare: a span longer than the stage
-                uint32_t c = 0;
-                for (int64_t b = p; b < e - 2; b++) c = ((c << 8) & 0xFFFFu) ^ d_crc16[((c >> 8) ^ blob[b]) & 0xFF];
-                const uint32_t got = ((uint32_t)blob[e - 2] << 8) | blob[e - 1];
-                if (c == got) {
-                    result = e;
-                    rnext = (j < nc && cpos[j] < send) ? j : -2;
-                    break;
+    for (int i = blockIdx.x; i < nc; i += gridDim.x) {
+        const int64_t p = cpos[i];
+        const int s = stream_of(soff, ns, p);
+        const int64_t send = soff[s + 1];
+        const int64_t lim = min(send, p + max_frame);
+        int64_t result = -1;
+        int32_t rnext = -1;  // candidate index at the span's end, -2 = the stream's end
+        for (int j = i + 1;; j++) {
+            int64_t e = (j < nc) ? cpos[j] : send;
+            if (e > send) e = send;
+            if (e > lim) break;
+            if (e >= p + 7) {
+                const int64_t wb = p >> 2, we = (e + 3) >> 2;  // aligned words covering [p, e)
+                const int64_t nwords = we - wb;
+                uint32_t crc = 0;
+                if (nwords <= kSpanWords) {
+                    for (int64_t k = lane; k < nwords; k += 64) stage[k] = load_word_guarded(blob, wb + k, send);
+                    __builtin_amdgcn_s_waitcnt(0xC07F);
+                    __builtin_amdgcn_wave_barrier();
+                    const uint32_t nb = (uint32_t)(e - 2 - p);  // bytes covered by the CRC
+                    const uint32_t off0 = (uint32_t)(p & 3);    // byte offset of p in stage
+                    auto byte_at = [&](uint32_t b) -> uint32_t {  // b relative to p
+                        const uint32_t a = b + off0;
+                        return (stage[a >> 2] >> (8 * (a & 3))) & 0xFFu;
+                    };
+                    // bytes per lane: a multiple of 4 whose word count is odd (lane bases in distinct LDS banks)
+                    uint32_t ch = ((nb + 63) / 64 + 3) & ~3u;
+                    if (!((ch >> 2) & 1u)) ch += 4;
+                    const uint32_t b0 = min(nb, (uint32_t)lane * ch), b1 = min(nb, b0 + ch);
+                    uint32_t c = 0, b = b0;
+                    for (; b + 4 <= b1; b += 4) {
+                        const uint32_t a = b + off0;
+                        const uint32_t lo = stage[a >> 2], hi = stage[(a >> 2) + 1];
+                        const uint32_t w = __builtin_amdgcn_alignbyte(hi, lo, a & 3);  // bytes b..b+3, LE
+                        c = (uint32_t)t4[3][((c >> 8) ^ (w & 0xFF)) & 0xFF] ^ t4[2][((c & 0xFF) ^ ((w >> 8) & 0xFF)) & 0xFF] ^
+                            t4[1][(w >> 16) & 0xFF] ^ t4[0][w >> 24];
+                    }
+                    for (; b < b1; b++) c = ((c << 8) & 0xFFFFu) ^ t4[0][((c >> 8) ^ byte_at(b)) & 0xFF];
+                    const uint32_t m = nb - b1;  // bytes after this lane's chunk
+                    c = dec_gfmul(dec_gfmul(c, xlo[m & 255]), d_xpow_hi[m >> 8]);
+    #pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) c ^= __shfl_xor(c, o);
+                    crc = c;
+                    const uint32_t got = (byte_at(nb) << 8) | byte_at(nb + 1);
+                    __builtin_amdgcn_wave_barrier();
+                    if (crc == got) {
+                        result = e;
+                        rnext = (j < nc && cpos[j] < send) ? j : -2;
+                        break;
+                    }
+                } else {  // rare: a span longer than the stage
+                    uint32_t c = 0;
+                    for (int64_t b = p; b < e - 2; b++) c = ((c << 8) & 0xFFFFu) ^ d_crc16[((c >> 8) ^ blob[b]) & 0xFF];
+                    const uint32_t got = ((uint32_t)blob[e - 2] << 8) | blob[e - 1];
+                    if (c == got) {
+                        result = e;
+                        rnext = (j < nc && cpos[j] < send) ? j : -2;
+                        break;
+                    }
                 }
             }
+            if (e >= send) break;
         }
-        if (e >= send) break;
-    }
-    if (lane == 0) {
-        ends[i] = result;
-        nexti[i] = rnext;
+        if (lane == 0) {
+            ends[i] = result;
+            nexti[i] = rnext;
+        }
     }
 }
 
@@ -294,6 +297,7 @@ __device__ inline int lower_bound_pos(const int64_t *cpos, int n, int64_t p) {
     return lo;
 }
 __global__ void __launch_bounds__(64) k_chain_lds(const int64_t *soff, int ns, const int64_t *cpos, const int *ncand,
+                                                 int cand_cap,
                                                  const int32_t *nexti, const int64_t *fbase, int64_t *frame_cand,
                                                  int *bad) {
     __shared__ int32_t nx[kChainLds];
@@ -302,6 +306,10 @@ __global__ void __launch_bounds__(64) k_chain_lds(const int64_t *soff, int ns, c
     if (s >= ns) return;
     const int lane = threadIdx.x;
     const int nc = *ncand;
+    if (nc > cand_cap) {  // uniform: the selection overflowed its buffer
+        if (threadIdx.x == 0) atomicAdd(bad, 1);
+        return;
+    }
     if (lane == 0) {
         rng[0] = ns == 1 ? 0 : lower_bound_pos(cpos, nc, soff[s]);
         rng[1] = ns == 1 ? nc : lower_bound_pos(cpos, nc, soff[s + 1]);
@@ -486,6 +494,7 @@ __device__ __attribute__((always_inline)) inline void decode_one_frame(const uin
                                         int64_t fi, int channels, int stream_bps, int32_t *pcm, int blocksize,
                                         int *nvalid, int32_t *resbuf, const uint32_t *lds_words) {
     const int64_t ci = frame_cand[fi];
+    if (ci < 0) return;  // not on a valid chain (the host reports it)
     const int64_t fpos = cpos[ci];
     const int64_t fend_known = ends[ci];
     const int s = stream_of(soff, ns, fpos);
@@ -859,6 +868,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     if (fi >= nframes) return;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t ci = frame_cand[fi];
+    if (ci < 0) return;  // not on a valid chain (the host reports it)
     const int64_t fpos = cpos[ci], fend_known = ends[ci];
     const int s = stream_of(soff, ns, fpos);
     const int64_t send = soff[s + 1];
@@ -1229,6 +1239,7 @@ __global__ void __launch_bounds__(64) k_decode_frames_wave(const uint8_t *blob, 
     if (fi >= nframes) return;
     const int lane = threadIdx.x;
     const int64_t ci = frame_cand[fi];
+    if (ci < 0) return;  // not on a valid chain (the host reports it)
     const int64_t fpos = cpos[ci], fend = ends[ci];
     const int s = stream_of(soff, ns, fpos);
     const int64_t send = soff[s + 1];
@@ -1345,21 +1356,29 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     FRS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmp, it, flags, cpos, ncand, (int)blob_bytes, st));
     FRS_HIP(ctx->scan_tmp.ensure(tmp));
     FRS_HIP(hipcub::DeviceSelect::Flagged(ctx->scan_tmp.ptr, tmp, it, flags, cpos, ncand, (int)blob_bytes, st));
-    int hc = 0;
-    FRS_HIP(hipMemcpyAsync(&hc, ncand, sizeof(int), hipMemcpyDeviceToHost, st));
-    FRS_HIP(hipStreamSynchronize(st));
-    if ((size_t)hc > cand_cap) {
-        ctx->err = "too many frame sync candidates";
-        return FRS_E_CORRUPT;
+    const bool wave_span = max_frame < (int64_t)4096 * 256;  // x^(8m) table range
+    int hc = -1;  // candidate count on the host: only the fallback span kernels need it
+    if (!wave_span) {
+        FRS_HIP(hipMemcpyAsync(&hc, ncand, sizeof(int), hipMemcpyDeviceToHost, st));
+        FRS_HIP(hipStreamSynchronize(st));
+        if ((size_t)hc > cand_cap) {
+            ctx->err = "too many frame sync candidates";
+            return FRS_E_CORRUPT;
+        }
     }
     prof_end(ctx, "decode", ev);
-    if (hc > 0) {
+    // frames the chain does not reach keep -1 and are skipped by the decoders (the final count reports them)
+    FRS_HIP(hipMemsetAsync(dchain, 0xFF, sizeof(int64_t) * (size_t)frames, st));
+    if (frames > 0 && hc != 0) {
         prof_begin(ctx, "decode_span", &ev);
-        if (max_frame < (int64_t)4096 * 256) {  // x^(8m) table range
-            FRS_HIP(ctx->dec_next.ensure(sizeof(int32_t) * (size_t)hc + 64));
+        if (wave_span) {
+            FRS_HIP(ctx->dec_next.ensure(sizeof(int32_t) * cand_cap + 64));
             int32_t *nexti = ctx->dec_next.as<int32_t>();
-            k_span_crc_wave<<<hc, 64, 0, st>>>(blob_dev, dsoff, nstreams, cpos, ncand, max_frame, ends, nexti);
-            k_chain_lds<<<nstreams, 64, 0, st>>>(dsoff, nstreams, cpos, ncand, nexti, dfbase, dchain, bad);
+            const int64_t grid = std::min<int64_t>((int64_t)cand_cap, 2 * frames + 256);
+            k_span_crc_wave<<<(unsigned)grid, 64, 0, st>>>(blob_dev, dsoff, nstreams, cpos, ncand, (int)cand_cap,
+                                                           max_frame, ends, nexti);
+            k_chain_lds<<<nstreams, 64, 0, st>>>(dsoff, nstreams, cpos, ncand, (int)cand_cap, nexti, dfbase, dchain,
+                                                 bad);
         } else {
             k_span_crc<<<(hc + 63) / 64, 64, 0, st>>>(blob_dev, dsoff, nstreams, flags, cpos, ncand, max_frame, ends);
             k_chain<<<(nstreams + 63) / 64, 64, 0, st>>>(dsoff, nstreams, cpos, ncand, ends, dfbase, dchain, bad);
@@ -1382,6 +1401,10 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     FRS_HIP(hipMemcpyAsync(hv, ncand, sizeof(int) * 3, hipMemcpyDeviceToHost, st));
     FRS_HIP(hipStreamSynchronize(st));
     prof_collect(ctx);
+    if ((size_t)hv[0] > cand_cap) {
+        ctx->err = "too many frame sync candidates";
+        return FRS_E_CORRUPT;
+    }
     if (hv[2] != 0 || hv[1] != frames) {
         ctx->err = "decoded " + std::to_string(hv[1]) + " valid frames, expected " + std::to_string(frames) +
                    (hv[2] ? " (broken frame chain)" : "");

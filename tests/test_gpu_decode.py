@@ -52,3 +52,26 @@ def test_decode_matches_oracle(gpu_ctx, ablate, monkeypatch):
             got = pcm[int(np.sum(counts[:t])):int(np.sum(counts[:t + 1]))]
             assert np.array_equal(got, ref), (name, t)
     dctx.close()
+
+
+def test_decode_corrupt_streams_report_errors(gpu_ctx):
+    """Damaged data must end in FrsError (CRC-16 span check fails, chain broken, or no sync codes at all), never a
+    fault or a silent wrong decode; the context then still decodes good data (the decode path launches its span
+    and frame kernels before the host knows the candidate count, so the unchained frames are skipped on device)."""
+    from flac_raster_amd import _native
+    dctx = _native.Context(0)
+    band = _bands()[0][1][:256, :256].copy()
+    d = gpu_ctx.make_desc(256, 256, band.dtype, tile_h=128, tile_w=128, sample_rate=44100, bits_per_sample=16)
+    arena, off, mn, mx, bps = gpu_ctx.encode_tiles_host(band, d)
+    counts = [128 * 128] * 4
+    flipped = arena.copy()
+    flipped[off[1] + 200:off[1] + 260] ^= 0x5A  # inside tile 1's first frame
+    with pytest.raises(_native.FrsError):
+        dctx.decode_frames_host(flipped, off, counts, channels=1, bps=16)
+    with pytest.raises(_native.FrsError):  # no sync codes anywhere
+        dctx.decode_frames_host(np.zeros_like(arena), off, counts, channels=1, bps=16)
+    pcm = dctx.decode_frames_host(arena, off, counts, channels=1, bps=16)
+    for t in range(4):
+        ref = O.decode_frames(arena[off[t]:off[t + 1]].tobytes(), 1, 16, counts[t])
+        assert np.array_equal(pcm[t * counts[t]:(t + 1) * counts[t]], ref), t
+    dctx.close()
