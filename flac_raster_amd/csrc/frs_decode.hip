@@ -1336,9 +1336,17 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     int64_t *dsoff = ctx->dec_soff.as<int64_t>();
     int64_t *dfbase = dsoff + (nstreams + 1);
     int64_t *dchain = dfbase + (nstreams + 1);
-    FRS_HIP(hipMemcpyAsync(dsoff, stream_off, sizeof(int64_t) * (nstreams + 1), hipMemcpyHostToDevice, st));
-    FRS_HIP(hipMemcpyAsync(dfbase, fbase.data(), sizeof(int64_t) * (nstreams + 1), hipMemcpyHostToDevice, st));
-    FRS_HIP(hipMemcpyAsync(ctx->dec_poff.ptr, pcm_off, sizeof(int64_t) * (nstreams + 1), hipMemcpyHostToDevice, st));
+    // the per-call tables go through the context's pinned staging (DMA copies, no staged pageable transfers):
+    // [stream_off | fbase] -> dsoff/dfbase (contiguous on the device), pcm_off -> dec_poff; the result counters
+    // come back into the same staging after the tables
+    const size_t tab = sizeof(int64_t) * (size_t)(nstreams + 1);
+    FRS_HIP(ctx->pin.ensure(3 * tab + 64));
+    int64_t *htab = ctx->pin.at<int64_t>(0);
+    memcpy(htab, stream_off, tab);
+    memcpy(htab + (nstreams + 1), fbase.data(), tab);
+    memcpy(htab + 2 * (nstreams + 1), pcm_off, tab);
+    FRS_HIP(hipMemcpyAsync(dsoff, htab, 2 * tab, hipMemcpyHostToDevice, st));
+    FRS_HIP(hipMemcpyAsync(ctx->dec_poff.ptr, htab + 2 * (nstreams + 1), tab, hipMemcpyHostToDevice, st));
     FRS_HIP(hipMemsetAsync(ctx->dec_count.ptr, 0, sizeof(int) * 4, st));
     int *ncand = ctx->dec_count.as<int>();
     int *nvalid = ncand + 1;
@@ -1397,7 +1405,7 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
                                                                   nvalid);
         prof_end(ctx, "decode_frames", ev);
     }
-    int hv[3] = {0, 0, 0};
+    int *hv = ctx->pin.at<int>(3 * tab);
     FRS_HIP(hipMemcpyAsync(hv, ncand, sizeof(int) * 3, hipMemcpyDeviceToHost, st));
     FRS_HIP(hipStreamSynchronize(st));
     prof_collect(ctx);
