@@ -863,7 +863,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     __shared__ int32_t resbuf[kDecResMax];
     __shared__ uint32_t xout[kDecResMax / 2];  // restored samples as int16 pairs
     __shared__ PipeInfo info;
-    __shared__ uint16_t jt[6][kJumpN];  // producer's Rice-window jump tables (window + fixed points)
+    __shared__ __attribute__((aligned(16))) uint16_t jt[6][kJumpN];  // producer's Rice-window jump tables (window + fixed points)
     const int64_t fi = blockIdx.x;
     if (fi >= nframes) return;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1034,9 +1034,9 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
             }
             P = br.pos();
             const int k1 = kp + 1;
-            // Window step over kRiceWinBits = 1024 bits: lane j decodes the Rice codes that would start at bits
-            // P + j + 64q (q < kRiceWinQ, from big-endian stage words); the chain of actual code starts through them
-            // is resolved by pointer jumping over LDS tables (lane m lands on the m-th start in six reads, no
+            // Window step over kRiceWinBits = 1024 bits: lane j decodes the lengths of the Rice codes that would
+            // start at bits P + 16j + t (t < kRiceWinQ, from big-endian stage words); the chain of actual code starts
+            // through them is resolved by pointer jumping over LDS tables (lane m lands on the m-th start in six reads, no
             // per-code scalar loop); lane m then decodes the value of the code at that start and the window's residuals
             // leave in one contiguous LDS store.  A 1024-bit window holds ~64 codes (the lane
             // cap) of a 15-bit/sample frame: measured per tile 0.221 / 0.204 / 0.192 ms at 512 / 768 / 1024 bits.
@@ -1045,41 +1045,47 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                     bad = true;
                     break;
                 }
-                const uint32_t b = P + (uint32_t)lane, wi = b >> 5, sh = b & 31u;
-                uint32_t wv[2 * kRiceWinQ + 1];
-#pragma unroll
-                for (int m = 0; m < 2 * kRiceWinQ + 1; m++) wv[m] = stage[wi + m];
                 auto window64 = [&](uint32_t x0, uint32_t x1, uint32_t x2, uint32_t sft) -> uint64_t {
                     const uint32_t hi = sft ? __builtin_amdgcn_alignbit(x0, x1, 32u - sft) : x0;
                     const uint32_t lo = sft ? __builtin_amdgcn_alignbit(x1, x2, 32u - sft) : x1;
                     return ((uint64_t)hi << 32) | lo;
                 };
-                auto cand = [&](uint32_t x0, uint32_t x1, uint32_t x2) -> uint32_t {
-                    const uint64_t win = window64(x0, x1, x2, sh);
-                    const int tot = (win ? __builtin_clzll(win) : 64) + k1;
-                    return tot <= 64 ? (uint32_t)tot : 0xFFu;  // code length, or "long"
-                };
-                // code lengths of the candidates at P + lane + 64q packed as byte q (0xff: longer than 64 bits);
-                // the values are decoded after the walk, only at the chain's code starts
-                uint32_t lq[kRiceWinQ];
-#pragma unroll
-                for (int q = 0; q < kRiceWinQ; q++) lq[q] = cand(wv[2 * q], wv[2 * q + 1], wv[2 * q + 2]);
+                // lane j owns the kRiceWinQ consecutive candidates c = kRiceWinQ * j + t (bits P + c): their 64-bit
+                // windows all lie in four stage words, and the lane's jump-table entries are one contiguous run
+                // (16-byte LDS stores)
+                const uint32_t b = P + (uint32_t)(kRiceWinQ * lane), wi = b >> 5, sh = b & 31u;
+                const uint64_t wA = ((uint64_t)stage[wi] << 32) | stage[wi + 1];
+                const uint64_t wB = ((uint64_t)stage[wi + 2] << 32) | stage[wi + 3];
                 // chain by pointer jumping: jt[k][c] = the code start 2^k codes after candidate c (absorbing at a
-                // long code and past the window), so lane m finds the m-th code start in six dependent LDS reads
+                // long code and past the window), so lane m finds the m-th code start in six dependent LDS reads;
+                // the values are decoded after it, only at the chain's code starts
                 const int cap = left < 64 ? left : 64;
                 int jq[kRiceWinQ];
 #pragma unroll
-                for (int q = 0; q < kRiceWinQ; q++) {
-                    const int c = lane + 64 * q;
-                    jq[q] = lq[q] == 0xFFu ? c : c + (int)lq[q];
-                    jt[0][c] = (uint16_t)jq[q];
+                for (int t = 0; t < kRiceWinQ; t++) {
+                    const uint32_t s2 = sh + (uint32_t)t;  // < 64
+                    const uint64_t win = s2 ? (wA << s2) | (wB >> (64u - s2)) : wA;
+                    const int tot = (win ? __builtin_clzll(win) : 64) + k1;
+                    const int c = kRiceWinQ * lane + t;
+                    jq[t] = tot <= 64 ? c + tot : c;
                 }
+                auto store_run = [&](uint16_t *row) {  // jq -> row[kRiceWinQ * lane ...], 16 bytes at a time
+#pragma unroll
+                    for (int v = 0; v < kRiceWinQ / 8; v++) {
+                        uint4 u;
+                        u.x = (uint32_t)jq[8 * v] | ((uint32_t)jq[8 * v + 1] << 16);
+                        u.y = (uint32_t)jq[8 * v + 2] | ((uint32_t)jq[8 * v + 3] << 16);
+                        u.z = (uint32_t)jq[8 * v + 4] | ((uint32_t)jq[8 * v + 5] << 16);
+                        u.w = (uint32_t)jq[8 * v + 6] | ((uint32_t)jq[8 * v + 7] << 16);
+                        reinterpret_cast<uint4 *>(row + kRiceWinQ * lane)[v] = u;
+                    }
+                };
+                store_run(jt[0]);
 #pragma unroll
                 for (int k = 0; k < 5; k++) {
 #pragma unroll
                     for (int q = 0; q < kRiceWinQ; q++) jq[q] = jt[k][jq[q]];
-#pragma unroll
-                    for (int q = 0; q < kRiceWinQ; q++) jt[k + 1][lane + 64 * q] = (uint16_t)jq[q];
+                    store_run(jt[k + 1]);
                 }
                 int posv = 0;
 #pragma unroll
