@@ -29,7 +29,8 @@ DTYPE_CODES = {np.dtype(np.uint8): 1, np.dtype(np.uint16): 2, np.dtype(np.int16)
 EXPORTS = (
     "frs_abi_version", "frs_device_count", "frs_ctx_create", "frs_ctx_destroy", "frs_last_error",
     "frs_encode_arena_bound", "frs_encode_tiles_device", "frs_encode_tiles",
-    "frs_decode_frames_device", "frs_decode_frames", "frs_denormalize_device", "frs_denormalize",
+    "frs_decode_frames_device", "frs_decode_frames", "frs_decode_tiles_device", "frs_decode_tiles",
+    "frs_denormalize_device", "frs_denormalize",
     "frs_dev_malloc", "frs_dev_free", "frs_memcpy_h2d", "frs_memcpy_d2h", "frs_ctx_sync",
     "frs_synth_raster_device", "frs_ctx_stream", "frs_profile_enable", "frs_profile_avg_ms",
     "frs_profile_reset",
@@ -102,6 +103,11 @@ def load_library(path: Optional[os.PathLike] = None):
         L.frs_decode_frames_device.argtypes = dec_args
         L.frs_decode_frames.restype = i32
         L.frs_decode_frames.argtypes = dec_args
+        dect_args = [ctxp, vp, ip64, i32, i32, i32, i32, ip64, dp, dp, i32, vp]
+        L.frs_decode_tiles_device.restype = i32
+        L.frs_decode_tiles_device.argtypes = dect_args
+        L.frs_decode_tiles.restype = i32
+        L.frs_decode_tiles.argtypes = dect_args
         den_args = [ctxp, vp, i64, i32, ctypes.c_double, ctypes.c_double, i32, vp]
         L.frs_denormalize_device.restype = i32
         L.frs_denormalize_device.argtypes = den_args
@@ -298,6 +304,46 @@ class Context:
             self.handle, ctypes.c_void_p(blob.ptr), soff.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
             len(pcm_counts), channels, bps, blocksize, ctypes.c_void_p(pcm.ptr),
             poff.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        return poff
+
+    def decode_tiles_host(self, blob, stream_off: Sequence[int], pcm_counts: Sequence[int], channels: int, bps: int,
+                          data_min: Sequence[float], data_max: Sequence[float], dtype,
+                          blocksize: int = 4096) -> np.ndarray:
+        """Decode + de-normalise streams in one pass -> `dtype` [sum(pcm_counts), channels] (converter.py:241-282)."""
+        b = np.frombuffer(blob, dtype=np.uint8) if not isinstance(blob, np.ndarray) else blob
+        b = np.ascontiguousarray(b)
+        soff = np.ascontiguousarray(np.asarray(stream_off, dtype=np.int64))
+        poff = np.zeros(len(pcm_counts) + 1, dtype=np.int64)
+        poff[1:] = np.cumsum(np.asarray(pcm_counts, dtype=np.int64))
+        mn = np.ascontiguousarray(np.asarray(data_min, dtype=np.float64))
+        mx = np.ascontiguousarray(np.asarray(data_max, dtype=np.float64))
+        if len(mn) != len(pcm_counts) or len(mx) != len(pcm_counts) or len(soff) != len(pcm_counts) + 1:
+            raise ValueError("one stream offset pair and one data_min/data_max per stream")
+        out = np.empty((int(poff[-1]), channels), dtype=dtype)
+        dp = ctypes.POINTER(ctypes.c_double)
+        self._check(self.lib.frs_decode_tiles(
+            self.handle, _p(b), soff.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), len(pcm_counts), channels, bps,
+            blocksize, poff.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), mn.ctypes.data_as(dp),
+            mx.ctypes.data_as(dp), DTYPE_CODES[np.dtype(dtype)], _p(out)))
+        return out
+
+    def decode_tiles_device(self, blob: DeviceBuffer, stream_off: np.ndarray, pcm_counts: Sequence[int], channels: int,
+                            bps: int, data_min: Sequence[float], data_max: Sequence[float], dtype, out: DeviceBuffer,
+                            blocksize: int = 4096, blob_ptr: Optional[int] = None) -> np.ndarray:
+        """Device-resident fused decode into `out`; returns the sample offsets (pcm_off)."""
+        soff = np.ascontiguousarray(np.asarray(stream_off, dtype=np.int64))
+        poff = np.zeros(len(pcm_counts) + 1, dtype=np.int64)
+        poff[1:] = np.cumsum(np.asarray(pcm_counts, dtype=np.int64))
+        mn = np.ascontiguousarray(np.asarray(data_min, dtype=np.float64))
+        mx = np.ascontiguousarray(np.asarray(data_max, dtype=np.float64))
+        if int(poff[-1]) * channels * np.dtype(dtype).itemsize > out.nbytes:
+            raise ValueError("output buffer too small")
+        dp = ctypes.POINTER(ctypes.c_double)
+        self._check(self.lib.frs_decode_tiles_device(
+            self.handle, ctypes.c_void_p(blob.ptr if blob_ptr is None else blob_ptr),
+            soff.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), len(pcm_counts), channels, bps, blocksize,
+            poff.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), mn.ctypes.data_as(dp), mx.ctypes.data_as(dp),
+            DTYPE_CODES[np.dtype(dtype)], ctypes.c_void_p(out.ptr)))
         return poff
 
     def denormalize_host(self, pcm: np.ndarray, data_min: float, data_max: float, dtype, pcm_bps: int = 16) -> np.ndarray:

@@ -151,10 +151,11 @@ class RasterFLACConverter:
         if sm.bps not in (16, 32):
             raise ValueError("Only int16/int32 data type is supported")  # pyflac decoder.py check
         frames = np.frombuffer(buf, dtype=np.uint8)[sm.audio_offset:]
-        pcm = self.ctx.decode_frames_host(frames, [0, len(frames)], [W * H], channels=sm.channels, bps=sm.bps,
-                                          blocksize=sm.blocksize)
         dtype = np.dtype(md["dtype"])
-        out = self.ctx.denormalize_host(pcm, md["data_min"], md["data_max"], dtype, pcm_bps=sm.bps)
+        # FileDecoder + WAV round trip + _denormalize_from_audio in one GPU pass (converter.py:241-282)
+        out = self.ctx.decode_tiles_host(frames, [0, len(frames)], [W * H], channels=sm.channels, bps=sm.bps,
+                                         data_min=[md["data_min"]], data_max=[md["data_max"]], dtype=dtype,
+                                         blocksize=sm.blocksize)
         if count > 1:
             return np.ascontiguousarray(out.reshape(H, W, count).transpose(2, 0, 1))
         return out.reshape(1, H, W)

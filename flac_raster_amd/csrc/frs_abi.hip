@@ -118,7 +118,7 @@ void frs_ctx_destroy(frs_ctx *ctx) {
     frs::prof_collect(ctx);
     DevBuf *bufs[] = {&ctx->tiles, &ctx->norms, &ctx->analysis, &ctx->slots, &ctx->frame_bytes, &ctx->frame_off,
                       &ctx->scan_tmp, &ctx->window, &ctx->tile_sizes, &ctx->luts, &ctx->status, &ctx->frame_tile, &ctx->hdr_tab, &ctx->wave_tab, &ctx->raster_stage, &ctx->arena_stage, &ctx->host_pack,
-                      &ctx->dec_cand, &ctx->dec_count, &ctx->dec_blob, &ctx->dec_pcm, &ctx->dec_soff, &ctx->dec_poff, &ctx->dec_next};
+                      &ctx->dec_cand, &ctx->dec_count, &ctx->dec_pcm, &ctx->dec_soff, &ctx->dec_next, &ctx->dec_status};
     for (DevBuf *b : bufs) b->release();
     ctx->pin.release();
     hipStreamDestroy(ctx->stream);
@@ -191,29 +191,49 @@ int frs_encode_tiles(frs_ctx *ctx, const frs_encode_desc *desc, const void *rast
     return FRS_OK;
 }
 
-int frs_decode_frames_device(frs_ctx *ctx, const uint8_t *blob_dev, const int64_t *stream_off, int32_t nstreams,
-                             int32_t channels, int32_t bps, int32_t blocksize, int32_t *pcm_dev, const int64_t *pcm_off) {
-    if (!ctx) return FRS_E_ARG;
-    if (!blob_dev || !stream_off || !pcm_dev || !pcm_off || nstreams < 0 || channels < 1 || channels > 8 ||
-        blocksize < 16 || blocksize > 65535) {
+}  // extern "C"
+
+// shared argument checks and stream rebasing of the decode entry points: only [stream_off[0],
+// stream_off[nstreams]) is scanned, so a tile query inside a large arena touches just its own bytes
+static int decode_entry(frs_ctx *ctx, const uint8_t *blob_dev, const int64_t *stream_off, int32_t nstreams,
+                        int32_t channels, int32_t bps, int32_t blocksize, int32_t *pcm_dev, const int64_t *pcm_off,
+                        const double *dmin, const double *dmax, int32_t out_dtype, void *out_dev) {
+    if (!blob_dev || !stream_off || !pcm_off || nstreams < 0 || channels < 1 || channels > 8 || blocksize < 16 ||
+        blocksize > 65535 || bps < 4 || bps > 32) {
         ctx->err = "bad decode arguments";
+        return FRS_E_ARG;
+    }
+    if (out_dev && (!dmin || !dmax || frs::dtype_size(out_dtype) == 0)) {
+        ctx->err = "bad decode arguments (data_min/data_max/out dtype)";
+        return FRS_E_ARG;
+    }
+    if (!out_dev && !pcm_dev) {
+        ctx->err = "bad decode arguments (no output)";
         return FRS_E_ARG;
     }
     FRS_HIP(hipSetDevice(ctx->device));
     if (nstreams == 0) return FRS_OK;
-    // only [stream_off[0], stream_off[nstreams]) is scanned: a tile query inside a large arena touches
-    // just its own bytes
     const int64_t base = stream_off[0];
     std::vector<int64_t> rel(nstreams + 1);
     for (int s = 0; s <= nstreams; s++) {
         rel[s] = stream_off[s] - base;
-        if (s && rel[s] < rel[s - 1]) {
-            ctx->err = "stream offsets must be non-decreasing";
+        if (s && (rel[s] < rel[s - 1] || pcm_off[s] < pcm_off[s - 1])) {
+            ctx->err = "stream and sample offsets must be non-decreasing";
             return FRS_E_ARG;
         }
     }
     return frs::decode_job(ctx, blob_dev + base, rel[nstreams], rel.data(), nstreams, channels, bps, blocksize,
-                           pcm_dev, pcm_off);
+                           pcm_dev, pcm_off, dmin, dmax, out_dtype, out_dev);
+}
+
+extern "C" {
+
+int frs_decode_frames_device(frs_ctx *ctx, const uint8_t *blob_dev, const int64_t *stream_off, int32_t nstreams,
+                             int32_t channels, int32_t bps, int32_t blocksize, int32_t *pcm_dev, const int64_t *pcm_off) {
+    if (!ctx) return FRS_E_ARG;
+    if (!pcm_dev) { ctx->err = "bad decode arguments"; return FRS_E_ARG; }
+    return decode_entry(ctx, blob_dev, stream_off, nstreams, channels, bps, blocksize, pcm_dev, pcm_off, nullptr,
+                        nullptr, 0, nullptr);
 }
 
 int frs_decode_frames(frs_ctx *ctx, const uint8_t *blob_host, const int64_t *stream_off, int32_t nstreams,
@@ -224,12 +244,51 @@ int frs_decode_frames(frs_ctx *ctx, const uint8_t *blob_host, const int64_t *str
     const int64_t nbytes = nstreams ? stream_off[nstreams] : 0;
     const int64_t nsamp = nstreams ? pcm_off[nstreams] : 0;
     FRS_HIP(ctx->raster_stage.ensure((size_t)nbytes + 16));
-    FRS_HIP(ctx->dec_pcm.ensure((size_t)nsamp * channels * 4 + 16));
+    FRS_HIP(ctx->arena_stage.ensure((size_t)nsamp * channels * 4 + 16));
     FRS_HIP(hipMemcpyAsync(ctx->raster_stage.ptr, blob_host, (size_t)nbytes, hipMemcpyHostToDevice, ctx->stream));
     int rc = frs_decode_frames_device(ctx, ctx->raster_stage.as<uint8_t>(), stream_off, nstreams, channels, bps,
-                                      blocksize, ctx->dec_pcm.as<int32_t>(), pcm_off);
+                                      blocksize, ctx->arena_stage.as<int32_t>(), pcm_off);
     if (rc) return rc;
-    FRS_HIP(hipMemcpyAsync(pcm_host, ctx->dec_pcm.ptr, (size_t)nsamp * channels * 4, hipMemcpyDeviceToHost, ctx->stream));
+    FRS_HIP(hipMemcpyAsync(pcm_host, ctx->arena_stage.ptr, (size_t)nsamp * channels * 4, hipMemcpyDeviceToHost, ctx->stream));
+    FRS_HIP(hipStreamSynchronize(ctx->stream));
+    return FRS_OK;
+}
+
+int frs_decode_tiles_device(frs_ctx *ctx, const uint8_t *blob_dev, const int64_t *stream_off, int32_t nstreams,
+                            int32_t channels, int32_t bps, int32_t blocksize, const int64_t *pcm_off,
+                            const double *data_min, const double *data_max, int32_t out_dtype, void *out_dev) {
+    if (!ctx) return FRS_E_ARG;
+    if (!out_dev) { ctx->err = "bad decode arguments (no output)"; return FRS_E_ARG; }
+    return decode_entry(ctx, blob_dev, stream_off, nstreams, channels, bps, blocksize, nullptr, pcm_off, data_min,
+                        data_max, out_dtype, out_dev);
+}
+
+int frs_decode_tiles(frs_ctx *ctx, const uint8_t *blob_host, const int64_t *stream_off, int32_t nstreams,
+                     int32_t channels, int32_t bps, int32_t blocksize, const int64_t *pcm_off, const double *data_min,
+                     const double *data_max, int32_t out_dtype, void *out_host) {
+    if (!ctx) return FRS_E_ARG;
+    const int es = frs::dtype_size(out_dtype);
+    if (!blob_host || !stream_off || !out_host || !pcm_off || nstreams < 0 || es == 0 || channels < 1) {
+        ctx->err = "bad decode arguments";
+        return FRS_E_ARG;
+    }
+    FRS_HIP(hipSetDevice(ctx->device));
+    if (nstreams == 0) return FRS_OK;
+    const int64_t nbytes = stream_off[nstreams] - stream_off[0];
+    const int64_t nout = (pcm_off[nstreams] - pcm_off[0]) * channels;
+    FRS_HIP(ctx->raster_stage.ensure((size_t)nbytes + 16));
+    FRS_HIP(ctx->arena_stage.ensure((size_t)nout * es + 16));
+    FRS_HIP(hipMemcpyAsync(ctx->raster_stage.ptr, blob_host + stream_off[0], (size_t)nbytes, hipMemcpyHostToDevice,
+                           ctx->stream));
+    std::vector<int64_t> rel(nstreams + 1);
+    for (int s = 0; s <= nstreams; s++) rel[s] = stream_off[s] - stream_off[0];
+    // the device output starts at sample pcm_off[0] of the host array
+    uint8_t *dout = ctx->arena_stage.as<uint8_t>() - pcm_off[0] * channels * es;
+    int rc = decode_entry(ctx, ctx->raster_stage.as<uint8_t>(), rel.data(), nstreams, channels, bps, blocksize, nullptr,
+                          pcm_off, data_min, data_max, out_dtype, dout);
+    if (rc) return rc;
+    FRS_HIP(hipMemcpyAsync(static_cast<uint8_t *>(out_host) + pcm_off[0] * channels * es, ctx->arena_stage.ptr,
+                           (size_t)nout * es, hipMemcpyDeviceToHost, ctx->stream));
     FRS_HIP(hipStreamSynchronize(ctx->stream));
     return FRS_OK;
 }

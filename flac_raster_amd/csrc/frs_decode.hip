@@ -5,15 +5,20 @@
 // converter.py:88-110 (_denormalize_from_audio), as used by cli.py:1022-1023 (extract-streaming).
 //
 // Frames carry no size field and STREAMINFO min/max framesize are 0 in these files, so frames are
-// located in parallel: k_flag_sync marks every byte that starts a sync code with a parseable,
-// CRC-8-correct header; the marks are compacted into sorted candidates; k_span_crc finds for each
+// located in parallel: k_sync_select finds every byte that starts a sync code with a parseable,
+// CRC-8-correct header and compacts them, in one pass (block counts + decoupled look-back), into the
+// sorted candidate list (bounded: overflow is counted, never written); k_span_crc_wave finds for each
 // candidate the first later candidate (or stream end) whose preceding two bytes are the CRC-16 of the
-// span; k_chain follows those spans from each stream's first byte (so false syncs inside frame data are
-// never used); k_decode_frames decodes the true frames (one lane per frame, all channels) and checks
-// that the subframes end exactly at the CRC footer.
-#include <hipcub/hipcub.hpp>
+// span; k_chain_lds follows those spans from each stream's first byte (so false syncs inside frame data
+// are never used); the frame decoders decode the true frames and check that the subframes end exactly at
+// the CRC footer.  Positions are 64-bit throughout (a C4 arena is 3.1 GB); candidate indices are int32
+// and the candidate buffer is capped below 2^31.
+#include <string.h>
 
+#include <algorithm>
+#include <string>
 #include <type_traits>
+#include <vector>
 
 #include "frs_internal.h"
 
@@ -90,43 +95,168 @@ __device__ FrameHdr parse_header(const uint8_t *blob, int64_t p, int64_t end, in
     return h;
 }
 
-// flags[p] = 1 where a sync code starts a valid header
-__global__ void k_flag_sync(const uint8_t *blob, int64_t nbytes, const int64_t *soff, int ns, int channels,
-                            int stream_bps, uint8_t *flags) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= nbytes) return;
-    uint8_t f = 0;
-    if (blob[p] == 0xFF && p + 1 < nbytes && (blob[p + 1] & 0xFE) == 0xF8) {
-        const int s = stream_of(soff, ns, p);
-        f = parse_header(blob, p, soff[s + 1], channels, stream_bps).ok ? 1 : 0;
+// ---------------------------------------------------------------------------------- candidate selection
+// One pass over the blob: a block takes 4096 bytes (16 per thread, one 16-byte load), flags the bytes that
+// start a sync code with a parseable CRC-8-correct header, and writes their positions, in order, at its
+// exclusive prefix -- found by decoupled look-back over the blocks' published counts.  Blocks take their
+// ordinal from a ticket (the block that draws the last ticket re-arms the counter for the next call), so a
+// predecessor is always resident or done.  Status word: [63:40] call epoch, [39:38] flag, [37:0] count;
+// words of another epoch read as "not published", so the buffer is never cleared between calls.
+constexpr int kSelThreads = 256, kSelBytes = 4096;
+constexpr uint64_t kSelAgg = 1ull << 38, kSelIncl = 2ull << 38, kSelVal = (1ull << 38) - 1;
+
+__global__ void __launch_bounds__(kSelThreads) k_sync_select(const uint8_t *blob, int64_t nbytes, const int64_t *soff,
+                                                           int ns, int channels, int stream_bps, uint64_t *status,
+                                                           unsigned long long *ticket, uint32_t epoch, int64_t nblocks,
+                                                           int64_t *cpos, int64_t cap, int *counts) {
+    __shared__ int64_t s_ord, s_base;
+    __shared__ int s_wsum[kSelThreads / 64];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (t == 0) {
+        const int64_t o = (int64_t)atomicAdd(ticket, 1ull);
+        if (o == nblocks - 1) atomicExch(ticket, 0ull);  // every ticket of this launch is drawn: re-arm
+        s_ord = o;
     }
-    flags[p] = f;
+    __syncthreads();
+    const int64_t ord = s_ord;
+    // aligned view: byte q of `base` is blob[q - lead]; a 16-byte line holding a blob byte is mapped
+    const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
+    const uint8_t *base = blob - lead;
+    const int64_t q0 = ord * kSelBytes + 16 * t, qend = nbytes + lead;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (q0 < qend) v = *reinterpret_cast<const uint4 *>(base + q0);
+    // the byte after this thread's 16 (the next lane's first byte; the wave's last lane loads it)
+    uint32_t nxt = (uint32_t)__shfl_down((int)(v.x & 0xFF), 1);
+    if (lane == 63) nxt = (q0 + 16 < qend) ? base[q0 + 16] : 0u;
+    uint32_t mask = 0;
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t x = w[k];
+        if (((~x) - 0x01010101u) & x & 0x80808080u) {  // some byte is 0xFF
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t b0 = (x >> (8 * j)) & 0xFF;
+                const uint32_t b1 = j < 3 ? (x >> (8 * j + 8)) & 0xFF : (k < 3 ? w[k + 1] & 0xFF : nxt);
+                const int64_t p = q0 + 4 * k + j - lead;
+                if (b0 == 0xFF && (b1 & 0xFE) == 0xF8 && p >= 0 && p + 1 < nbytes) {
+                    const int s = stream_of(soff, ns, p);
+                    if (parse_header(blob, p, soff[s + 1], channels, stream_bps).ok) mask |= 1u << (4 * k + j);
+                }
+            }
+        }
+    }
+    const int cnt = __builtin_popcount(mask);
+    int x = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_wsum[wv] = x;
+    __syncthreads();
+    int wbase = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kSelThreads / 64; k++) {
+        const int sv = s_wsum[k];
+        wbase += k < wv ? sv : 0;
+        tot += sv;
+    }
+    if (t == 0) {
+        const uint64_t tag = (uint64_t)epoch << 40;
+        int64_t excl = 0;
+        if (ord == 0) {
+            __hip_atomic_store(&status[0], tag | kSelIncl | (uint64_t)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            counts[1] = 0;  // nvalid, bad: zeroed here (the later kernels of this call run after this one)
+            counts[2] = 0;
+        } else {
+            __hip_atomic_store(&status[ord], tag | kSelAgg | (uint64_t)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            for (int64_t j = ord - 1;;) {
+                const uint64_t sv = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((sv >> 40) != epoch || !(sv & (kSelAgg | kSelIncl))) {
+                    __builtin_amdgcn_s_sleep(2);
+                    continue;
+                }
+                excl += (int64_t)(sv & kSelVal);
+                if (sv & kSelIncl) break;
+                j--;
+            }
+            __hip_atomic_store(&status[ord], tag | kSelIncl | (uint64_t)(excl + tot), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (ord == nblocks - 1) counts[0] = (int)min<int64_t>(excl + tot, (int64_t)0x7FFFFFFF);
+        s_base = excl;
+    }
+    __syncthreads();
+    int64_t idx = s_base + wbase + x - cnt;
+    while (mask) {  // positions in increasing order; past the cap only counted
+        const int j = __builtin_ctz(mask);
+        mask &= mask - 1;
+        if (idx < cap) cpos[idx] = q0 + j - lead;
+        idx++;
+    }
 }
 
-// For candidate i find the first later position e (a candidate start or the stream end) such that the
-// CRC-16 of [pos_i, e-2) equals the two bytes before e.  ends[i] = e or -1.
-__global__ void k_span_crc(const uint8_t *blob, const int64_t *soff, int ns, const uint8_t *flags,
-                           const int64_t *cpos, const int *ncand, int64_t max_frame, int64_t *ends) {
+// Fused de-normalisation of decoded samples (converter.py:88-110 after pyflac + soundfile's PCM_16 WAV round
+// trip, sonos-pyflac.txt:1629): v = float32(pcm16 / 32768); out = rint(((v + 1) / 2) * f32(max - min) + f32(min))
+// in fp32 without contraction, cast to the raster dtype; float dtypes get v itself.
+struct DecOut {
+    void *out;         // nullptr: the decoders write int32 PCM
+    const float2 *dn;  // per stream: (float32(data_max - data_min), float32(data_min))
+    int dtype;         // enum frs_dtype of out
+    int shift;         // 16 for 32-bit streams (libsndfile int -> short keeps the high half), else 0
+};
+
+__device__ inline void dn_store(const DecOut &o, int64_t i, int32_t pcm, float2 p) {
+    const float v = (float)(pcm >> o.shift) * (1.0f / 32768.0f);
+    if (o.dtype == FRS_DT_F32) { static_cast<float *>(o.out)[i] = v; return; }
+    if (o.dtype == FRS_DT_F64) { static_cast<double *>(o.out)[i] = (double)v; return; }
+    float a = __fadd_rn(v, 1.0f);
+    a = __fdiv_rn(a, 2.0f);
+    a = __fmul_rn(a, p.x);
+    a = __fadd_rn(a, p.y);
+    const int64_t r = (int64_t)rintf(a);
+    switch (o.dtype) {
+    case FRS_DT_U8: static_cast<uint8_t *>(o.out)[i] = (uint8_t)r; break;
+    case FRS_DT_U16: static_cast<uint16_t *>(o.out)[i] = (uint16_t)r; break;
+    case FRS_DT_I16: static_cast<int16_t *>(o.out)[i] = (int16_t)r; break;
+    case FRS_DT_I32: static_cast<int32_t *>(o.out)[i] = (int32_t)r; break;
+    default: static_cast<uint32_t *>(o.out)[i] = (uint32_t)r; break;
+    }
+}
+
+// Span check for frames too large for the wave kernel's tables (max frame >= 1 MiB: many channels of
+// 32-bit samples), one thread per candidate: the CRC-16 runs incrementally over the bytes from the
+// candidate, compared at every later candidate start (and the stream end).  Same outputs as
+// k_span_crc_wave: ends[i] = e or -1, nexti[i] = candidate index at e, -2 at the stream end.
+__global__ void k_span_crc(const uint8_t *blob, const int64_t *soff, int ns, const int64_t *cpos, const int *ncand,
+                           int cand_cap, int64_t max_frame, int64_t *ends, int32_t *nexti) {
+    const int nc = *ncand;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= *ncand) return;
+    if (nc > cand_cap || i >= nc) return;
     const int64_t p = cpos[i];
     const int s = stream_of(soff, ns, p);
     const int64_t send = soff[s + 1];
     const int64_t lim = min(send, p + max_frame);
-    uint32_t crc = 0;
-    int64_t e = -1;
-    for (int64_t b = p; b + 2 <= lim; b++) {
-        // crc covers [p, b)
-        if (b > p + 4 && (b + 2 == send || flags[b + 2])) {
-            const uint32_t got = ((uint32_t)blob[b] << 8) | blob[b + 1];
-            if (crc == got) {
-                e = b + 2;
+    uint32_t crc = 0;  // covers [p, b)
+    int64_t b = p, result = -1;
+    int32_t rnext = -1;
+    for (int j = i + 1;; j++) {
+        int64_t e = j < nc ? cpos[j] : send;
+        if (e > send) e = send;
+        if (e > lim) break;
+        if (e >= p + 7) {
+            for (; b < e - 2; b++) crc = ((crc << 8) & 0xFFFFu) ^ d_crc16[((crc >> 8) ^ blob[b]) & 0xFF];
+            if (crc == (((uint32_t)blob[e - 2] << 8) | blob[e - 1])) {
+                result = e;
+                rnext = (j < nc && cpos[j] < send) ? j : -2;
                 break;
             }
         }
-        crc = ((crc << 8) & 0xFFFFu) ^ d_crc16[((crc >> 8) ^ blob[b]) & 0xFF];
+        if (e >= send) break;
     }
-    ends[i] = e;
+    ends[i] = result;
+    nexti[i] = rnext;
 }
 
 
@@ -252,40 +382,11 @@ __global__ void __launch_bounds__(64) k_span_crc_wave(const uint8_t *blob, const
     }
 }
 
-__device__ inline int find_pos(const int64_t *cpos, int n, int64_t p) {
-    int lo = 0, hi = n - 1;
-    while (lo <= hi) {
-        const int mid = (lo + hi) >> 1;
-        if (cpos[mid] == p) return mid;
-        if (cpos[mid] < p) lo = mid + 1;
-        else hi = mid - 1;
-    }
-    return -1;
-}
-
-// Follow the frame chain of each stream from its first byte: frame k of stream s -> true[fbase[s]+k].
-__global__ void k_chain(const int64_t *soff, int ns, const int64_t *cpos, const int *ncand, const int64_t *ends,
-                        const int64_t *fbase, int64_t *frame_cand, int *bad) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= ns) return;
-    const int nc = *ncand;
-    int64_t cur = soff[s];
-    const int64_t nf = fbase[s + 1] - fbase[s];
-    for (int64_t k = 0; k < nf; k++) {
-        const int idx = find_pos(cpos, nc, cur);
-        if (idx < 0 || ends[idx] < 0) {
-            atomicAdd(bad, 1);
-            return;
-        }
-        frame_cand[fbase[s] + k] = idx;
-        cur = ends[idx];
-    }
-    if (cur != soff[s + 1]) atomicAdd(bad, 1);
-}
-
-// k_chain with the span links in LDS: one work-group per stream loads the stream's candidate -> next-candidate
-// links (k_span_crc_wave's nexti) and lane 0 walks them, one LDS read per frame instead of a binary search of
-// global memory per frame.  Streams with more candidates than the LDS table take the global walk.
+// Frame chain of each stream from its first byte: one work-group per stream loads the stream's candidate ->
+// next-candidate links (the span kernels' nexti) into LDS and lane 0 walks them, one LDS read per frame (streams
+// with more candidates than the LDS table walk global memory).  frame_cand[fbase[s] + k] = candidate of frame k,
+// written only once that candidate's CRC span is verified (its link is not -1); frames the walk does not reach
+// get -1 and are skipped by the decoders; any break is counted in *bad.
 constexpr int kChainLds = 4096;
 __device__ inline int lower_bound_pos(const int64_t *cpos, int n, int64_t p) {
     int lo = 0, hi = n;
@@ -306,8 +407,10 @@ __global__ void __launch_bounds__(64) k_chain_lds(const int64_t *soff, int ns, c
     if (s >= ns) return;
     const int lane = threadIdx.x;
     const int nc = *ncand;
-    if (nc > cand_cap) {  // uniform: the selection overflowed its buffer
-        if (threadIdx.x == 0) atomicAdd(bad, 1);
+    const int64_t fb = fbase[s], nf = fbase[s + 1] - fb;
+    if (nc > cand_cap) {  // uniform: the selection overflowed its buffer (the host reports it)
+        for (int64_t k = lane; k < nf; k += 64) frame_cand[fb + k] = -1;
+        if (lane == 0) atomicAdd(bad, 1);
         return;
     }
     if (lane == 0) {
@@ -321,25 +424,31 @@ __global__ void __launch_bounds__(64) k_chain_lds(const int64_t *soff, int ns, c
         for (int k = lane; k < c1 - c0; k += 64) nx[k] = nexti[c0 + k];
     __syncthreads();
     if (lane != 0) return;
-    const int64_t nf = fbase[s + 1] - fbase[s];
-    if (c0 >= c1 || cpos[c0] != soff[s]) {
-        atomicAdd(bad, 1);
-        return;
-    }
+    bool ok = c0 < c1 && cpos[c0] == soff[s];
+    int64_t k = 0;
     int idx = c0;
-    for (int64_t k = 0; k < nf; k++) {
-        frame_cand[fbase[s] + k] = idx;
-        const int n = in_lds ? nx[idx - c0] : nexti[idx];
-        if (k + 1 < nf) {
-            if (n < 0) {
-                atomicAdd(bad, 1);
-                return;
+    if (ok) {
+        for (; k < nf; k++) {
+            const int n = in_lds ? nx[idx - c0] : nexti[idx];
+            if (n == -1) {  // frame k failed its CRC span: not handed to the decoders
+                ok = false;
+                break;
             }
-            idx = n;
-        } else if (n != -2) {
-            atomicAdd(bad, 1);
+            frame_cand[fb + k] = idx;
+            if (k + 1 < nf) {
+                if (n < 0) {  // the stream ends before its last frame
+                    ok = false;
+                    k++;
+                    break;
+                }
+                idx = n;
+            } else if (n != -2) {
+                ok = false;  // bytes after the last frame
+            }
         }
     }
+    for (; k < nf; k++) frame_cand[fb + k] = -1;
+    if (!ok) atomicAdd(bad, 1);
 }
 
 constexpr int kDecResMax = 4096;  // residual buffer (LDS) of the fast subframe path
@@ -492,11 +601,13 @@ __device__ __attribute__((always_inline)) inline void decode_one_frame(const uin
                                         const int64_t *soff, int ns, const int64_t *poff, const int64_t *cpos,
                                         const int64_t *ends, const int64_t *fbase, const int64_t *frame_cand,
                                         int64_t fi, int channels, int stream_bps, int32_t *pcm, int blocksize,
-                                        int *nvalid, int32_t *resbuf, const uint32_t *lds_words) {
+                                        int *nvalid, int32_t *resbuf, const uint32_t *lds_words,
+                                        int32_t *outb_override = nullptr) {
     const int64_t ci = frame_cand[fi];
     if (ci < 0) return;  // not on a valid chain (the host reports it)
     const int64_t fpos = cpos[ci];
     const int64_t fend_known = ends[ci];
+    if (fend_known < 0) return;  // no verified CRC span
     const int s = stream_of(soff, ns, fpos);
     const int64_t send = soff[s + 1];
     const FrameHdr cd = parse_header(blob, fpos, send, channels, stream_bps);
@@ -504,7 +615,8 @@ __device__ __attribute__((always_inline)) inline void decode_one_frame(const uin
     const int64_t kk = fi - fbase[s];
     const int64_t first = kk * blocksize;
     if (!cd.ok || cd.frame_no != kk || cd.bs > blocksize || first + cd.bs > nsamp) return;
-    int32_t *outb = pcm + (poff[s] + first) * channels;
+    // frame-local output (an LDS buffer of the fused decode) or the frame's place in the PCM array
+    int32_t *outb = outb_override ? outb_override : pcm + (poff[s] + first) * channels;
     BitReader br;  // bits_base[k] = blob[k + bits_shift] (LDS stage or the blob itself)
     br.init(bits_base, fpos + cd.hdr_len - bits_shift, fend_known - bits_shift);
     const int nch = channels;
@@ -728,17 +840,6 @@ __device__ __attribute__((always_inline)) inline void decode_one_frame(const uin
 }
 
 
-__global__ void __launch_bounds__(64) k_decode_frames(const uint8_t *blob, const int64_t *soff, int ns,
-                                                     const int64_t *poff, const int64_t *cpos, const int64_t *ends,
-                                                     const int64_t *fbase, const int64_t *frame_cand, int64_t nframes,
-                                                     int channels, int stream_bps, int32_t *pcm, int blocksize,
-                                                     int *nvalid) {
-    const int64_t fi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (fi >= nframes) return;
-    decode_one_frame(blob, blob, 0, soff, ns, poff, cpos, ends, fbase, frame_cand, fi, channels, stream_bps, pcm,
-                     blocksize, nvalid, nullptr, nullptr);
-}
-
 // ------------------------------------------------------------------ wave-uniform (scalar-unit) frame decoder
 // A subframe's Rice codes are a sequential bit walk and its LPC restore a nonlinear recurrence, so one frame is
 // serial work.  It runs here on the scalar unit: every value is wave-uniform (SGPRs: s_flbit_i32_b64,
@@ -858,17 +959,28 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                                                            const int64_t *poff, const int64_t *cpos,
                                                            const int64_t *ends, const int64_t *fbase,
                                                            const int64_t *frame_cand, int64_t nframes, int channels,
-                                                           int stream_bps, int32_t *pcm, int blocksize, int *nvalid) {
+                                                           int stream_bps, int32_t *pcm, int blocksize, int *nvalid,
+                                                           DecOut dout) {
     __shared__ uint32_t stage[kDecStageWords + 2 * kRiceWinQ + 4];  // + the window step's look-ahead words
     __shared__ int32_t resbuf[kDecResMax];
-    __shared__ uint32_t xout[kDecResMax / 2];  // restored samples as int16 pairs
     __shared__ PipeInfo info;
-    __shared__ __attribute__((aligned(16))) uint16_t jt[6][kJumpN];  // producer's Rice-window jump tables (window + fixed points)
+    // restored samples as int16 pairs + the producer's Rice-window jump tables (window + fixed points); a frame
+    // that falls back to the one-lane decoder under a fused decode is decoded into `fb` instead (same bytes)
+    union PipeU {
+        struct {
+            uint32_t xout[kDecResMax / 2];
+            uint16_t jt[6][kJumpN];
+        } p;
+        int32_t fb[kDecResMax];
+    };
+    __shared__ __attribute__((aligned(16))) PipeU pu;
+    uint32_t *xout = pu.p.xout;
+    uint16_t(*jt)[kJumpN] = pu.p.jt;
     const int64_t fi = blockIdx.x;
     if (fi >= nframes) return;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int64_t ci = frame_cand[fi];
-    if (ci < 0) return;  // not on a valid chain (the host reports it)
+    if (ci < 0 || ends[ci] < 0) return;  // not on a verified chain (the host reports it)
     const int64_t fpos = cpos[ci], fend_known = ends[ci];
     const int s = stream_of(soff, ns, fpos);
     const int64_t send = soff[s + 1];
@@ -887,7 +999,21 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     const int64_t nsamp = poff[s + 1] - poff[s];
     const int64_t kk = fi - fbase[s];
     const int64_t first = kk * blocksize;
-    int32_t *out = pcm + (poff[s] + first);
+    const int64_t obase = poff[s] + first;  // mono: sample i of the frame is element obase + i
+    const bool fused = dout.out != nullptr;
+    const float2 dnp = fused ? dout.dn[s] : make_float2(0.f, 0.f);
+    auto put = [&](int i, int32_t v) {
+        if (fused) dn_store(dout, obase + i, v, dnp);
+        else pcm[obase + i] = v;
+    };
+    // after a one-lane fallback decode into pu.fb (fused decodes): the wave de-normalises the frame out of LDS
+    auto flush_fb = [&]() {
+        if (!fused) return;
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+        const int n = (int)min<int64_t>(blocksize, nsamp - first);
+        for (int i = lane; i < n; i += 64) dn_store(dout, obase + i, pu.fb[i], dnp);
+    };
     volatile PipeInfo *vi = &info;
     if (wave == 0) {
         // ================= producer: parse + Rice decode (wave-uniform, scalar unit)
@@ -902,7 +1028,8 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
             finish(kPipeFallback, 0);
             if (lane == 0)
                 decode_one_frame(blob, blob, 0, soff, ns, poff, cpos, ends, fbase, frame_cand, fi, channels,
-                                 stream_bps, pcm, blocksize, nvalid, resbuf, nullptr);
+                                 stream_bps, pcm, blocksize, nvalid, resbuf, nullptr, fused ? pu.fb : nullptr);
+            flush_fb();
             return;
         }
         const FrameHdr cd = parse_header(blob, fpos, send, channels, stream_bps);
@@ -930,13 +1057,15 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
             __builtin_amdgcn_wave_barrier();
             if (lane == 0)
                 decode_one_frame(blob, reinterpret_cast<const uint8_t *>(stage), wb * 4, soff, ns, poff, cpos, ends,
-                                 fbase, frame_cand, fi, channels, stream_bps, pcm, blocksize, nvalid, resbuf, stage);
+                                 fbase, frame_cand, fi, channels, stream_bps, pcm, blocksize, nvalid, resbuf, stage,
+                                 fused ? pu.fb : nullptr);
+            flush_fb();
         };
         if (cd.bps > 16 || sbps <= 0) { fallback(); return; }
         auto end_ok = [&]() { return (int64_t)((br.pos() + 7) >> 3) + 4 * wb + 2 == fend_known; };
         if (t == 0) {  // CONSTANT
             const int32_t v = br.sbits(sbps);
-            for (int i = lane; i < bs; i += 64) out[i] = (int32_t)((uint32_t)v << w);
+            for (int i = lane; i < bs; i += 64) put(i, (int32_t)((uint32_t)v << w));
             const int ok = end_ok();
             if (ok && lane == 0) atomicAdd(nvalid, 1);
             finish(kPipeDone, ok);
@@ -949,7 +1078,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                 vo = lane == (i & 63) ? ((uint32_t)x << w) : vo;
                 if ((i & 63) == 63 || i == bs - 1) {
                     const int b0 = i & ~63;
-                    if (b0 + lane <= i) out[b0 + lane] = (int32_t)vo;
+                    if (b0 + lane <= i) put(b0 + lane, (int32_t)vo);
                 }
             }
             const int ok = end_ok();
@@ -1227,25 +1356,27 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     __builtin_amdgcn_wave_barrier();
     if (failed || !info.valid) return;
     const int16_t *x16 = reinterpret_cast<const int16_t *>(xout);
-    for (int i = lane; i < bs; i += 64) out[i] = (int32_t)((uint32_t)(int32_t)x16[i] << w);
+    for (int i = lane; i < bs; i += 64) put(i, (int32_t)((uint32_t)(int32_t)x16[i] << w));
     if (lane == 0) atomicAdd(nvalid, 1);
 }
 
 // One wave per frame: the frame's bytes are staged in LDS by the whole wave (coalesced dword loads), then lane 0
 // decodes from LDS (bit refills are LDS reads instead of dependent global loads).  Frames larger than the stage
-// are decoded straight from global memory.  Multi-channel and wide streams (and FRS_ABLATE 1024).
+// are decoded straight from global memory.  Multi-channel and wide streams.  Under a fused decode the int32
+// samples land in the `pcm` scratch first and the wave de-normalises the frame from there.
 __global__ void __launch_bounds__(64) k_decode_frames_wave(const uint8_t *blob, const int64_t *soff, int ns,
                                                           const int64_t *poff, const int64_t *cpos,
                                                           const int64_t *ends, const int64_t *fbase,
                                                           const int64_t *frame_cand, int64_t nframes, int channels,
-                                                          int stream_bps, int32_t *pcm, int blocksize, int *nvalid) {
+                                                          int stream_bps, int32_t *pcm, int blocksize, int *nvalid,
+                                                          DecOut dout) {
     __shared__ uint32_t stage[kDecStageWords + 4];
     __shared__ int32_t resbuf[kDecResMax];
     const int64_t fi = blockIdx.x;
     if (fi >= nframes) return;
     const int lane = threadIdx.x;
     const int64_t ci = frame_cand[fi];
-    if (ci < 0) return;  // not on a valid chain (the host reports it)
+    if (ci < 0 || ends[ci] < 0) return;  // not on a verified chain (the host reports it)
     const int64_t fpos = cpos[ci], fend = ends[ci];
     const int s = stream_of(soff, ns, fpos);
     const int64_t send = soff[s + 1];
@@ -1254,13 +1385,21 @@ __global__ void __launch_bounds__(64) k_decode_frames_wave(const uint8_t *blob, 
     if (staged)
         for (int64_t k = lane; k < we - wb + 4; k += 64) stage[k] = load_word_guarded(blob, wb + k, send);
     __syncthreads();
-    if (lane != 0) return;
-    if (staged)
-        decode_one_frame(blob, reinterpret_cast<const uint8_t *>(stage), wb * 4, soff, ns, poff, cpos, ends, fbase,
-                         frame_cand, fi, channels, stream_bps, pcm, blocksize, nvalid, resbuf, stage);
-    else
-        decode_one_frame(blob, blob, 0, soff, ns, poff, cpos, ends, fbase, frame_cand, fi, channels, stream_bps, pcm,
-                         blocksize, nvalid, resbuf, nullptr);
+    if (lane == 0) {
+        if (staged)
+            decode_one_frame(blob, reinterpret_cast<const uint8_t *>(stage), wb * 4, soff, ns, poff, cpos, ends, fbase,
+                             frame_cand, fi, channels, stream_bps, pcm, blocksize, nvalid, resbuf, stage);
+        else
+            decode_one_frame(blob, blob, 0, soff, ns, poff, cpos, ends, fbase, frame_cand, fi, channels, stream_bps,
+                             pcm, blocksize, nvalid, resbuf, nullptr);
+    }
+    if (dout.out == nullptr) return;
+    __syncthreads();  // lane 0's global writes are visible to the work-group (one wave)
+    const int64_t first = (fi - fbase[s]) * blocksize;
+    const int64_t n = min<int64_t>(blocksize, poff[s + 1] - poff[s] - first) * channels;
+    const int64_t e0 = (poff[s] + first) * channels;
+    const float2 dnp = dout.dn[s];
+    for (int64_t i = lane; i < n; i += 64) dn_store(dout, e0 + i, pcm[e0 + i], dnp);
 }
 
 // converter.py:88-110 (fp32, round half to even) after the pyflac/soundfile WAV round trip.
@@ -1286,7 +1425,7 @@ static bool g_dec_tables[64];
 
 int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const int64_t *stream_off,
                int32_t nstreams, int32_t channels, int32_t bps, int32_t blocksize, int32_t *pcm_dev,
-               const int64_t *pcm_off) {
+               const int64_t *pcm_off, const double *dmin, const double *dmax, int32_t out_dtype, void *out_dev) {
     hipStream_t st = ctx->stream;
     if (!g_dec_tables[ctx->device]) {
         uint8_t t8[256];
@@ -1328,95 +1467,111 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         g_dec_tables[ctx->device] = true;
     }
     if (blob_bytes <= 0 || nstreams <= 0) return FRS_OK;
+    const bool fused = out_dev != nullptr;
     std::vector<int64_t> fbase(nstreams + 1, 0);
     for (int s = 0; s < nstreams; s++) fbase[s + 1] = fbase[s] + (pcm_off[s + 1] - pcm_off[s] + blocksize - 1) / blocksize;
     const int64_t frames = fbase[nstreams];
+    if (frames == 0) return FRS_OK;
     const int64_t max_frame = (int64_t)blocksize * channels * 5 + 4096;
-    // scratch: flags (1 B/byte), candidate positions, ends, chain
-    FRS_HIP(ctx->dec_blob.ensure((size_t)blob_bytes + 64));
-    uint8_t *flags = ctx->dec_blob.as<uint8_t>();
-    FRS_HIP(ctx->dec_cand.ensure(sizeof(int64_t) * (size_t)(2 * blob_bytes / 16 + 2 * frames + 1024)));
-    FRS_HIP(ctx->dec_count.ensure(sizeof(int) * 4));
-    FRS_HIP(ctx->dec_soff.ensure(sizeof(int64_t) * (nstreams + 1) * 3 + sizeof(int64_t) * frames));
-    FRS_HIP(ctx->dec_poff.ensure(sizeof(int64_t) * (nstreams + 1)));
-    int64_t *dsoff = ctx->dec_soff.as<int64_t>();
-    int64_t *dfbase = dsoff + (nstreams + 1);
-    int64_t *dchain = dfbase + (nstreams + 1);
-    // the per-call tables go through the context's pinned staging (DMA copies, no staged pageable transfers):
-    // [stream_off | fbase] -> dsoff/dfbase (contiguous on the device), pcm_off -> dec_poff; the result counters
-    // come back into the same staging after the tables
+    // FRS_FORCE_GENERIC (tests): every frame through the one-lane wave decoder
+    const bool pipe = channels == 1 && bps <= 16 && blocksize <= kDecResMax && !ctx->force_generic;
+    if (fused && !pipe) {  // the wave decoder de-normalises out of an int32 scratch
+        const int64_t nsamp = pcm_off[nstreams] - pcm_off[0];
+        if (!pcm_dev) {
+            FRS_HIP(ctx->dec_pcm.ensure((size_t)nsamp * channels * 4 + 16));
+            pcm_dev = ctx->dec_pcm.as<int32_t>() - pcm_off[0] * channels;
+        }
+    }
+    // Candidate capacity: every true frame plus false syncs (a sync pattern with a CRC-8-correct header inside
+    // frame data, ~1e-7 per byte) with a wide margin; a crafted stream with more is rejected (nothing is written
+    // past the cap).  Indices stay below 2^31.
+    const int64_t cand_cap = std::min<int64_t>(2 * frames + blob_bytes / 1024 + 4096, (int64_t)0x7FFFFFF0);
+    const int64_t nblocks = (blob_bytes + (int64_t)(reinterpret_cast<uintptr_t>(blob_dev) & 15) + kSelBytes - 1) / kSelBytes;
+    if (nblocks > (int64_t)0xFFFFFFFF) {
+        ctx->err = "decode range too large";
+        return FRS_E_UNSUPPORTED;
+    }
+    FRS_HIP(ctx->dec_cand.ensure(sizeof(int64_t) * 2 * (size_t)cand_cap));
+    FRS_HIP(ctx->dec_next.ensure(sizeof(int32_t) * (size_t)cand_cap + 64));
+    if (!ctx->dec_count.ptr) {  // counters + the selection ticket: zeroed once, re-armed by the kernel
+        FRS_HIP(ctx->dec_count.ensure(64));
+        FRS_HIP(hipMemsetAsync(ctx->dec_count.ptr, 0, ctx->dec_count.bytes, st));
+    }
+    {
+        void *before = ctx->dec_status.ptr;
+        FRS_HIP(ctx->dec_status.ensure(sizeof(uint64_t) * (size_t)nblocks));
+        if (ctx->dec_status.ptr != before) FRS_HIP(hipMemsetAsync(ctx->dec_status.ptr, 0, ctx->dec_status.bytes, st));
+    }
+    if (++ctx->dec_epoch >= (1u << 24)) ctx->dec_epoch = 1;
+    // per-call tables through the context's pinned staging in one DMA copy: stream_off | fbase | pcm_off | the
+    // fused decode's per-stream (float32(max - min), float32(min)) pairs; the result counters come back after them
     const size_t tab = sizeof(int64_t) * (size_t)(nstreams + 1);
-    FRS_HIP(ctx->pin.ensure(3 * tab + 64));
+    const size_t dn_bytes = fused ? sizeof(float2) * (size_t)nstreams : 0;
+    FRS_HIP(ctx->dec_soff.ensure(3 * tab + dn_bytes + sizeof(int64_t) * frames + 64));
+    FRS_HIP(ctx->pin.ensure(3 * tab + dn_bytes + 64));
     int64_t *htab = ctx->pin.at<int64_t>(0);
     memcpy(htab, stream_off, tab);
     memcpy(htab + (nstreams + 1), fbase.data(), tab);
     memcpy(htab + 2 * (nstreams + 1), pcm_off, tab);
-    FRS_HIP(hipMemcpyAsync(dsoff, htab, 2 * tab, hipMemcpyHostToDevice, st));
-    FRS_HIP(hipMemcpyAsync(ctx->dec_poff.ptr, htab + 2 * (nstreams + 1), tab, hipMemcpyHostToDevice, st));
-    FRS_HIP(hipMemsetAsync(ctx->dec_count.ptr, 0, sizeof(int) * 4, st));
+    float2 *hdn = reinterpret_cast<float2 *>(htab + 3 * (nstreams + 1));
+    if (fused)  // python-float arithmetic first (data_max - data_min in double), then NEP 50 casts to float32
+        for (int s = 0; s < nstreams; s++) hdn[s] = make_float2((float)(dmax[s] - dmin[s]), (float)dmin[s]);
+    FRS_HIP(hipMemcpyAsync(ctx->dec_soff.ptr, htab, 3 * tab + dn_bytes, hipMemcpyHostToDevice, st));
+    int64_t *dsoff = ctx->dec_soff.as<int64_t>();
+    int64_t *dfbase = dsoff + (nstreams + 1);
+    int64_t *dpoff = dfbase + (nstreams + 1);
+    const float2 *ddn = reinterpret_cast<const float2 *>(dpoff + (nstreams + 1));
+    int64_t *dchain = reinterpret_cast<int64_t *>(
+        (reinterpret_cast<uintptr_t>(dpoff + (nstreams + 1)) + dn_bytes + 7) & ~(uintptr_t)7);
     int *ncand = ctx->dec_count.as<int>();
     int *nvalid = ncand + 1;
     int *bad = ncand + 2;
-    hipEvent_t ev;
-    prof_begin(ctx, "decode", &ev);
-    k_flag_sync<<<(unsigned)((blob_bytes + 255) / 256), 256, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams, channels,
-                                                                     bps, flags);
-    // compact candidate positions (sorted)
-    const size_t cand_cap = (size_t)(2 * blob_bytes / 16 + 2 * frames + 1024) / 2;
+    unsigned long long *ticket = reinterpret_cast<unsigned long long *>(ctx->dec_count.as<char>() + 16);
     int64_t *cpos = ctx->dec_cand.as<int64_t>();
     int64_t *ends = cpos + cand_cap;
-    size_t tmp = 0;
-    hipcub::CountingInputIterator<int64_t> it(0);
-    FRS_HIP(hipcub::DeviceSelect::Flagged(nullptr, tmp, it, flags, cpos, ncand, (int)blob_bytes, st));
-    FRS_HIP(ctx->scan_tmp.ensure(tmp));
-    FRS_HIP(hipcub::DeviceSelect::Flagged(ctx->scan_tmp.ptr, tmp, it, flags, cpos, ncand, (int)blob_bytes, st));
-    const bool wave_span = max_frame < (int64_t)4096 * 256;  // x^(8m) table range
-    int hc = -1;  // candidate count on the host: only the fallback span kernels need it
-    if (!wave_span) {
-        FRS_HIP(hipMemcpyAsync(&hc, ncand, sizeof(int), hipMemcpyDeviceToHost, st));
-        FRS_HIP(hipStreamSynchronize(st));
-        if ((size_t)hc > cand_cap) {
-            ctx->err = "too many frame sync candidates";
-            return FRS_E_CORRUPT;
-        }
-    }
+    int32_t *nexti = ctx->dec_next.as<int32_t>();
+    hipEvent_t ev;
+    prof_begin(ctx, "decode", &ev);
+    k_sync_select<<<(unsigned)nblocks, kSelThreads, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams, channels, bps,
+                                                             ctx->dec_status.as<uint64_t>(), ticket, ctx->dec_epoch,
+                                                             nblocks, cpos, cand_cap, ncand);
     prof_end(ctx, "decode", ev);
-    // frames the chain does not reach keep -1 and are skipped by the decoders (the final count reports them)
-    FRS_HIP(hipMemsetAsync(dchain, 0xFF, sizeof(int64_t) * (size_t)frames, st));
-    if (frames > 0 && hc != 0) {
-        prof_begin(ctx, "decode_span", &ev);
-        if (wave_span) {
-            FRS_HIP(ctx->dec_next.ensure(sizeof(int32_t) * cand_cap + 64));
-            int32_t *nexti = ctx->dec_next.as<int32_t>();
-            const int64_t grid = std::min<int64_t>((int64_t)cand_cap, 2 * frames + 256);
-            k_span_crc_wave<<<(unsigned)grid, 64, 0, st>>>(blob_dev, dsoff, nstreams, cpos, ncand, (int)cand_cap,
-                                                           max_frame, ends, nexti);
-            k_chain_lds<<<nstreams, 64, 0, st>>>(dsoff, nstreams, cpos, ncand, (int)cand_cap, nexti, dfbase, dchain,
-                                                 bad);
-        } else {
-            k_span_crc<<<(hc + 63) / 64, 64, 0, st>>>(blob_dev, dsoff, nstreams, flags, cpos, ncand, max_frame, ends);
-            k_chain<<<(nstreams + 63) / 64, 64, 0, st>>>(dsoff, nstreams, cpos, ncand, ends, dfbase, dchain, bad);
-        }
-        prof_end(ctx, "decode_span", ev);
-        prof_begin(ctx, "decode_frames", &ev);
-        if (channels == 1 && bps <= 16 && blocksize <= kDecResMax && !(ctx->ablate & 1024))
-            k_decode_frames_pipe<<<(unsigned)frames, 128, 0, st>>>(blob_dev, dsoff, nstreams,
-                                                                   ctx->dec_poff.as<int64_t>(), cpos, ends, dfbase,
-                                                                   dchain, frames, channels, bps, pcm_dev, blocksize,
-                                                                   nvalid);
-        else
-            k_decode_frames_wave<<<(unsigned)frames, 64, 0, st>>>(blob_dev, dsoff, nstreams,
-                                                                  ctx->dec_poff.as<int64_t>(), cpos, ends, dfbase,
-                                                                  dchain, frames, channels, bps, pcm_dev, blocksize,
-                                                                  nvalid);
-        prof_end(ctx, "decode_frames", ev);
+    prof_begin(ctx, "decode_span", &ev);
+    // launched before the host knows the candidate count (no mid-query sync): an upper-bound grid strides over
+    // *ncand on the device; an overflowing selection makes every later kernel a no-op and is reported below
+    if (max_frame < (int64_t)4096 * 256) {  // x^(8m) table range of the wave CRC
+        const int64_t grid = std::min<int64_t>(cand_cap, std::min<int64_t>(2 * frames + 256, (int64_t)ctx->num_cus * 64));
+        k_span_crc_wave<<<(unsigned)grid, 64, 0, st>>>(blob_dev, dsoff, nstreams, cpos, ncand, (int)cand_cap,
+                                                       max_frame, ends, nexti);
+    } else {
+        k_span_crc<<<(unsigned)((cand_cap + 63) / 64), 64, 0, st>>>(blob_dev, dsoff, nstreams, cpos, ncand,
+                                                                    (int)cand_cap, max_frame, ends, nexti);
     }
-    int *hv = ctx->pin.at<int>(3 * tab);
+    k_chain_lds<<<nstreams, 64, 0, st>>>(dsoff, nstreams, cpos, ncand, (int)cand_cap, nexti, dfbase, dchain, bad);
+    prof_end(ctx, "decode_span", ev);
+    DecOut dout;
+    dout.out = out_dev;
+    dout.dn = ddn;
+    dout.dtype = out_dtype;
+    dout.shift = bps > 16 ? 16 : 0;
+    prof_begin(ctx, "decode_frames", &ev);
+    if (pipe)
+        k_decode_frames_pipe<<<(unsigned)frames, 128, 0, st>>>(blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase,
+                                                               dchain, frames, channels, bps, pcm_dev, blocksize, nvalid,
+                                                               dout);
+    else
+        k_decode_frames_wave<<<(unsigned)frames, 64, 0, st>>>(blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase,
+                                                              dchain, frames, channels, bps, pcm_dev, blocksize, nvalid,
+                                                              dout);
+    prof_end(ctx, "decode_frames", ev);
+    FRS_HIP(hipGetLastError());
+    int *hv = reinterpret_cast<int *>(reinterpret_cast<char *>(htab) + ((3 * tab + dn_bytes + 15) & ~(size_t)15));
     FRS_HIP(hipMemcpyAsync(hv, ncand, sizeof(int) * 3, hipMemcpyDeviceToHost, st));
     FRS_HIP(hipStreamSynchronize(st));
     prof_collect(ctx);
-    if ((size_t)hv[0] > cand_cap) {
-        ctx->err = "too many frame sync candidates";
+    if ((int64_t)hv[0] > cand_cap) {
+        ctx->err = "too many frame sync candidates (" + std::to_string(hv[0]) + " > " + std::to_string(cand_cap) +
+                   "): not a FLAC stream of the expected layout";
         return FRS_E_CORRUPT;
     }
     if (hv[2] != 0 || hv[1] != frames) {

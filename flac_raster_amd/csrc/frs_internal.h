@@ -77,7 +77,8 @@ struct frs_ctx {
     HostPin pin;                       // pinned staging of the fast encode path (tiles, wave table, results)
     DevBuf host_pack;                  // device side of the packed fast-path results
     // decode scratch
-    DevBuf dec_cand, dec_count, dec_blob, dec_pcm, dec_soff, dec_poff, dec_next;
+    DevBuf dec_cand, dec_count, dec_pcm, dec_soff, dec_next, dec_status;
+    uint32_t dec_epoch = 0;  // call counter tagging the candidate selection's look-back words (24 bits, never 0)
     // profiling
     bool prof = false;
     std::map<std::string, ProfEntry> prof_tab;
@@ -104,9 +105,13 @@ void prof_collect(frs_ctx *ctx);
 
 int encode_job(frs_ctx *ctx, const frs_encode_desc *d, const void *raster_dev, void *arena_dev, int64_t arena_cap,
                int64_t *tile_off, double *tile_min, double *tile_max, int32_t *stream_bps);
+// Decode the frames of nstreams streams.  out_dev == nullptr: int32 PCM into pcm_dev.  Otherwise the samples are
+// de-normalised in the decode kernels (converter.py:88-110) with per-stream dmin/dmax into out_dev (out_dtype),
+// and pcm_dev is only an optional int32 scratch (multi-channel / wide streams).
 int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const int64_t *stream_off,
                int32_t nstreams, int32_t channels, int32_t bps, int32_t blocksize, int32_t *pcm_dev,
-               const int64_t *pcm_off);
+               const int64_t *pcm_off, const double *dmin = nullptr, const double *dmax = nullptr,
+               int32_t out_dtype = 0, void *out_dev = nullptr);
 int denormalize_job(frs_ctx *ctx, const int32_t *pcm_dev, int64_t n, int pcm_bps, double dmin, double dmax,
                     int32_t out_dtype, void *out_dev);
 int64_t arena_bound(const frs_encode_desc *d);

@@ -256,19 +256,29 @@ class TileDecoder:
             groups.setdefault((m.channels, m.bps, m.blocksize), []).append(i)
         for (ch, bps, bs), idx in groups.items():
             blobs = [np.frombuffer(streams[i], dtype=np.uint8)[metas[i].audio_offset:] for i in idx]
-            soff = np.zeros(len(idx) + 1, dtype=np.int64)
-            soff[1:] = np.cumsum([len(b) for b in blobs])
-            blob = np.concatenate(blobs) if blobs else np.zeros(0, np.uint8)
             counts = [int(mds[i]["width"]) * int(mds[i]["height"]) for i in idx]
-            pcm = self.ctx.decode_frames_host(blob, soff, counts, channels=ch, bps=bps, blocksize=bs)
-            p0 = 0
+            # one fused decode + de-normalise per raster dtype (tiles of one file share it)
+            by_dt: Dict[str, List[int]] = {}
+            for j, i in enumerate(idx):
+                by_dt.setdefault(str(mds[i]["dtype"]), []).append(j)
+            vals_of: Dict[int, np.ndarray] = {}
+            for dts, js in by_dt.items():
+                sel = [idx[j] for j in js]
+                sb = [blobs[j] for j in js]
+                so = np.zeros(len(sb) + 1, dtype=np.int64)
+                so[1:] = np.cumsum([len(b) for b in sb])
+                cnt = [counts[j] for j in js]
+                allv = self.ctx.decode_tiles_host(np.concatenate(sb), so, cnt, channels=ch, bps=bps,
+                                                  data_min=[mds[i]["data_min"] for i in sel],
+                                                  data_max=[mds[i]["data_max"] for i in sel], dtype=np.dtype(dts),
+                                                  blocksize=bs)
+                p0 = 0
+                for j, n in zip(js, cnt):
+                    vals_of[j] = allv[p0:p0 + n]
+                    p0 += n
             for j, i in enumerate(idx):
                 md = mds[i]
-                n = counts[j]
-                seg = pcm[p0:p0 + n]
-                p0 += n
-                dt = np.dtype(md["dtype"])
-                vals = self.ctx.denormalize_host(seg, md["data_min"], md["data_max"], dt, pcm_bps=bps)
+                vals = vals_of[j]
                 H, W, C = int(md["height"]), int(md["width"]), int(md["count"])
                 arr = vals.reshape(H, W, C).transpose(2, 0, 1) if C > 1 else vals.reshape(1, H, W)
                 out[i] = (np.ascontiguousarray(arr), md)

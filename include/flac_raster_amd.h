@@ -120,13 +120,28 @@ int frs_encode_tiles(frs_ctx *ctx, const frs_encode_desc *desc, const void *rast
  * and must start at its first frame (the caller skips the metadata blocks; container.py parses them).
  * channels/bps describe every stream (STREAMINFO); samples are written interleaved as int32 at
  * pcm_out + pcm_off[s] * channels, pcm_off has nstreams+1 entries (per-stream sample counts known
- * from the tile windows).  Frames are located by sync code + CRC-8/CRC-16, decoded one lane per
- * subframe. */
+ * from the tile windows).  Frames are located by sync code + CRC-8/CRC-16 and decoded one work-group
+ * per frame.  Ranges of any size are accepted (64-bit positions); a stream with more sync-code
+ * candidates than the capacity (2 x frames + bytes / 1024 + 4096) is rejected with FRS_E_CORRUPT before
+ * anything is written past it. */
 int frs_decode_frames_device(frs_ctx *ctx, const uint8_t *blob_dev, const int64_t *stream_off, int32_t nstreams,
                              int32_t channels, int32_t bps, int32_t blocksize, int32_t *pcm_dev,
                              const int64_t *pcm_off);
 int frs_decode_frames(frs_ctx *ctx, const uint8_t *blob_host, const int64_t *stream_off, int32_t nstreams,
                       int32_t channels, int32_t bps, int32_t blocksize, int32_t *pcm_host, const int64_t *pcm_off);
+
+/* Decode + de-normalise in one pass: replaces converter.py:241-282 as a whole (pyflac FileDecoder ->
+ * soundfile PCM_16 WAV -> _denormalize_from_audio, sonos-pyflac.txt:1584-1640, converter.py:88-110) for
+ * `nstreams` tiles at once.  Same stream layout as frs_decode_frames; stream s carries its own
+ * GEOSPATIAL_DATA_MIN/MAX (data_min[s], data_max[s], converter.py:375-427) and its samples are written
+ * interleaved as out_dtype at out + (pcm_off[s] + i) * channels + c -- the int32 PCM never reaches memory for
+ * mono 16-bit streams (create-streaming tiles).  Errors as frs_decode_frames. */
+int frs_decode_tiles_device(frs_ctx *ctx, const uint8_t *blob_dev, const int64_t *stream_off, int32_t nstreams,
+                            int32_t channels, int32_t bps, int32_t blocksize, const int64_t *pcm_off,
+                            const double *data_min, const double *data_max, int32_t out_dtype, void *out_dev);
+int frs_decode_tiles(frs_ctx *ctx, const uint8_t *blob_host, const int64_t *stream_off, int32_t nstreams,
+                     int32_t channels, int32_t bps, int32_t blocksize, const int64_t *pcm_off, const double *data_min,
+                     const double *data_max, int32_t out_dtype, void *out_host);
 
 /* converter.py:88-110 after pyflac+soundfile's WAV round trip (sonos-pyflac.txt:1629, 1827-1852): the
  * decoder's int32 samples go into a PCM_16 WAV (16-bit streams unchanged; 32-bit streams keep x >> 16,

@@ -10,6 +10,17 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 
+def _header_len(frames: np.ndarray) -> int:
+    """Bytes of the first frame's header up to and including its CRC-8 (RFC 9639 9.1)."""
+    b = frames.tobytes()
+    n = 4
+    v = b[n]
+    n += 1 + (0 if v < 0x80 else 1 if v < 0xE0 else 2 if v < 0xF0 else 3)
+    bsc, src = b[2] >> 4, b[2] & 15
+    n += {6: 1, 7: 2}.get(bsc, 0) + {12: 1, 13: 2, 14: 2}.get(src, 0)
+    return n + 1
+
+
 def _bands():
     rng = np.random.default_rng(77)
     H, W = 512, 768
@@ -32,10 +43,10 @@ def _bands():
             ("flat", flat, 256), ("spiky", spiky, 256)]
 
 
-@pytest.mark.parametrize("ablate", ["0", "1024"])  # 1024: force the lane-0 decoder
-def test_decode_matches_oracle(gpu_ctx, ablate, monkeypatch):
+@pytest.mark.parametrize("generic", ["0", "1"])  # 1: every frame through the lane-0 wave decoder
+def test_decode_matches_oracle(gpu_ctx, generic, monkeypatch):
     from flac_raster_amd import _native
-    monkeypatch.setenv("FRS_ABLATE", ablate)
+    monkeypatch.setenv("FRS_FORCE_GENERIC", generic)
     dctx = _native.Context(0)
     for name, band, tile in _bands():
         H, W = band.shape
@@ -46,19 +57,26 @@ def test_decode_matches_oracle(gpu_ctx, ablate, monkeypatch):
             for c0 in range(0, W, tile):
                 counts.append(min(tile, H - r0) * min(tile, W - c0))
         pcm = dctx.decode_frames_host(arena, off, counts, channels=1, bps=16)
+        # fused decode + de-normalisation (converter.py:241-282 in one pass) against the oracle's two steps
+        vals = dctx.decode_tiles_host(arena, off, counts, channels=1, bps=16, data_min=mn, data_max=mx,
+                                      dtype=band.dtype)
         for t, n in enumerate(counts):
             frames = arena[off[t]:off[t + 1]].tobytes()
             ref = O.decode_frames(frames, 1, 16, n)
-            got = pcm[int(np.sum(counts[:t])):int(np.sum(counts[:t + 1]))]
-            assert np.array_equal(got, ref), (name, t)
+            a, b = int(np.sum(counts[:t])), int(np.sum(counts[:t + 1]))
+            assert np.array_equal(pcm[a:b], ref), (name, t)
+            assert np.array_equal(vals[a:b], O.denormalize_i16(ref, mn[t], mx[t], band.dtype)), (name, t)
     dctx.close()
 
 
-def test_decode_corrupt_streams_report_errors(gpu_ctx):
+@pytest.mark.parametrize("generic", ["0", "1"])
+def test_decode_corrupt_streams_report_errors(gpu_ctx, generic, monkeypatch):
     """Damaged data must end in FrsError (CRC-16 span check fails, chain broken, or no sync codes at all), never a
-    fault or a silent wrong decode; the context then still decodes good data (the decode path launches its span
-    and frame kernels before the host knows the candidate count, so the unchained frames are skipped on device)."""
+    fault, a stall or a silent wrong decode; the context then still decodes good data (the decode path launches its
+    span and frame kernels before the host knows the candidate count, so the unchained frames are skipped on
+    device: a frame whose CRC span fails is never handed to a decoder)."""
     from flac_raster_amd import _native
+    monkeypatch.setenv("FRS_FORCE_GENERIC", generic)
     dctx = _native.Context(0)
     band = _bands()[0][1][:256, :256].copy()
     d = gpu_ctx.make_desc(256, 256, band.dtype, tile_h=128, tile_w=128, sample_rate=44100, bits_per_sample=16)
@@ -68,8 +86,20 @@ def test_decode_corrupt_streams_report_errors(gpu_ctx):
     flipped[off[1] + 200:off[1] + 260] ^= 0x5A  # inside tile 1's first frame
     with pytest.raises(_native.FrsError):
         dctx.decode_frames_host(flipped, off, counts, channels=1, bps=16)
+    # a frame that is not the first: tile 2's third frame (the chain breaks in the middle of a stream)
+    third = off[2] + (off[3] - off[2]) * 2 // 4 + 100
+    flipped = arena.copy()
+    flipped[third:third + 48] ^= 0xA5
+    with pytest.raises(_native.FrsError):
+        dctx.decode_tiles_host(flipped, off, counts, channels=1, bps=16, data_min=mn, data_max=mx, dtype=band.dtype)
     with pytest.raises(_native.FrsError):  # no sync codes anywhere
         dctx.decode_frames_host(np.zeros_like(arena), off, counts, channels=1, bps=16)
+    # a crafted range where a valid frame header repeats every few bytes: more sync candidates than the bounded
+    # selection keeps -> rejected before anything is written past the candidate buffer
+    one = arena[:_header_len(arena)].tobytes()
+    spam = np.frombuffer(one * (400000 // len(one)), dtype=np.uint8)
+    with pytest.raises(_native.FrsError, match="candidates"):
+        dctx.decode_frames_host(spam, [0, len(spam)], [4096 * 2], channels=1, bps=16)
     pcm = dctx.decode_frames_host(arena, off, counts, channels=1, bps=16)
     for t in range(4):
         ref = O.decode_frames(arena[off[t]:off[t + 1]].tobytes(), 1, 16, counts[t])

@@ -109,6 +109,10 @@ def test_decode_roundtrip_and_denormalize(gpu_ctx, golden):
     assert np.array_equal(out, O.denormalize_i16(pcm, 1.0, 255.0, np.uint8))
     # lossless for uint8: back to the TIFF pixels
     assert np.array_equal(out.reshape(256, 256, 3).transpose(2, 0, 1), r.data)
+    # fused decode + de-normalisation (3 interleaved channels: the wave decoder with the int32 scratch)
+    fused = gpu_ctx.decode_tiles_host(frames, [0, len(frames)], [65536], channels=3, bps=16, data_min=[1.0],
+                                      data_max=[255.0], dtype=np.uint8)
+    assert np.array_equal(fused, out)
 
 
 @pytest.mark.parametrize("dtype,lo,hi,shape,tile", [
