@@ -23,7 +23,8 @@ struct TileGeom {
     int32_t h, w;        // tile size (edge tiles truncated, cli.py:694-696)
     int64_t frame_base;  // index of the tile's first frame in the job's frame list
     int32_t nframes;
-    int32_t pad;
+    int32_t partial;     // fast path: 1 + index of the tile's partial last frame among the job's partial frames
+                         // (coded by the generic kernels beforehand), 0 when every frame is a full block
 };
 
 // Per-tile normalisation parameters (k_tile_stats).

@@ -342,13 +342,17 @@ __device__ inline double expected_bits(double lpc_error, double error_scale) {
 template <int DT, bool WIDE>
 __global__ void __launch_bounds__(128) k_analyze(const typename Elem<DT>::T *raster, EncodeParams P,
                                                 const TileGeom *tiles, const TileNorm *norms,
-                                                const float *__restrict__ window, SubAnalysis *out) {
+                                                const float *__restrict__ window, SubAnalysis *out,
+                                                const int64_t *__restrict__ flist, int64_t nlist) {
+    // flist: the frames to analyse (the fast path's partial last frames), nullptr = every frame of the job
     using T = typename Elem<DT>::T;
-    const int64_t sub = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t nsub = P.nframes * P.nch;
-    const bool live = sub < nsub;
-    const int64_t f = live ? sub / P.nch : 0;
-    const int ch = live ? (int)(sub - f * P.nch) : 0;
+    const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nsub = (flist ? nlist : P.nframes) * P.nch;
+    const bool live = li < nsub;
+    const int64_t fi = live ? li / P.nch : 0;
+    const int ch = live ? (int)(li - fi * P.nch) : 0;
+    const int64_t f = flist ? flist[fi] : fi;
+    const int64_t sub = f * P.nch + ch;
     const int t = tile_of_frame(tiles, P.ntiles, f);
     const TileGeom g = tiles[t];
     const int64_t s0 = (f - g.frame_base) * P.blocksize;
@@ -767,11 +771,15 @@ template <int DT>
 __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename Elem<DT>::T *raster, EncodeParams P,
                                                              const TileGeom *tiles, const TileNorm *norms,
                                                              const SubAnalysis *ana, uint32_t *slots,
-                                                             int64_t *frame_bytes, int *error_flag) {
+                                                             int64_t *frame_bytes, int *error_flag,
+                                                             const int64_t *__restrict__ flist) {
+    // flist: frames to code (the fast path's partial last frames; slot / frame_bytes indexed by list position),
+    // nullptr = frame blockIdx.x
     using T = typename Elem<DT>::T;
     __shared__ EncShared S;
     const int tid = threadIdx.x;
-    const int64_t f = blockIdx.x;
+    const int64_t si = blockIdx.x;
+    const int64_t f = flist ? flist[si] : si;
     const int t = tile_of_frame(tiles, P.ntiles, f);
     const TileGeom g = tiles[t];
     const int64_t fk = f - g.frame_base;  // frame number within the tile's stream
@@ -779,7 +787,7 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
     const int64_t tile_px = (int64_t)g.h * g.w;
     const int n = (int)((tile_px - s0) < P.blocksize ? (tile_px - s0) : P.blocksize);
     const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits, P.norm_mode);
-    uint32_t *slot = slots + (size_t)f * P.slot_words;
+    uint32_t *slot = slots + (size_t)si * P.slot_words;
     const int rice_limit = P.bps > 16 ? 31 : 15;
     const int max_po_block = min(kMaxPartOrder, __builtin_ctz((unsigned)n));
 
@@ -1119,7 +1127,7 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
     const uint64_t bits_total = (uint64_t)w0 * 32 + fb;
     const uint64_t bytes = (bits_total + 7) >> 3;
     if (fb && tid == 0) slot[w0] = __builtin_bswap32(S.bits[0]);
-    if (tid == 0) frame_bytes[f] = (int64_t)bytes + 2;  // + CRC-16 footer
+    if (tid == 0) frame_bytes[si] = (int64_t)bytes + 2;  // + CRC-16 footer
 }
 
 // ------------------------------------------------------------------------------------ k_compact
@@ -1171,6 +1179,30 @@ __global__ void __launch_bounds__(256) k_compact(const uint32_t *slots, int slot
     if (threadIdx.x == 0) {
         arena[D + L] = (uint8_t)(crc >> 8);
         arena[D + L + 1] = (uint8_t)crc;
+    }
+}
+
+// Fast path: the partial last frames coded by k_encode_frames get their CRC-16 footer in place (slot bytes
+// [0, S - 2) -> [S - 2, S)), so k_encode_v3 copies finished frames.
+__global__ void __launch_bounds__(256) k_seal_partial(uint32_t *slots, int slot_words, const int64_t *frame_bytes,
+                                                     int64_t nlist) {
+    const int64_t si = blockIdx.x;
+    if (si >= nlist) return;
+    uint8_t *src = reinterpret_cast<uint8_t *>(slots + (size_t)si * slot_words);
+    const int64_t L = frame_bytes[si] - 2;
+    const int64_t ch = (L + 255) / 256;
+    const int64_t b0 = min(L, (int64_t)threadIdx.x * ch), b1 = min(L, b0 + ch);
+    uint32_t c = 0;
+    for (int64_t i = b0; i < b1; i++) c = ((c << 8) & 0xFFFFu) ^ c_crc16[((c >> 8) ^ src[i]) & 0xFF];
+    if (b1 > b0 && b1 < L) c = gf_mulmod(c, xpow8((uint64_t)(L - b1)));
+    for (int o = 32; o > 0; o >>= 1) c ^= __shfl_xor(c, o);
+    __shared__ uint32_t wc[4];
+    if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t crc = wc[0] ^ wc[1] ^ wc[2] ^ wc[3];
+        src[L] = (uint8_t)(crc >> 8);
+        src[L + 1] = (uint8_t)crc;
     }
 }
 
@@ -1725,8 +1757,10 @@ __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *
     const int mode = tn.mode;  // wave-uniform: one tile per wave
     const bool lean = mode == kNormLut || mode == kNormZero;
     if (lean == SLOW) return;
-    const bool live = wt.y + lane < g.nframes;
-    const int64_t fk = live ? wt.y + lane : g.nframes - 1;  // dead lanes re-read the tile's last frame
+    const int nfull = g.nframes - (g.partial ? 1 : 0);  // a partial last frame is analysed by k_analyze
+    if (nfull == 0) return;                              // (wave-uniform) only its stats were needed here
+    const bool live = wt.y + lane < nfull;
+    const int64_t fk = live ? wt.y + lane : nfull - 1;  // dead lanes re-read the tile's last full frame
     const int64_t f = g.frame_base + fk;
     const int64_t s0 = fk * P.blocksize;
     const int64_t tile_px = (int64_t)g.h * g.w;
@@ -2206,11 +2240,39 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
                                        const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
                                        const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap, int64_t *frame_off,
                                        uint64_t *status, int *err, EncV3Shared &S, int want, int64_t f, int lane,
-                                       const int32_t *ftile, PendingFrame &prev, const uint4 *hdr_tab, int hdr_n) {
+                                       const int32_t *ftile, PendingFrame &prev, const uint4 *hdr_tab, int hdr_n,
+                                       const uint32_t *pslots, const int64_t *pbytes) {
     using T = typename Elem<DT>::T;
     uint32_t *fbuf = S.bits[threadIdx.x >> 6];
     const int t = ftile[f];
     const TileGeom g = tiles[t];
+    if (g.partial && f - g.frame_base == g.nframes - 1) {
+        // (wave-uniform) the tile's partial last frame: already coded and sealed by the generic kernels, so it
+        // only joins the look-back chain -- publish its size, finish the previous frame, and stage its bytes in
+        // the bit buffer for resolve_and_store like a frame coded here
+        const int64_t si = g.partial - 1;
+        const uint64_t nb = (uint64_t)pbytes[si];
+        const uint32_t words = (uint32_t)((nb + 3) >> 2);
+        const bool ok = words + 2 <= (uint32_t)kFrameWordsV3;
+        if (!ok && lane == 0) atomicOr(err, 2);
+        const uint64_t fbytes = ok ? nb : 0;
+        const FbMap M = fb_map(words + 1);
+        if (lane == 0)
+            __hip_atomic_store(&status[f], (f == 0 ? kFlagIncl : kFlagAgg) | fbytes, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
+        if (ok) {
+            const uint32_t *src = pslots + (size_t)si * P.slot_words;
+            for (uint32_t w = (uint32_t)lane; w < words; w += 64) fbuf[M(w)] = __builtin_bswap32(src[w]);
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+        prev.f = f;
+        prev.fbytes = fbytes;
+        prev.ok = ok;
+        prev.map = M;
+        return;
+    }
     TileNorm tn = norms[t];
     // the WG's LDS LUT belongs to tile `want`; a frame of another tile takes the exact division instead
     if (t != want && tn.mode == kNormLut) tn.mode = kNormSlow;
@@ -2710,7 +2772,8 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
                                                   const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap,
                                                   int64_t *frame_off, uint64_t *status, int *ticket_ctr, int *err,
                                                   const int32_t *__restrict__ ftile, const uint4 *__restrict__ hdr_tab,
-                                                  int hdr_n) {
+                                                  int hdr_n, const uint32_t *__restrict__ pslots,
+                                                  const int64_t *__restrict__ pbytes) {
     __shared__ EncV3Shared S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int i = threadIdx.x; i < 1024; i += blockDim.x) (&S.crc4[0][0])[i] = (&c_crc16x4[0][0])[i];
@@ -2745,7 +2808,7 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
         const int64_t f = fbase + wave;
         if (f < P.nframes)
             encode_frame_v3<DT>(raster, P, tiles, norms, luts, ana, arena, arena_cap, frame_off, status, err, S, want, f,
-                                lane, ftile, prev, hdr_tab, hdr_n);
+                                lane, ftile, prev, hdr_tab, hdr_n, pslots, pbytes);
     }
     if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
 }
@@ -2878,7 +2941,7 @@ static void build_tiles(const frs_encode_desc *d, std::vector<TileGeom> &tiles, 
         const int64_t px = (int64_t)g.h * g.w;
         g.nframes = (int32_t)((px + d->blocksize - 1) / d->blocksize);
         g.frame_base = nframes;
-        g.pad = 0;
+        g.partial = 0;
         nframes += g.nframes;
         tiles.push_back(g);
     }
@@ -2891,9 +2954,11 @@ int64_t arena_bound(const frs_encode_desc *d) {
     return nframes * (slot_words_for(d) * 4) + 64;
 }
 
+constexpr int kFastDeclined = 1000;  // run_encode: the fast path hit a frame it cannot hold; rerun generic
+
 template <int DT>
 static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster_dev, void *arena_dev,
-                      int64_t arena_cap, int64_t *tile_off, double *tile_min, double *tile_max) {
+                      int64_t arena_cap, int64_t *tile_off, double *tile_min, double *tile_max, bool allow_fast) {
     using T = typename Elem<DT>::T;
     std::vector<TileGeom> tiles;
     int64_t nframes;
@@ -2934,7 +2999,21 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     const size_t wt_cap = (size_t)(nframes / 64 + ntiles + 1);
     const size_t pin_res = (pin_wt + sizeof(int2) * wt_cap + 255) & ~(size_t)255;
     const size_t res_bytes = sizeof(int64_t) * (3 * (size_t)ntiles + 2);
-    FRS_HIP(ctx->pin.ensure(pin_res + res_bytes));
+    const size_t pin_pl = (pin_res + res_bytes + 255) & ~(size_t)255;  // partial-frame list of the fast path
+    FRS_HIP(ctx->pin.ensure(pin_pl + sizeof(int64_t) * (size_t)ntiles));
+    // fast path: mono 16-bit streams of 4096-sample blocks.  A tile whose pixel count is not a multiple of 4096
+    // ends in a partial frame: those frames (at most one per tile) are coded by the generic kernels first and
+    // the fast encoder copies them into the arena in stream order
+    const bool fast = allow_fast && !ctx->force_generic && P.bps == 16 && P.nch == 1 && P.norm_mode == 0 &&
+                      d->blocksize == 4096 && !Elem<DT>::is_float;
+    int64_t npartial = 0;
+    int64_t *hplist = ctx->pin.at<int64_t>(pin_pl);
+    if (fast)
+        for (TileGeom &tg : tiles)
+            if (((int64_t)tg.h * tg.w) % d->blocksize != 0) {
+                hplist[npartial] = tg.frame_base + tg.nframes - 1;
+                tg.partial = (int32_t)(++npartial);
+            }
     if (ctx->window_bs != d->blocksize) {
         std::vector<float> win(d->blocksize, 1.0f);
         // FLAC__window_tukey(0.5) computed in double with the host libm cos, stored as float (window.c)
@@ -2963,14 +3042,8 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     SubAnalysis *dana = ctx->analysis.as<SubAnalysis>();
 
     hipEvent_t ev;
-    // fast path: mono 16-bit streams whose frames are all full 4096-sample blocks
-    bool all_full = true, one_wave_tiles = true;
-    for (const TileGeom &tg : tiles) {
-        all_full = all_full && (((int64_t)tg.h * tg.w) % d->blocksize == 0);
-        one_wave_tiles = one_wave_tiles && tg.nframes <= 64;
-    }
-    const bool fast = !ctx->force_generic && P.bps == 16 && P.nch == 1 && P.norm_mode == 0 && d->blocksize == 4096 &&
-                      all_full && !Elem<DT>::is_float;
+    bool one_wave_tiles = true;
+    for (const TileGeom &tg : tiles) one_wave_tiles = one_wave_tiles && tg.nframes <= 64;
     bool stats_vec = false;
     if constexpr (sizeof(T) <= 2 && !Elem<DT>::is_float) {
         const int64_t es = (int64_t)sizeof(T);
@@ -3043,6 +3116,24 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                                                           nwaves);
         }
         prof_end(ctx, "analyze", ev);
+        // partial last frames: generic analysis + frame coding into compact slots, CRC-16 sealed in place
+        int64_t *dpbytes = ctx->frame_bytes.as<int64_t>();  // [npartial] (< nframes + 1: below err_flag)
+        if (npartial > 0) {
+            prof_begin(ctx, "partial", &ev);
+            FRS_HIP(ctx->plist.ensure(sizeof(int64_t) * (size_t)npartial));
+            FRS_HIP(hipMemcpyAsync(ctx->plist.ptr, hplist, sizeof(int64_t) * (size_t)npartial, hipMemcpyHostToDevice,
+                                   st));
+            FRS_HIP(ctx->slots.ensure((size_t)npartial * P.slot_words * 4));
+            const int64_t *dpl = ctx->plist.as<int64_t>();
+            k_analyze<DT, false><<<(unsigned)((npartial + 127) / 128), 128, 0, st>>>(
+                raster, P, dtiles, dnorms, ctx->window.as<float>(), dana, dpl, npartial);
+            k_encode_frames<DT><<<(unsigned)npartial, kEncThreads, 0, st>>>(raster, P, dtiles, dnorms, dana,
+                                                                           ctx->slots.as<uint32_t>(), dpbytes,
+                                                                           err_flag, dpl);
+            k_seal_partial<<<(unsigned)npartial, 256, 0, st>>>(ctx->slots.as<uint32_t>(), P.slot_words, dpbytes,
+                                                               npartial);
+            prof_end(ctx, "partial", ev);
+        }
         uint64_t *dstatus = ctx->status.as<uint64_t>();
         int *ticket = reinterpret_cast<int *>(dstatus + nframes);
         FRS_HIP(hipMemsetAsync(dstatus, 0, sizeof(uint64_t) * (nframes + 1), st));
@@ -3119,7 +3210,7 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                                                             reinterpret_cast<uint8_t *>(arena_dev), arena_cap,
                                                             ctx->frame_off.as<int64_t>(), dstatus, ticket, err_flag,
                                                             ctx->frame_tile.as<int32_t>(), ctx->hdr_tab.as<uint4>(),
-                                                            hdr_n);
+                                                            hdr_n, ctx->slots.as<uint32_t>(), dpbytes);
         }
         prof_end(ctx, "encode", ev);
         if (P.ablate & 64) {
@@ -3151,9 +3242,9 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
             ctx->err = "arena too small";
             return FRS_E_NOSPACE;
         }
-        if (errv) {
-            ctx->err = "fast encode failed, flags " + std::to_string(errv);
-            return FRS_E_UNSUPPORTED;
+        if (errv) {  // a frame the fast kernels cannot hold (never seen: estimates stay below verbatim)
+            ctx->err = "fast encode declined, flags " + std::to_string(errv);
+            return kFastDeclined;
         }
         return FRS_OK;
     }
@@ -3163,18 +3254,18 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     prof_begin(ctx, "analyze", &ev);
     if (P.bps > 16) {
         k_analyze<DT, true><<<(unsigned)((nsub + 127) / 128), 128, 0, st>>>(raster, P, dtiles, dnorms,
-                                                                             ctx->window.as<float>(), dana);
+                                                                             ctx->window.as<float>(), dana, nullptr, 0);
         k_analyze_fixed_wide<DT><<<(unsigned)((nsub + 127) / 128), 128, 0, st>>>(raster, P, dtiles, dnorms, dana);
     } else {
         k_analyze<DT, false><<<(unsigned)((nsub + 127) / 128), 128, 0, st>>>(raster, P, dtiles, dnorms,
-                                                                              ctx->window.as<float>(), dana);
+                                                                              ctx->window.as<float>(), dana, nullptr, 0);
     }
     prof_end(ctx, "analyze", ev);
     // 3. encode frames into slots
     prof_begin(ctx, "encode", &ev);
     k_encode_frames<DT><<<(unsigned)nframes, kEncThreads, 0, st>>>(raster, P, dtiles, dnorms, dana,
                                                                    ctx->slots.as<uint32_t>(),
-                                                                   ctx->frame_bytes.as<int64_t>(), err_flag);
+                                                                   ctx->frame_bytes.as<int64_t>(), err_flag, nullptr);
     prof_end(ctx, "encode", ev);
     // 4. offsets
     size_t tmp_bytes = 0;
@@ -3219,17 +3310,25 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     return FRS_OK;
 }
 
+template <int DT>
+static int run_encode_any(frs_ctx *ctx, const frs_encode_desc *d, const void *raster_dev, void *arena_dev,
+                          int64_t arena_cap, int64_t *tile_off, double *tile_min, double *tile_max) {
+    int rc = run_encode<DT>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max, true);
+    if (rc == kFastDeclined) rc = run_encode<DT>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max, false);
+    return rc;
+}
+
 int encode_job(frs_ctx *ctx, const frs_encode_desc *d, const void *raster_dev, void *arena_dev, int64_t arena_cap,
                int64_t *tile_off, double *tile_min, double *tile_max, int32_t *stream_bps) {
     if (stream_bps) *stream_bps = stream_bps_of(d);
     switch (d->dtype) {
-    case FRS_DT_U8: return run_encode<FRS_DT_U8>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
-    case FRS_DT_U16: return run_encode<FRS_DT_U16>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
-    case FRS_DT_I16: return run_encode<FRS_DT_I16>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
-    case FRS_DT_I32: return run_encode<FRS_DT_I32>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
-    case FRS_DT_U32: return run_encode<FRS_DT_U32>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
-    case FRS_DT_F32: return run_encode<FRS_DT_F32>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
-    case FRS_DT_F64: return run_encode<FRS_DT_F64>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
+    case FRS_DT_U8: return run_encode_any<FRS_DT_U8>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
+    case FRS_DT_U16: return run_encode_any<FRS_DT_U16>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
+    case FRS_DT_I16: return run_encode_any<FRS_DT_I16>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
+    case FRS_DT_I32: return run_encode_any<FRS_DT_I32>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
+    case FRS_DT_U32: return run_encode_any<FRS_DT_U32>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
+    case FRS_DT_F32: return run_encode_any<FRS_DT_F32>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
+    case FRS_DT_F64: return run_encode_any<FRS_DT_F64>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
     default: ctx->err = "bad dtype"; return FRS_E_ARG;
     }
 }

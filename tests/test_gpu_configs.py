@@ -156,3 +156,31 @@ def test_c5_bbox_queries_match_linear_scan_and_oracle(gpu_ctx, c4):
         r0, c0 = wnd["row_off"], wnd["col_off"]
         assert np.array_equal(got, c4["band"][r0:r0 + wnd["height"], c0:c0 + wnd["width"]]), q
     out.close()
+
+
+# ------------------------------------------------------------------------- partial frames on the fast path
+@pytest.mark.parametrize("shape,tile,dtype", [
+    ((10980, 10980), 1024, np.uint16),  # the reference's Sentinel-2 B04 example (FLAC-SPATIAL.md:82-88): last tile 740^2
+    ((512, 512), 200, np.int16),        # sample_dem at tile 200: every tile ends in a partial frame
+    ((1000, 1000), 30, np.int16),       # tiles smaller than one frame (900 px: a single partial frame each)
+])
+def test_partial_frame_tiles_take_the_fast_path(gpu_ctx, shape, tile, dtype):
+    """Tiles whose pixel count is not a multiple of 4096 keep the fast kernels (their partial last frames are coded
+    by the generic kernels and joined into the fast encoder's look-back chain); bytes equal the oracle's."""
+    H, W = shape
+    rng = np.random.default_rng(11)
+    y = np.linspace(0, 20, H, dtype=np.float32)[:, None]
+    x = np.linspace(0, 20, W, dtype=np.float32)[None, :]
+    base = 3000 + 1200 * np.sin(x * 0.7) * np.cos(y * 0.3) + 400 * np.sin(1.3 * x) * np.sin(1.1 * y)
+    band = (base + 60 * rng.random((H, W), dtype=np.float32)).astype(dtype)
+    gpu_ctx.profile(True)
+    gpu_ctx.profile_reset()
+    d = gpu_ctx.make_desc(H, W, dtype, tile_h=tile, tile_w=tile, sample_rate=44100, bits_per_sample=16)
+    arena, off, mn, mx, bps = gpu_ctx.encode_tiles_host(band, d)
+    partial_ms, compact_ms = gpu_ctx.profile_avg_ms("partial"), gpu_ctx.profile_avg_ms("compact")
+    gpu_ctx.profile(False)
+    assert partial_ms > 0 and compact_ms < 0, "expected the fast path with a partial-frame pass"
+    o_arena, o_off, o_mn, o_mx = O.encode_tiles(band, tile, threads=workloads.oracle_threads())
+    assert np.array_equal(off, o_off)
+    assert arena.tobytes() == o_arena.tobytes()
+    assert np.array_equal(mn, o_mn) and np.array_equal(mx, o_mx)
