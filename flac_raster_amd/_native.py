@@ -33,7 +33,7 @@ EXPORTS = (
     "frs_denormalize_device", "frs_denormalize",
     "frs_dev_malloc", "frs_dev_free", "frs_memcpy_h2d", "frs_memcpy_d2h", "frs_ctx_sync",
     "frs_synth_raster_device", "frs_ctx_stream", "frs_profile_enable", "frs_profile_avg_ms",
-    "frs_profile_reset",
+    "frs_profile_reset", "frs_comm_unique_id", "frs_comm_init", "frs_comm_destroy", "frs_comm_allgather_i64",
 )
 
 
@@ -133,6 +133,14 @@ def load_library(path: Optional[os.PathLike] = None):
         L.frs_profile_avg_ms.argtypes = [ctxp, ctypes.c_char_p]
         L.frs_profile_reset.restype = None
         L.frs_profile_reset.argtypes = [ctxp]
+        L.frs_comm_unique_id.restype = i32
+        L.frs_comm_unique_id.argtypes = [vp]
+        L.frs_comm_init.restype = i32
+        L.frs_comm_init.argtypes = [ctxp, vp, i32, i32, ctypes.POINTER(ctypes.c_void_p)]
+        L.frs_comm_destroy.restype = None
+        L.frs_comm_destroy.argtypes = [vp]
+        L.frs_comm_allgather_i64.restype = i32
+        L.frs_comm_allgather_i64.argtypes = [vp, ip64, i64, ip64]
         if L.frs_abi_version() != 1:
             raise NativeUnavailable("ABI version mismatch")
         if path is None:

@@ -1,0 +1,127 @@
+// frs_comm.hip -- RCCL over xGMI for the multi-GPU create-streaming.
+//
+// Tiles shard by contiguous tile rows with no data-path collective; the one exchange of the sharded path is an
+// all-gather of per-tile byte sizes (a few KB) so every rank knows every tile's offset in the streaming file.
+// librccl.so is loaded at run time (dlopen), so the codec library itself has no hard RCCL dependency; the
+// ncclUniqueId of rank 0 reaches the other ranks through the host's bootstrap (flac_raster_amd/distributed.py).
+#include <dlfcn.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+
+#include <rccl/rccl.h>
+
+#include "frs_internal.h"
+
+struct frs_comm {
+    ncclComm_t comm = nullptr;
+    int rank = 0, nranks = 1;
+    frs_ctx *ctx = nullptr;
+    DevBuf buf;  // send | recv staging of the all-gathers
+};
+
+namespace {
+struct RcclApi {
+    void *h = nullptr;
+    ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*all_gather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    const char *(*error_string)(ncclResult_t) = nullptr;
+    std::string err;
+};
+RcclApi g_api;
+std::once_flag g_once;
+
+bool load_rccl() {
+    std::call_once(g_once, [] {
+        const char *names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
+        for (const char *n : names)
+            if ((g_api.h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
+        if (!g_api.h) {
+            g_api.err = std::string("cannot load librccl.so: ") + dlerror();
+            return;
+        }
+        g_api.get_unique_id = (decltype(g_api.get_unique_id))dlsym(g_api.h, "ncclGetUniqueId");
+        g_api.comm_init_rank = (decltype(g_api.comm_init_rank))dlsym(g_api.h, "ncclCommInitRank");
+        g_api.comm_destroy = (decltype(g_api.comm_destroy))dlsym(g_api.h, "ncclCommDestroy");
+        g_api.all_gather = (decltype(g_api.all_gather))dlsym(g_api.h, "ncclAllGather");
+        g_api.error_string = (decltype(g_api.error_string))dlsym(g_api.h, "ncclGetErrorString");
+        if (!g_api.get_unique_id || !g_api.comm_init_rank || !g_api.comm_destroy || !g_api.all_gather)
+            g_api.err = "librccl.so lacks the nccl* entry points";
+    });
+    return g_api.h && g_api.err.empty();
+}
+
+std::string nccl_msg(ncclResult_t r) {
+    return g_api.error_string ? g_api.error_string(r) : ("ncclResult " + std::to_string((int)r));
+}
+}  // namespace
+
+extern "C" {
+
+int frs_comm_unique_id(uint8_t *id_out) {
+    if (!id_out) return FRS_E_ARG;
+    if (!load_rccl()) return FRS_E_UNSUPPORTED;
+    ncclUniqueId id;
+    if (g_api.get_unique_id(&id) != ncclSuccess) return FRS_E_HIP;
+    memcpy(id_out, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return FRS_OK;
+}
+
+int frs_comm_init(frs_ctx *ctx, const uint8_t *id, int32_t nranks, int32_t rank, frs_comm **out) {
+    if (!ctx || !id || !out || nranks < 1 || rank < 0 || rank >= nranks) return FRS_E_ARG;
+    *out = nullptr;
+    if (!load_rccl()) {
+        ctx->err = g_api.err;
+        return FRS_E_UNSUPPORTED;
+    }
+    FRS_HIP(hipSetDevice(ctx->device));
+    ncclUniqueId uid;
+    memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
+    frs_comm *c = new frs_comm();
+    const ncclResult_t r = g_api.comm_init_rank(&c->comm, nranks, uid, rank);
+    if (r != ncclSuccess) {
+        ctx->err = "ncclCommInitRank: " + nccl_msg(r);
+        delete c;
+        return FRS_E_HIP;
+    }
+    c->rank = rank;
+    c->nranks = nranks;
+    c->ctx = ctx;
+    *out = c;
+    return FRS_OK;
+}
+
+void frs_comm_destroy(frs_comm *c) {
+    if (!c) return;
+    if (c->ctx) {
+        hipSetDevice(c->ctx->device);
+        hipStreamSynchronize(c->ctx->stream);
+    }
+    if (c->comm) g_api.comm_destroy(c->comm);
+    c->buf.release();
+    delete c;
+}
+
+int frs_comm_allgather_i64(frs_comm *c, const int64_t *send_host, int64_t count, int64_t *recv_host) {
+    if (!c || count < 0 || (count && (!send_host || !recv_host))) return FRS_E_ARG;
+    frs_ctx *ctx = c->ctx;
+    if (count == 0) return FRS_OK;
+    FRS_HIP(hipSetDevice(ctx->device));
+    const size_t sb = sizeof(int64_t) * (size_t)count;
+    FRS_HIP(c->buf.ensure(sb * (size_t)(c->nranks + 1)));
+    int64_t *dsend = c->buf.as<int64_t>(), *drecv = dsend + count;
+    FRS_HIP(hipMemcpyAsync(dsend, send_host, sb, hipMemcpyHostToDevice, ctx->stream));
+    const ncclResult_t r = g_api.all_gather(dsend, drecv, (size_t)count, ncclInt64, c->comm, ctx->stream);
+    if (r != ncclSuccess) {
+        ctx->err = "ncclAllGather: " + nccl_msg(r);
+        return FRS_E_HIP;
+    }
+    FRS_HIP(hipMemcpyAsync(recv_host, drecv, sb * (size_t)c->nranks, hipMemcpyDeviceToHost, ctx->stream));
+    FRS_HIP(hipStreamSynchronize(ctx->stream));
+    return FRS_OK;
+}
+
+}  // extern "C"

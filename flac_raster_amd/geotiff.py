@@ -92,13 +92,17 @@ class GeoRaster:
     @property
     def bounds(self) -> Tuple[float, float, float, float]:
         """rasterio DatasetBase.bounds for north-up transforms: (left, bottom, right, top)."""
-        t = self.transform or Affine(1.0, 0.0, 0.0, 0.0, 1.0, 0.0)
-        a, b, c, d, e, f = t.to_tuple()
-        if b == d == 0:
-            return (c, f + e * self.height, c + a * self.width, f)
-        xs = [c, c + a * self.width, c + b * self.height, c + a * self.width + b * self.height]
-        ys = [f, f + d * self.width, f + e * self.height, f + d * self.width + e * self.height]
-        return (min(xs), min(ys), max(xs), max(ys))
+        return bounds_of(self.transform or Affine(1.0, 0.0, 0.0, 0.0, 1.0, 0.0), self.width, self.height)
+
+
+def bounds_of(t: Affine, width: int, height: int) -> Tuple[float, float, float, float]:
+    """(left, bottom, right, top) of a width x height raster with transform t (rasterio DatasetBase.bounds)."""
+    a, b, c, d, e, f = t.to_tuple()
+    if b == d == 0:
+        return (c, f + e * height, c + a * width, f)
+    xs = [c, c + a * width, c + b * height, c + a * width + b * height]
+    ys = [f, f + d * width, f + e * height, f + d * width + e * height]
+    return (min(xs), min(ys), max(xs), max(ys))
 
 
 def _lzw_decode(data: bytes) -> bytes:

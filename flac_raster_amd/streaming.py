@@ -13,9 +13,11 @@ only the first intersecting tile.
 from __future__ import annotations
 
 import json
-import math
 import logging
+import math
+import os
 import struct
+import time
 from dataclasses import dataclass
 from pathlib import Path
 from typing import Dict, Iterable, List, Optional, Sequence, Tuple, Union
@@ -61,6 +63,64 @@ def tile_tags(crs: Optional[str], tt: geotiff.Affine, w: int, h: int, dtype, tmi
     return container.raster_tags(md)
 
 
+class TileHeaderBuilder:
+    """Per-tile FLAC headers of a streaming file, byte-identical to ``container.mutagen_header(..., tile_tags(...))``
+    (the mutagen rewrite of each temporary tile FLAC, converter.py:315-349) at a few microseconds per tile: the
+    constant tag entries are encoded once and the per-tile numbers (a C4 file has 6241 tiles but only 79 column
+    and 79 row origins) are formatted through a cache.  Checked against the direct path in tests."""
+
+    _PREFIX = (("TITLE", "Geospatial Raster Data"),
+               ("DESCRIPTION", "TIFF raster converted to FLAC with geospatial metadata"),
+               ("ENCODER", "FLAC-Raster v0.1.0"))
+
+    def __init__(self, crs: Optional[str], dtype, stream_bps: int, sample_rate: int = 44100, blocksize: int = 4096):
+        self._si = container.block(container.BLOCK_STREAMINFO,
+                                   container.streaminfo(blocksize, sample_rate, 1, stream_bps), False)
+        self._vendor = struct.pack("<I", len(container.VENDOR)) + container.VENDOR + struct.pack("<I", 14)
+        ent = self._entry
+        self._pre = b"".join(ent(k, v) for k, v in self._PREFIX) + ent("GEOSPATIAL_CRS", str(crs))
+        self._mid = (ent("GEOSPATIAL_COUNT", "1") + ent("GEOSPATIAL_DTYPE", str(np.dtype(dtype))) +
+                     ent("GEOSPATIAL_NODATA", "None"))
+        self._tail = ent("GEOSPATIAL_SPATIAL_TILING", "False")
+        self._num: Dict[Tuple[type, object, bool], str] = {}
+        self._ent: Dict[Tuple[str, str], bytes] = {}
+
+    @staticmethod
+    def _entry(k: str, v: str) -> bytes:
+        c = k.encode("ascii") + b"=" + v.encode("utf-8")
+        return struct.pack("<I", len(c)) + c
+
+    def _js(self, x) -> str:
+        """json.dumps of a number (float.__repr__ for finite floats), cached; -0.0 and 0.0 kept apart."""
+        key = (type(x), x, math.copysign(1.0, x) < 0 if isinstance(x, float) else False)
+        v = self._num.get(key)
+        if v is None:
+            v = self._num[key] = json.dumps(x)
+        return v
+
+    def _cached_entry(self, k: str, v: str) -> bytes:
+        e = self._ent.get((k, v))
+        if e is None:
+            e = self._ent[(k, v)] = self._entry(k, v)
+        return e
+
+    def header(self, tt: geotiff.Affine, w: int, h: int, tmin: float, tmax: float, frame_bytes: int) -> bytes:
+        js = self._js
+        left, bottom, right, top = geotiff.bounds_of(tt, w, h)
+        tr = "[" + ", ".join(js(v) for v in tt) + "]"
+        bd = '{"left": ' + js(left) + ', "bottom": ' + js(bottom) + ', "right": ' + js(right) + ', "top": ' + \
+             js(top) + "}"
+        ent = self._entry
+        body = b"".join((self._vendor, self._pre, self._cached_entry("GEOSPATIAL_WIDTH", str(w)),
+                         self._cached_entry("GEOSPATIAL_HEIGHT", str(h)), self._mid,
+                         self._cached_entry("GEOSPATIAL_DATA_MIN", str(tmin)),
+                         self._cached_entry("GEOSPATIAL_DATA_MAX", str(tmax)),
+                         ent("GEOSPATIAL_TRANSFORM", tr), ent("GEOSPATIAL_BOUNDS", bd), self._tail))
+        vc = container.block(container.BLOCK_VORBIS_COMMENT, body, False)
+        pad = container.mutagen_padding(86 - 4, len(self._si) + len(vc) + 4, frame_bytes)
+        return b"".join((b"fLaC", self._si, vc, container.block(container.BLOCK_PADDING, bytes(pad), True)))
+
+
 @dataclass
 class EncodedTiles:
     """Output of one GPU encode of all band-1 tiles."""
@@ -83,32 +143,106 @@ def encode_band_tiles(band: np.ndarray, tile_size: int, ctx: Optional[Context] =
     return EncodedTiles(tile_grid(H, W, tile_size), arena, off, mn, mx, sbps)
 
 
+def streaming_headers(enc: EncodedTiles, transform: geotiff.Affine, crs: Optional[str], width: int, height: int,
+                      tile_size: int, dtype, windows=None, frame_id0: int = 0, byte_offset0: int = 0):
+    """Per-tile headers and index entries of `enc`'s tiles (cli.py:702-759): (headers, frames entries, bytes)."""
+    windows = enc.windows if windows is None else windows
+    hb = TileHeaderBuilder(crs, dtype, enc.stream_bps)
+    headers: List[bytes] = []
+    frames: List[Dict] = []
+    total = byte_offset0
+    tile_bytes = np.diff(enc.tile_off)
+    for i, (col, row, w, h) in enumerate(windows):
+        tt = geotiff.window_transform(transform, col, row)
+        # sample rate of the tile: _calculate_audio_params on the (1, h, w) array -> shape0*shape1 = h
+        if h >= 1000000:
+            raise NotImplementedError("tile heights >= 1e6 rows change the sample rate; re-encode needed")
+        fb = int(tile_bytes[i])
+        hdr = hb.header(tt, w, h, float(enc.tile_min[i]), float(enc.tile_max[i]), fb)
+        xmin, ymax = tt.c, tt.f
+        frames.append({"frame_id": frame_id0 + i, "bbox": [xmin, ymax + (h * tt.e), xmin + (w * tt.a), ymax],
+                       "window": {"col_off": col, "row_off": row, "width": w, "height": h},
+                       "byte_offset": total, "byte_size": len(hdr) + fb})
+        headers.append(hdr)
+        total += len(hdr) + fb
+    return headers, frames, total - byte_offset0
+
+
+def streaming_head(index: Dict) -> bytes:
+    """[u32 BE index length][compact JSON index] (cli.py:769-773)."""
+    js = container.index_json(index)
+    return struct.pack(">I", len(js)) + js
+
+
 def assemble_streaming(enc: EncodedTiles, transform: geotiff.Affine, crs: Optional[str], width: int, height: int,
                        tile_size: int, dtype) -> Tuple[bytes, List[bytes], Dict]:
     """Index JSON + per-tile FLAC streams (header bytes + frames) -> (head, tile_streams, index)."""
+    headers, frames, _ = streaming_headers(enc, transform, crs, width, height, tile_size, dtype)
     index = {"crs": str(crs), "transform": list(transform), "width": width, "height": height,
-             "tile_size": tile_size, "frames": []}
-    streams: List[bytes] = []
-    total = 0
-    frames = enc.frames
-    for i, (col, row, w, h) in enumerate(enc.windows):
-        tt, bbox = tile_transform_and_bbox(transform, col, row, w, h)
-        # sample rate of the tile: _calculate_audio_params on the (1, h, w) array -> shape0*shape1 = h
-        sr, _ = audio_params(1, h, dtype)
-        body = frames[enc.tile_off[i]:enc.tile_off[i + 1]].tobytes()
-        if sr != 44100:
-            raise NotImplementedError("tile heights >= 1e6 rows change the sample rate; re-encode needed")
-        hdr = container.mutagen_header(1, enc.stream_bps, sr,
-                                       tile_tags(crs, tt, w, h, dtype, float(enc.tile_min[i]), float(enc.tile_max[i])),
-                                       len(body))
-        s = hdr + body
-        index["frames"].append({"frame_id": i, "bbox": bbox,
-                                "window": {"col_off": col, "row_off": row, "width": w, "height": h},
-                                "byte_offset": total, "byte_size": len(s)})
-        streams.append(s)
-        total += len(s)
-    js = container.index_json(index)
-    return struct.pack(">I", len(js)) + js, streams, index
+             "tile_size": tile_size, "frames": frames}
+    streams = [hdr + enc.frames[enc.tile_off[i]:enc.tile_off[i + 1]].tobytes() for i, hdr in enumerate(headers)]
+    return streaming_head(index), streams, index
+
+
+def write_tiles(fd: int, offset: int, headers: Sequence[bytes], enc: EncodedTiles, threads: int = 8) -> None:
+    """pwritev of (header, frames) pairs straight from the arena (no per-tile copies), tile ranges in parallel
+    threads (os.pwritev releases the GIL); the tiles land back to back from file offset `offset`."""
+    from concurrent.futures import ThreadPoolExecutor
+    n = len(headers)
+    if n == 0:
+        return
+    mv = memoryview(enc.frames)
+    sizes = np.array([len(h) for h in headers], dtype=np.int64) + np.diff(enc.tile_off)
+    starts = offset + np.concatenate(([0], np.cumsum(sizes)[:-1]))
+    off = enc.tile_off
+
+    def run(a: int, b: int):
+        i = a
+        while i < b:
+            j = min(b, i + 512)  # 1024 iovecs per call (IOV_MAX)
+            iov = []
+            for k in range(i, j):
+                iov.append(headers[k])
+                iov.append(mv[off[k]:off[k + 1]])
+            want = int(starts[j - 1] + sizes[j - 1] - starts[i])
+            done = os.pwritev(fd, iov, int(starts[i]))
+            if done != want:  # short write: finish byte-wise
+                buf = b"".join(bytes(x) for x in iov)
+                while done < want:
+                    done += os.pwrite(fd, buf[done:], int(starts[i]) + done)
+            i = j
+
+    k = max(1, min(threads, n // 64 or 1))
+    bounds = [n * t // k for t in range(k + 1)]
+    with ThreadPoolExecutor(k) as ex:
+        list(ex.map(lambda t: run(bounds[t], bounds[t + 1]), range(k)))
+
+
+def create_streaming_array(band: np.ndarray, transform: geotiff.Affine, crs: Optional[str], output: Path,
+                           tile_size: int = 1024, ctx: Optional[Context] = None,
+                           timings: Optional[Dict[str, float]] = None) -> Dict:
+    """cli.py:620-804 on an in-memory band-1 array: one GPU encode of every tile, headers and index on the host,
+    tiles written from the arena with parallel pwritev.  Returns the index; `timings` gets the stage seconds."""
+    tm = timings if timings is not None else {}
+    t0 = time.perf_counter()
+    H, W = band.shape
+    enc = encode_band_tiles(band, tile_size, ctx)
+    t1 = time.perf_counter()
+    headers, frames, body = streaming_headers(enc, transform, crs, W, H, tile_size, band.dtype)
+    index = {"crs": str(crs), "transform": list(transform), "width": W, "height": H, "tile_size": tile_size,
+             "frames": frames}
+    head = streaming_head(index)
+    t2 = time.perf_counter()
+    fd = os.open(output, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    try:
+        os.ftruncate(fd, len(head) + body)
+        os.pwrite(fd, head, 0)
+        write_tiles(fd, len(head), headers, enc)
+    finally:
+        os.close(fd)
+    t3 = time.perf_counter()
+    tm.update(encode_s=t1 - t0, index_s=t2 - t1, write_s=t3 - t2, total_s=t3 - t0)
+    return index
 
 
 def create_streaming(input_file: Path, output_file: Path, tile_size: int = 1024,
@@ -116,14 +250,8 @@ def create_streaming(input_file: Path, output_file: Path, tile_size: int = 1024,
     """cli.py:620-804 without the console output: writes the streaming file, returns the index."""
     r = geotiff.read(input_file)
     transform = r.transform or geotiff.Affine(1.0, 0.0, 0.0, 0.0, 1.0, 0.0)
-    band = np.ascontiguousarray(r.data[0])
-    enc = encode_band_tiles(band, tile_size, ctx)
-    head, streams, index = assemble_streaming(enc, transform, r.crs_string, r.width, r.height, tile_size, band.dtype)
-    with open(output_file, "wb") as fh:
-        fh.write(head)
-        for s in streams:
-            fh.write(s)
-    return index
+    return create_streaming_array(np.ascontiguousarray(r.data[0]), transform, r.crs_string, output_file, tile_size,
+                                  ctx)
 
 
 # ----------------------------------------------------------------------------- read / select

@@ -153,6 +153,20 @@ int frs_denormalize_device(frs_ctx *ctx, const int32_t *pcm_dev, int64_t n, int3
 int frs_denormalize(frs_ctx *ctx, const int32_t *pcm_host, int64_t n, int32_t pcm_bps, double data_min,
                     double data_max, int32_t out_dtype, void *out_host);
 
+/* Multi-GPU create-streaming (one process per GPU).  The reference's tile loop (cli.py:690-763) is
+ * serial; here tiles shard by contiguous tile rows and the only exchange is an RCCL all-gather (xGMI) of per-tile
+ * byte sizes, after which every rank writes its own tiles at their file offsets.  librccl.so is loaded at run
+ * time; rank 0 calls frs_comm_unique_id and the host ships the FRS_COMM_ID_BYTES bytes to every rank (any
+ * bootstrap: flac_raster_amd/distributed.py uses a TCP star), then each rank calls frs_comm_init with its context
+ * (one GPU per rank).  frs_comm_allgather_i64: `count` int64 per rank, host in/out, result in rank order;
+ * synchronous on the context's stream. */
+typedef struct frs_comm frs_comm;
+#define FRS_COMM_ID_BYTES 128
+int frs_comm_unique_id(uint8_t *id_out);
+int frs_comm_init(frs_ctx *ctx, const uint8_t *id, int32_t nranks, int32_t rank, frs_comm **out);
+void frs_comm_destroy(frs_comm *comm);
+int frs_comm_allgather_i64(frs_comm *comm, const int64_t *send_host, int64_t count, int64_t *recv_host);
+
 /* Device memory helpers so hosts need no other GPU runtime binding (no PyTorch in the codec path). */
 void *frs_dev_malloc(frs_ctx *ctx, int64_t bytes);
 void frs_dev_free(frs_ctx *ctx, void *ptr);

@@ -1,0 +1,130 @@
+"""Multi-rank create-streaming: tile-row sharding + the size all-gather + pwritev assembly.
+
+CPU tests run world-size 2 and 3 with the host exchange (TcpComm) and the oracle injected as the encoder; the GPU
+variants run two ranks on the one GPU of the box with the HIP encoder (RCCL needs one GPU per rank, so they also
+use the host exchange) and RCCL itself at world size 1.  Every variant must write the single-process file.
+"""
+import multiprocessing as mp
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+TRANSFORM = [10.0, 0.0, 500000.0, 0.0, -10.0, 4000000.0]
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _band(H=700, W=650, seed=11):
+    rng = np.random.default_rng(seed)
+    y, x = np.meshgrid(np.linspace(0, 20, H), np.linspace(0, 20, W), indexing="ij")
+    return (1000 + 300 * np.sin(x * 0.5) * np.cos(y * 0.3) + 50 * rng.random((H, W))).astype(np.int16)
+
+
+def _oracle_encode(slab, tile):
+    from flac_raster_amd.streaming import EncodedTiles, tile_grid
+    from oracle import oracle as O
+    arena, off, mn, mx = O.encode_tiles(slab, tile)
+    return EncodedTiles(tile_grid(*slab.shape, tile), arena, off, mn, mx, 16)
+
+
+def _worker(rank, world, port, out, band, tile, use_gpu):
+    sys.path.insert(0, str(ROOT))
+    from flac_raster_amd import distributed as D, geotiff
+    comm = D.TcpComm(rank, world, "127.0.0.1", port)
+    H, W = band.shape
+    tr0, tr1 = D.shard_tile_rows((H + tile - 1) // tile, world, rank)
+    slab = np.ascontiguousarray(band[tr0 * tile:min(tr1 * tile, H)])
+    ctx = None
+    if use_gpu:
+        from flac_raster_amd import _native
+        ctx = _native.Context(0)
+        encode = D.gpu_encoder(ctx)
+    else:
+        encode = _oracle_encode
+    D.create_streaming_sharded(slab, tr0 * tile, (H, W), geotiff.Affine(*TRANSFORM), "EPSG:32636", tile, Path(out),
+                               comm, encode)
+    comm.close()
+    if ctx is not None:
+        ctx.close()
+
+
+def _run_ranks(world, out, band, tile, use_gpu=False):
+    port = _free_port()
+    ctxm = mp.get_context("spawn")
+    procs = [ctxm.Process(target=_worker, args=(r, world, port, str(out), band, tile, use_gpu)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def _reference(band, tile):
+    from oracle import pipeline as P
+    return P.create_streaming(band, TRANSFORM + [0.0, 0.0, 1.0], "EPSG:32636", tile)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_create_streaming_matches_single_process(tmp_path, world):
+    band = _band()
+    out = tmp_path / "sharded.flac"
+    out.write_bytes(b"x" * 5_000_000)  # a larger stale file: the ranks never truncate below their data
+    _run_ranks(world, out, band, 256)
+    assert out.read_bytes() == _reference(band, 256)
+
+
+def test_shard_tile_rows_balanced():
+    from flac_raster_amd.distributed import shard_tile_rows
+    parts = [shard_tile_rows(79, 8, r) for r in range(8)]
+    assert parts[0][0] == 0 and parts[-1][1] == 79
+    assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+    assert {p[1] - p[0] for p in parts} <= {9, 10}
+
+
+def test_tcp_allgather_variable_sizes():
+    from flac_raster_amd.distributed import all_gather_sizes
+
+    class Fake:  # world 1
+        rank, world = 0, 1
+
+        @staticmethod
+        def allgather_i64(a):
+            return np.asarray(a)
+
+    assert list(all_gather_sizes(np.array([5, 6]), [2], Fake())) == [5, 6]
+
+
+@pytest.mark.gpu
+def test_sharded_two_ranks_gpu_encoder(tmp_path):
+    band = _band(1100, 900, 5)
+    out = tmp_path / "sharded_gpu.flac"
+    _run_ranks(2, out, band, 256, use_gpu=True)
+    assert out.read_bytes() == _reference(band, 256)
+
+
+@pytest.mark.gpu
+def test_rccl_comm_world_one(gpu_ctx, tmp_path, monkeypatch):
+    """RCCL through the C-ABI (frs_comm_*): a world-1 communicator all-gathers and drives the sharded writer."""
+    from flac_raster_amd import distributed as D, geotiff
+    monkeypatch.setenv("FRS_COMM_PORT", str(_free_port()))
+    comm = D.init_comm(gpu_ctx, "rccl", rank=0, world=1)
+    try:
+        assert list(comm.allgather_i64(np.array([3, -1, 2 ** 40]))) == [3, -1, 2 ** 40]
+        band = _band()
+        out = tmp_path / "rccl1.flac"
+        D.create_streaming_sharded(band, 0, band.shape, geotiff.Affine(*TRANSFORM), "EPSG:32636", 256, out, comm,
+                                   D.gpu_encoder(gpu_ctx))
+    finally:
+        comm.close()
+    assert out.read_bytes() == _reference(band, 256)

@@ -1,5 +1,6 @@
 """CPU tests of the product's host-side logic (containers, GeoTIFF, tile selection) -- no GPU calls."""
 import json
+import os
 import struct
 
 import numpy as np
@@ -112,3 +113,43 @@ def test_first_intersecting_matches_linear_scan():
         hits = streaming.intersecting(index, bbox)
         got = streaming.first_intersecting(index, bbox)
         assert (got is None and not hits) or (hits and got is hits[0]), bbox
+
+
+@pytest.mark.parametrize("crs,dtype,tr", [
+    ("EPSG:32636", np.int16, geotiff.Affine(10.0, 0.0, 500000.0, 0.0, -10.0, 4000000.0)),
+    (None, np.uint8, geotiff.Affine(0.5, 0.1, -0.0, 0.2, -0.5, 0.0)),   # rotated, negative zero
+    ("EPSG:4326", np.uint16, geotiff.Affine(1, 0, 0, 0, -1, 10)),       # integer coefficients
+])
+def test_tile_header_builder_equals_direct_path(crs, dtype, tr):
+    """The cached per-tile header builder writes the same bytes as tile_tags + mutagen_header."""
+    rng = np.random.default_rng(0)
+    grid = streaming.tile_grid(40000, 40000, 512)
+    b = streaming.TileHeaderBuilder(crs, dtype, 16)
+    for i in rng.integers(0, len(grid), 200):
+        col, row, w, h = grid[i]
+        tt, _ = streaming.tile_transform_and_bbox(tr, col, row, w, h)
+        mn, mx = float(rng.integers(0, 1000)), float(rng.integers(1000, 5000))
+        fb = int(rng.integers(0, 10 ** 7))
+        ref = container.mutagen_header(1, 16, 44100, streaming.tile_tags(crs, tt, w, h, dtype, mn, mx), fb)
+        assert b.header(tt, w, h, mn, mx, fb) == ref
+
+
+def test_streaming_writer_equals_assembled_bytes(tmp_path):
+    """create-streaming's file writer (parallel pwritev from the arena) == head + concatenated tile streams."""
+    rng = np.random.default_rng(3)
+    H, W, T = 1300, 2100, 256
+    grid = streaming.tile_grid(H, W, T)
+    sizes = rng.integers(100, 5000, len(grid))
+    off = np.concatenate(([0], np.cumsum(sizes))).astype(np.int64)
+    enc = streaming.EncodedTiles(grid, rng.integers(0, 256, int(off[-1]), dtype=np.uint8), off,
+                                 rng.random(len(grid)) * 100, 100 + rng.random(len(grid)) * 100, 16)
+    tr = geotiff.Affine(10.0, 0.0, 500000.0, 0.0, -10.0, 4000000.0)
+    head, streams, index = streaming.assemble_streaming(enc, tr, "EPSG:32636", W, H, T, np.int16)
+    headers, frames, body = streaming.streaming_headers(enc, tr, "EPSG:32636", W, H, T, np.int16)
+    assert frames == index["frames"] and body == sum(len(s) for s in streams)
+    out = tmp_path / "s.flac"
+    fd = os.open(out, os.O_WRONLY | os.O_CREAT)
+    streaming.write_tiles(fd, len(head), headers, enc, threads=4)
+    os.pwrite(fd, head, 0)
+    os.close(fd)
+    assert out.read_bytes() == head + b"".join(streams)
