@@ -98,8 +98,6 @@ int frs_ctx_create(int device, frs_ctx **out) {
     ctx->device = device;
     const char *fg = getenv("FRS_FORCE_GENERIC");
     ctx->force_generic = fg && fg[0] == '1';
-    const char *ab = getenv("FRS_ABLATE");
-    ctx->ablate = ab ? atoi(ab) : 0;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return FRS_E_HIP;
@@ -117,7 +115,7 @@ void frs_ctx_destroy(frs_ctx *ctx) {
     hipStreamSynchronize(ctx->stream);
     frs::prof_collect(ctx);
     DevBuf *bufs[] = {&ctx->tiles, &ctx->norms, &ctx->analysis, &ctx->slots, &ctx->frame_bytes, &ctx->frame_off,
-                      &ctx->scan_tmp, &ctx->window, &ctx->tile_sizes, &ctx->luts, &ctx->status, &ctx->frame_tile, &ctx->hdr_tab, &ctx->wave_tab, &ctx->plist, &ctx->raster_stage, &ctx->arena_stage, &ctx->host_pack,
+                      &ctx->window, &ctx->tile_sizes, &ctx->luts, &ctx->status, &ctx->frame_tile, &ctx->hdr_tab, &ctx->wave_tab, &ctx->plist, &ctx->raster_stage, &ctx->arena_stage, &ctx->host_pack,
                       &ctx->dec_cand, &ctx->dec_count, &ctx->dec_pcm, &ctx->dec_soff, &ctx->dec_next, &ctx->dec_status};
     for (DevBuf *b : bufs) b->release();
     ctx->pin.release();

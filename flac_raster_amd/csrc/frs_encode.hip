@@ -11,9 +11,8 @@
 //                    Levinson-Durbin, order guess, qlp quantisation        [fp64-VALU bound]
 //   k_encode_frames  workgroup = frame: candidate residuals, partition sums, Rice parameters, choice,
 //                    exact bit positions (block prefix scan) and LDS bit packing into a frame slot
-//   (scan)           exclusive scan of frame sizes -> arena offsets (tiles are consecutive frame runs)
+//   k_scan_sizes     exclusive scan of frame sizes -> arena offsets (tiles are consecutive frame runs)
 //   k_compact        workgroup = frame: CRC-16 (parallel GF(2) combine) + copy slot -> arena offset
-#include <hipcub/hipcub.hpp>
 
 #include <type_traits>
 
@@ -1206,6 +1205,37 @@ __global__ void __launch_bounds__(256) k_seal_partial(uint32_t *slots, int slot_
     }
 }
 
+// Exclusive scan of the generic path's frame sizes in one work-group: out[i] = sum(in[0..i)), out[n] = total.
+// Thread t owns the contiguous run [t c, (t + 1) c); run totals are scanned through LDS by wave shuffles.
+constexpr int kScanThreads = 1024;
+__global__ void __launch_bounds__(kScanThreads) k_scan_sizes(const int64_t *in, int64_t *out, int64_t n) {
+    __shared__ int64_t wsum[kScanThreads / 64];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int64_t c = (n + kScanThreads - 1) / kScanThreads;
+    const int64_t a = min(n, (int64_t)t * c), b = min(n, a + c);
+    int64_t run = 0;
+    for (int64_t i = a; i < b; i++) run += in[i];
+    int64_t x = run;  // inclusive scan of the run totals within the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    int64_t base = 0, total = 0;
+    for (int k = 0; k < kScanThreads / 64; k++) {
+        base += k < wv ? wsum[k] : 0;
+        total += wsum[k];
+    }
+    int64_t acc = base + x - run;
+    for (int64_t i = a; i < b; i++) {
+        out[i] = acc;
+        acc += in[i];
+    }
+    if (t == 0) out[n] = total;
+}
+
 __global__ void k_gather_tile_off(const int64_t *frame_off, const TileGeom *tiles, int ntiles, int64_t total,
                                   int64_t *tile_off) {
     int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1216,7 +1246,7 @@ __global__ void k_gather_tile_off(const int64_t *frame_off, const TileGeom *tile
 // =================================================================================================
 // FAST PATH (16-bit mono streams: create-streaming band-1 tiles, converter bps 16)
 //   k_build_lut     per tile: pcm = lut[x - min] for x - min in [0, R] (exact double path, once per value)
-//   k_analyze_v2    lane = frame; 64-sample chunks loaded as 8 x 16 B per lane (no L1 reuse needed),
+//   k_analyze_v3    lane = frame; 64-sample chunks loaded as 8 x 16 B per lane (no L1 reuse needed),
 //                   LUT normalisation, wave-uniform window from LDS, 9 fp64 FMA chains per lane
 //   k_encode_v3     persistent WGs, wave = frame, 64 consecutive samples per lane held as packed int16
 //                   pairs: fixed totals, v_dot2 residuals, partition sums by lane shuffles, Rice search,
@@ -1411,7 +1441,7 @@ __device__ inline void norm_block8(const Chunk64<DT> &ch, int b, const TileNorm 
 }
 
 // wasted bits, LPC order choice (expected bits), Levinson coefficients and quantisation of one frame from its
-// windowed autocorrelation sums (stream_encoder.c process_subframe_ / lpc.c; shared by k_analyze_v2/v3)
+// windowed autocorrelation sums (stream_encoder.c process_subframe_ / lpc.c)
 __device__ inline SubAnalysis analysis_finish(const double *acc, uint32_t or_acc, int n, const EncodeParams &P) {
     SubAnalysis A;
     A.n = n;
@@ -1514,97 +1544,8 @@ __device__ inline SubAnalysis analysis_finish(const double *acc, uint32_t or_acc
     return A;
 }
 
-template <int DT>
-__global__ void __launch_bounds__(256) k_analyze_v2(const typename Elem<DT>::T *raster, EncodeParams P,
-                                                   const TileGeom *tiles, const TileNorm *norms,
-                                                   const int16_t *luts, const float *__restrict__ window,
-                                                   SubAnalysis *out, const int32_t *__restrict__ ftile) {
-    using T = typename Elem<DT>::T;
-    const float *__restrict__ swin = window;  // uniform index in every lane: scalar (SMEM) loads
-    __shared__ int16_t slut[4][kLutCap];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t f = ((int64_t)blockIdx.x * 4 + wave) * 64 + lane;
-    const bool live = f < P.nframes;
-    const int64_t fq = live ? f : P.nframes - 1;  // dead lanes re-read the last frame (no out-of-tile loads)
-    const int t = ftile[fq];
-    const TileGeom g = tiles[t];
-    const int64_t s0 = (fq - g.frame_base) * P.blocksize;
-    const int64_t tile_px = (int64_t)g.h * g.w;
-    const int n = live ? (int)min((int64_t)P.blocksize, tile_px - s0) : 0;
-    TileNorm tn = norms[t];
-    // LUT: one per wave when the wave's frames share a tile; other LUT tiles take the exact division
-    const int t0 = __shfl(t, 0);
-    const bool uni = __all(t == t0);
-    const bool wave_lut = uni && tn.mode == kNormLut;
-    if (wave_lut) {
-        const int64_t R = tn.imax - tn.imin;
-        const int16_t *src = luts + (int64_t)t0 * kLutCap;
-        for (int64_t d = lane; d <= R; d += 64) slut[wave][d] = src[d];
-    }
-    __syncthreads();
-    const int16_t *lut = wave_lut ? slut[wave] : luts + (int64_t)t * kLutCap;
-    const T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
-    const bool vec = P.vec_ok && (g.w % 64) == 0;
-
-    uint32_t or_acc = 0;
-    double acc[kMaxLpc + 1];
-#pragma unroll
-    for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
-    double prev[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) prev[j] = 0.0;
-
-    // fast path: every frame is a full block (host guarantees), 64 chunks of 64 samples per lane; a
-    // row/column cursor walks the tile (no per-chunk division); the next chunk's loads are issued before
-    // the current chunk's FMAs
-    const uint32_t r0 = udiv_inv((uint32_t)s0, (uint32_t)g.w, 1.0 / (double)g.w);
-    int64_t crow = r0;
-    int ccol = (int)((uint32_t)s0 - r0 * (uint32_t)g.w);
-    auto advance = [&]() {
-        ccol += 64;
-        while (ccol >= g.w) {
-            ccol -= g.w;
-            crow++;
-        }
-    };
-    for (int c = 0; c < kMaxBlock / 64; c++) {
-        const int i0 = c * 64;
-        Chunk64<DT> chc;
-        chc.load(base, P.row_stride, g.w, crow, ccol, vec, 64);
-        advance();
-#pragma unroll
-        for (int half = 0; half < 2; half++) {
-        float xf[64];
-        norm_chunk<DT>(chc, tn, lut, [&](int j, int32_t x) {
-            if ((j >> 5) == half) {
-                or_acc |= (uint32_t)x;
-                xf[j] = (float)x;
-            }
-        });
-#pragma unroll
-        for (int b = half * 4; b < half * 4 + 4; b++) {
-            double cur[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) cur[j] = (double)(xf[b * 8 + j] * swin[i0 + b * 8 + j]);
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-#pragma unroll
-                for (int l = 0; l <= kMaxLpc; l++) {
-                    const double other = (j - l >= 0) ? cur[j - l] : prev[8 + j - l];
-                    acc[l] = fma(cur[j], other, acc[l]);
-                }
-            }
-#pragma unroll
-            for (int j = 0; j < 8; j++) prev[j] = cur[j];
-        }
-        }
-    }
-    if (!live) return;
-    out[f] = analysis_finish(acc, or_acc, n, P);
-}
-
 // ------------------------------------------------------------------------------ k_analyze_v3
-// Same per-frame arithmetic as k_analyze_v2 (lane = frame, libFLAC's sequential fp64 autocorrelation), laid
+// Lane = frame (libFLAC's sequential fp64 autocorrelation per lane), laid
 // out for occupancy and memory-level parallelism: a wave takes up to 64 frames of ONE tile (host wave table),
 // so the normaliser is wave-uniform and chosen once (LUT in LDS read by ds_read / zeros / fast division /
 // exact division) instead of a per-sample switch; each lane loads its next 64 samples as one 128-byte line
@@ -2000,7 +1941,6 @@ constexpr int kFrameWordsV3 = 2176;  // 69632 bits >= worst exact frame (DESIGN.
 constexpr int kXpowBytes = kFrameWordsV3 * 4 + 64;  // multiple of 64 (LDS split tables)
 __constant__ uint16_t c_crc16x4[4][256];           // T_k[v] = CRC-16 of byte v followed by k zero bytes
 __device__ uint16_t g_xpow_bytes[kXpowBytes];      // x^(8m) mod P for m bytes
-__device__ unsigned long long g_lb_stats[4];       // diagnostics (FRS_ABLATE bit 64): frames, rounds, spins, distance
 
 constexpr int kXpowHi = (kXpowBytes + 63) / 64;
 struct EncV3Shared {
@@ -2113,9 +2053,7 @@ __device__ inline void resolve_and_store(const EncodeParams &P, PendingFrame &pf
     const bool l0 = lane == 0;
     // ---- decoupled look-back for the exclusive prefix (kPer predecessors per lane and round)
     uint64_t prefix = 0;
-    if (P.ablate & 1) {
-        prefix = (uint64_t)f * 8320;  // diagnostic: fixed slots, no waiting
-    } else if (f > 0) {
+    if (f > 0) {
         constexpr int kPer = 1;
         int64_t hi = f - 1;
         uint64_t accum = 0;
@@ -2158,28 +2096,20 @@ __device__ inline void resolve_and_store(const EncodeParams &P, PendingFrame &pf
                 continue;
             }
             accum += dpp_wave_sum_u64(mine);
-            if (fl < 64) {
-                if ((P.ablate & 64) && l0) {
-                    atomicAdd(&g_lb_stats[0], 1ull);
-                    atomicAdd(&g_lb_stats[1], (unsigned long long)((f - 1 - hi) / (64 * kPer) + 1));
-                    atomicAdd(&g_lb_stats[2], (unsigned long long)spins);
-                    atomicAdd(&g_lb_stats[3], (unsigned long long)(f - 1 - hi + fl * kPer + first_i));
-                }
-                break;
-            }
+            if (fl < 64) break;
             hi -= 64 * kPer;
         }
         prefix = accum;
     }
     if (l0) {
-        if (f > 0 && !(P.ablate & 1))
+        if (f > 0)
             __hip_atomic_store(&status[f], kFlagIncl | (prefix + fbytes), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         frame_off[f] = (int64_t)prefix;
     }
     const FbMap M = pf.map;
     if ((int64_t)(prefix + fbytes) > arena_cap) {
         if (l0) atomicOr(err, 16);
-    } else if (!(P.ablate & 16) && fbytes) {
+    } else if (fbytes) {
         // ---- store [prefix, prefix + fbytes): bytes up to 16-B alignment, 16-B chunks, byte tail
         uint8_t *dst = arena + prefix;
         const uint32_t a0 = min((uint32_t)fbytes, (uint32_t)((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15));
@@ -2708,7 +2638,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         const uint32_t shl = 32u - (uint32_t)sbps;
 #pragma unroll
         for (int j = 0; j < 64; j++) lds_put_left(fbuf, M, p0 + (uint32_t)j * sbps, (uint32_t)X(j) << shl);
-    } else if (type >= 2 && ok && !(P.ablate & 4)) {
+    } else if (type >= 2 && ok) {
         // code = stop bit + k low bits, left-aligned: (u << (31 - k)) with the stop bit forced on
         const uint32_t sh = 31u - (uint32_t)k, oneL = 0x80000000u, lowL = (k ? (0xFFFFFFFFu >> (32 - k)) : 0u) << sh;
 #pragma unroll
@@ -2734,7 +2664,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS atomics have landed
     __builtin_amdgcn_wave_barrier();
     uint32_t crc = 0;
-    if (ok && !(P.ablate & 2)) {
+    if (ok) {
         // slice-by-4 over 32-bit words, one contiguous word range per lane, combined with x^(8m) factors
         const uint32_t nfw = body >> 2, tail = body & 3;
         // lane L takes column L of the buffer (words L C .. L C + C - 1), so at each step the lanes read one row:
@@ -2983,7 +2913,6 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     P.ntiles = ntiles;
     P.norm_mode = d->norm_mode;
     P.vec_ok = 0;
-    P.ablate = ctx->ablate;
 
     int rc = upload_tables(ctx);
     if (rc) return rc;
@@ -3054,7 +2983,7 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     // Tile stats on the fast path (16-bit samples, 16-B aligned rows, one wave per tile): fused into the analysis
     // launch (k_analyze_v3<DT, false, true>: min/max, parameters and LUT per wave).  Otherwise (and with
     // FRS_ABLATE 4096) the stats kernels run before the analysis.
-    const bool fuse_stats = fast && stats_vec && sizeof(T) == 2 && one_wave_tiles && !(P.ablate & (4096 | 256));
+    const bool fuse_stats = fast && stats_vec && sizeof(T) == 2 && one_wave_tiles;
     // 1. tile stats
     if (!fuse_stats) {
         prof_begin(ctx, "stats", &ev);
@@ -3088,11 +3017,7 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         FRS_HIP(ctx->frame_tile.ensure(sizeof(int32_t) * nframes));
         k_frame_tile<<<ntiles, 64, 0, st>>>(dtiles, ntiles, ctx->frame_tile.as<int32_t>());
         prof_begin(ctx, "analyze", &ev);
-        if (P.ablate & 256) {  // diagnostics: the previous analysis kernel (A/B)
-            k_analyze_v2<DT><<<(unsigned)((nframes + 255) / 256), 256, 0, st>>>(
-                raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(), ctx->window.as<float>(), dana,
-                ctx->frame_tile.as<int32_t>());
-        } else {
+        {
             // wave table: (tile, first frame) per wave, up to 64 frames of one tile each
             int2 *wt = ctx->pin.at<int2>(pin_wt);
             int nwaves = 0;
@@ -3213,16 +3138,6 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                                                             hdr_n, ctx->slots.as<uint32_t>(), dpbytes);
         }
         prof_end(ctx, "encode", ev);
-        if (P.ablate & 64) {
-            unsigned long long st4[4];
-            FRS_HIP(hipMemcpyFromSymbolAsync(st4, HIP_SYMBOL(g_lb_stats), sizeof(st4), 0, hipMemcpyDeviceToHost, st));
-            FRS_HIP(hipStreamSynchronize(st));
-            fprintf(stderr, "[lookback] frames %llu rounds/frame %.3f spins/frame %.3f dist/frame %.1f\n", st4[0],
-                    (double)st4[1] / std::max(1ull, st4[0]), (double)st4[2] / std::max(1ull, st4[0]),
-                    (double)st4[3] / std::max(1ull, st4[0]));
-            const unsigned long long z[4] = {0, 0, 0, 0};
-            FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_lb_stats), z, sizeof(z), 0, hipMemcpyHostToDevice, st));
-        }
         FRS_HIP(ctx->host_pack.ensure(res_bytes));
         int64_t *dpack = ctx->host_pack.as<int64_t>();
         k_fast_finish<<<(ntiles + 1 + 255) / 256, 256, 0, st>>>(ctx->frame_off.as<int64_t>(), dstatus, dtiles, dnorms,
@@ -3267,15 +3182,8 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                                                                    ctx->slots.as<uint32_t>(),
                                                                    ctx->frame_bytes.as<int64_t>(), err_flag, nullptr);
     prof_end(ctx, "encode", ev);
-    // 4. offsets
-    size_t tmp_bytes = 0;
-    FRS_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp_bytes, ctx->frame_bytes.as<int64_t>(),
-                                             ctx->frame_off.as<int64_t>(), (int)(nframes + 1), st));
-    FRS_HIP(ctx->scan_tmp.ensure(tmp_bytes));
-    // frame_bytes[nframes] must be 0 for the total
-    FRS_HIP(hipMemsetAsync(ctx->frame_bytes.as<int64_t>() + nframes, 0, sizeof(int64_t), st));
-    FRS_HIP(hipcub::DeviceScan::ExclusiveSum(ctx->scan_tmp.ptr, tmp_bytes, ctx->frame_bytes.as<int64_t>(),
-                                             ctx->frame_off.as<int64_t>(), (int)(nframes + 1), st));
+    // 4. offsets (frame_off[nframes] = total)
+    k_scan_sizes<<<1, kScanThreads, 0, st>>>(ctx->frame_bytes.as<int64_t>(), ctx->frame_off.as<int64_t>(), nframes);
     int64_t total = 0;
     int errv = 0;
     FRS_HIP(hipMemcpyAsync(&total, ctx->frame_off.as<int64_t>() + nframes, sizeof(int64_t), hipMemcpyDeviceToHost, st));

@@ -67,11 +67,10 @@ struct frs_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     // encode scratch
-    DevBuf tiles, norms, analysis, slots, frame_bytes, frame_off, scan_tmp, window, tile_sizes, luts, status, frame_tile,
+    DevBuf tiles, norms, analysis, slots, frame_bytes, frame_off, window, tile_sizes, luts, status, frame_tile,
         hdr_tab, wave_tab, plist;
     int hdr_tab_n = -1, hdr_tab_sr = -1;  // cached frame-header table (fast encode path)
     bool force_generic = false;  // testing: route every job through the generic kernels
-    int ablate = 0;              // diagnostics: FRS_ABLATE bitmask (outputs invalid when set)
     // host staging (pinned)
     DevBuf raster_stage, arena_stage;  // device copies for the host-pointer entry points
     HostPin pin;                       // pinned staging of the fast encode path (tiles, wave table, results)
