@@ -243,3 +243,26 @@ def gpu_encoder(ctx):
     """The production `encode` of create_streaming_sharded: the rank's GPU codec."""
     from .streaming import encode_band_tiles
     return lambda slab, tile: encode_band_tiles(slab, tile, ctx)
+
+
+def create_streaming_distributed(input_file: Path, output_file: Path, tile_size: int = 1024,
+                                 backend: Optional[str] = None) -> dict:
+    """One rank of `create-streaming` over the launcher's ranks: reads the GeoTIFF, encodes its tile rows on GPU
+    LOCAL_RANK, all-gathers the tile sizes and writes its tiles into the shared output file.  backend: "rccl"
+    (default) or "tcp" ($FRS_COMM_BACKEND; the host exchange, e.g. for ranks sharing one GPU in tests)."""
+    from ._native import Context, device_count
+    backend = backend or os.environ.get("FRS_COMM_BACKEND", "rccl")
+    rank, world, local_rank = env_rank_world()
+    r = geotiff.read(input_file)
+    transform = r.transform or geotiff.Affine(1.0, 0.0, 0.0, 0.0, 1.0, 0.0)
+    H, W = r.height, r.width
+    tr0, tr1 = shard_tile_rows((H + tile_size - 1) // tile_size, world, rank)
+    slab = np.ascontiguousarray(r.data[0, tr0 * tile_size:min(tr1 * tile_size, H)])
+    ctx = Context(local_rank % max(1, device_count()))
+    comm = init_comm(ctx, backend)
+    try:
+        return create_streaming_sharded(slab, tr0 * tile_size, (H, W), transform, r.crs_string, tile_size,
+                                        Path(output_file), comm, gpu_encoder(ctx))
+    finally:
+        comm.close()
+        ctx.close()

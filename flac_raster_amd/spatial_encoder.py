@@ -178,3 +178,80 @@ def load_spatial_index(flac_path: Path) -> SpatialIndex:
                                   fd["window"]["height"]), fd["byte_offset"], fd["byte_size"])
               for fd in data["frames"]]
     return SpatialIndex(frames, data["crs"], geotiff.Affine(*data["transform"][:6]))
+
+
+class SpatialFLACStreamer:
+    """HTTP-range streaming of raw-frames spatial FLAC files (reference spatial_encoder.py:376-507).
+
+    The index comes from the embedded GEOSPATIAL_SPATIAL_INDEX tag (for URLs: the first MiB through one Range
+    request, spatial_encoder.py:398) or the ``.spatial.json`` sidecar.  Its byte offsets are the reference's
+    pre-rewrite offsets (stale by the first stream's header growth) and are served as they are.
+    One divergence: the reference's ``stream_bbox_data`` calls ``.startswith`` on a ``Path`` and fails for local
+    files (Q7); here local paths (str or Path) are read with seek/read.
+    """
+
+    def __init__(self, flac_path):
+        self.flac_path = flac_path
+        self.is_url = isinstance(flac_path, str) and flac_path.startswith(("http://", "https://"))
+        self.logger = logging.getLogger("flac_raster.spatial_streamer")
+        self.spatial_index = self._load_spatial_index()
+
+    def _load_spatial_index(self) -> SpatialIndex:
+        data = None
+        try:
+            if self.is_url:
+                import requests
+                r = requests.get(self.flac_path, headers={"Range": "bytes=0-1048575"}, stream=True)
+                r.raise_for_status()
+                head = r.content
+            else:
+                with open(self.flac_path, "rb") as fh:
+                    head = fh.read(1 << 20)
+            enc = container.parse_metadata(head).tag("GEOSPATIAL_SPATIAL_INDEX")
+            if enc is None:
+                raise ValueError("No embedded spatial index found")
+            self.logger.info("Reading spatial index from embedded FLAC metadata")
+            data = json.loads(gzip.decompress(base64.b64decode(enc.encode("ascii"))).decode("utf-8"))
+        except Exception as e:  # reference: any failure -> sidecar (spatial_encoder.py:428-440)
+            self.logger.warning(f"Failed to read embedded metadata: {e}")
+            self.logger.info("Falling back to sidecar file")
+            side = Path(self.flac_path).with_suffix(".spatial.json")
+            if not side.exists():
+                raise FileNotFoundError(f"Spatial index not found in FLAC metadata or sidecar file: {side}")
+            data = json.loads(side.read_text())
+        frames = [SpatialFrame(fd["frame_id"], tuple(fd["bbox"]),
+                               Window(fd["window"]["col_off"], fd["window"]["row_off"], fd["window"]["width"],
+                                      fd["window"]["height"]), fd["byte_offset"], fd["byte_size"])
+                  for fd in data["frames"]]
+        return SpatialIndex(frames, data["crs"], geotiff.Affine(*data["transform"][:6]))
+
+    def get_byte_ranges_for_bbox(self, bbox) -> List[Tuple[int, int]]:
+        """Inclusive (start, end) byte ranges of the frames intersecting bbox, sorted and merged when overlapping or
+        adjacent (spatial_encoder.py:464-484)."""
+        ranges = sorted((f.byte_offset, f.byte_offset + f.byte_size - 1)
+                        for f in self.spatial_index.query_bbox(bbox) if f.byte_size > 0)
+        merged: List[Tuple[int, int]] = []
+        for start, end in ranges:
+            if merged and start <= merged[-1][1] + 1:
+                merged[-1] = (merged[-1][0], max(merged[-1][1], end))
+            else:
+                merged.append((start, end))
+        self.logger.info(f"Found {len(merged)} byte ranges for bbox {bbox}")
+        return merged
+
+    def stream_bbox_data(self, bbox) -> bytes:
+        """The bytes of those ranges, concatenated (spatial_encoder.py:486-507)."""
+        chunks = []
+        ranges = self.get_byte_ranges_for_bbox(bbox)
+        if self.is_url:
+            import requests
+            for start, end in ranges:
+                r = requests.get(self.flac_path, headers={"Range": f"bytes={start}-{end}"})
+                r.raise_for_status()
+                chunks.append(r.content)
+        else:
+            with open(self.flac_path, "rb") as fh:
+                for start, end in ranges:
+                    fh.seek(start)
+                    chunks.append(fh.read(end - start + 1))
+        return b"".join(chunks)
