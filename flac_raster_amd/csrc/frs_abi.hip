@@ -98,6 +98,8 @@ int frs_ctx_create(int device, frs_ctx **out) {
     ctx->device = device;
     const char *fg = getenv("FRS_FORCE_GENERIC");
     ctx->force_generic = fg && fg[0] == '1';
+    const char *dl = getenv("FRS_DECODE_LANE");
+    ctx->decode_lane = dl ? (dl[0] == '1' ? 1 : 0) : -1;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return FRS_E_HIP;
@@ -116,7 +118,7 @@ void frs_ctx_destroy(frs_ctx *ctx) {
     frs::prof_collect(ctx);
     DevBuf *bufs[] = {&ctx->tiles, &ctx->norms, &ctx->analysis, &ctx->slots, &ctx->frame_bytes, &ctx->frame_off,
                       &ctx->window, &ctx->tile_sizes, &ctx->luts, &ctx->status, &ctx->frame_tile, &ctx->hdr_tab, &ctx->wave_tab, &ctx->plist, &ctx->raster_stage, &ctx->arena_stage, &ctx->host_pack,
-                      &ctx->dec_cand, &ctx->dec_count, &ctx->dec_pcm, &ctx->dec_soff, &ctx->dec_next, &ctx->dec_status};
+                      &ctx->dec_cand, &ctx->dec_count, &ctx->dec_pcm, &ctx->dec_soff, &ctx->dec_next, &ctx->dec_status, &ctx->dec_fb};
     for (DevBuf *b : bufs) b->release();
     ctx->pin.release();
     hipStreamDestroy(ctx->stream);

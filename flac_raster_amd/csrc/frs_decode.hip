@@ -169,6 +169,7 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_select(const uint8_t *blob
             __hip_atomic_store(&status[0], tag | kSelIncl | (uint64_t)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             counts[1] = 0;  // nvalid, bad: zeroed here (the later kernels of this call run after this one)
             counts[2] = 0;
+            counts[3] = 0;  // frames queued for the wave decoder by the lane decoder
         } else {
             __hip_atomic_store(&status[ord], tag | kSelAgg | (uint64_t)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             for (int64_t j = ord - 1;;) {
@@ -1364,24 +1365,20 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
 // decodes from LDS (bit refills are LDS reads instead of dependent global loads).  Frames larger than the stage
 // are decoded straight from global memory.  Multi-channel and wide streams.  Under a fused decode the int32
 // samples land in the `pcm` scratch first and the wave de-normalises the frame from there.
-__global__ void __launch_bounds__(64) k_decode_frames_wave(const uint8_t *blob, const int64_t *soff, int ns,
-                                                          const int64_t *poff, const int64_t *cpos,
-                                                          const int64_t *ends, const int64_t *fbase,
-                                                          const int64_t *frame_cand, int64_t nframes, int channels,
-                                                          int stream_bps, int32_t *pcm, int blocksize, int *nvalid,
-                                                          DecOut dout) {
-    __shared__ uint32_t stage[kDecStageWords + 4];
-    __shared__ int32_t resbuf[kDecResMax];
-    const int64_t fi = blockIdx.x;
-    if (fi >= nframes) return;
+__device__ inline void wave_decode_frame(int64_t fi, uint32_t *stage, int32_t *resbuf, const uint8_t *blob,
+                                         const int64_t *soff, int ns, const int64_t *poff, const int64_t *cpos,
+                                         const int64_t *ends, const int64_t *fbase, const int64_t *frame_cand,
+                                         int channels, int stream_bps, int32_t *pcm, int blocksize, int *nvalid,
+                                         const DecOut &dout) {
     const int lane = threadIdx.x;
     const int64_t ci = frame_cand[fi];
-    if (ci < 0 || ends[ci] < 0) return;  // not on a verified chain (the host reports it)
+    if (ci < 0 || ends[ci] < 0) return;  // (block-uniform) not on a verified chain (the host reports it)
     const int64_t fpos = cpos[ci], fend = ends[ci];
     const int s = stream_of(soff, ns, fpos);
     const int64_t send = soff[s + 1];
     const int64_t wb = fpos >> 2, we = (fend + 3) >> 2;
     const bool staged = we - wb <= kDecStageWords;
+    __syncthreads();  // the stage's previous readers are done
     if (staged)
         for (int64_t k = lane; k < we - wb + 4; k += 64) stage[k] = load_word_guarded(blob, wb + k, send);
     __syncthreads();
@@ -1400,6 +1397,244 @@ __global__ void __launch_bounds__(64) k_decode_frames_wave(const uint8_t *blob, 
     const int64_t e0 = (poff[s] + first) * channels;
     const float2 dnp = dout.dn[s];
     for (int64_t i = lane; i < n; i += 64) dn_store(dout, e0 + i, pcm[e0 + i], dnp);
+}
+
+__global__ void __launch_bounds__(64) k_decode_frames_wave(const uint8_t *blob, const int64_t *soff, int ns,
+                                                          const int64_t *poff, const int64_t *cpos,
+                                                          const int64_t *ends, const int64_t *fbase,
+                                                          const int64_t *frame_cand, int64_t nframes, int channels,
+                                                          int stream_bps, int32_t *pcm, int blocksize, int *nvalid,
+                                                          DecOut dout) {
+    __shared__ uint32_t stage[kDecStageWords + 4];
+    __shared__ int32_t resbuf[kDecResMax];
+    const int64_t fi = blockIdx.x;
+    if (fi >= nframes) return;
+    wave_decode_frame(fi, stage, resbuf, blob, soff, ns, poff, cpos, ends, fbase, frame_cand, channels, stream_bps,
+                      pcm, blocksize, nvalid, dout);
+}
+
+// The frames the lane decoder queued (layouts it does not take), each by one wave; the grid strides over the
+// device-side count, so no host sync separates the two launches.
+__global__ void __launch_bounds__(64) k_decode_frames_wave_list(const uint8_t *blob, const int64_t *soff, int ns,
+                                                               const int64_t *poff, const int64_t *cpos,
+                                                               const int64_t *ends, const int64_t *fbase,
+                                                               const int64_t *frame_cand, int channels, int stream_bps,
+                                                               int32_t *pcm, int blocksize, int *nvalid, DecOut dout,
+                                                               const int32_t *list, const int *count) {
+    __shared__ uint32_t stage[kDecStageWords + 4];
+    __shared__ int32_t resbuf[kDecResMax];
+    const int nl = *count;
+    for (int j = blockIdx.x; j < nl; j += gridDim.x)
+        wave_decode_frame(list[j], stage, resbuf, blob, soff, ns, poff, cpos, ends, fbase, frame_cand, channels,
+                          stream_bps, pcm, blocksize, nvalid, dout);
+}
+
+// ------------------------------------------------------------------ lane-per-frame decoder (batched decodes)
+// Throughput form for decodes of many frames (a whole arena, FLAC -> TIFF of a large raster): one lane per frame.
+// Each lane walks its own frame with a 64-bit bit cache refilled one big-endian dword at a time from global memory
+// (a lane's successive loads hit the same cache lines) and restores the samples with the LPC recurrence on an
+// eight-register ring, eight samples per unrolled step (compile-time ring slots: no register indexing); FIXED
+// predictors are order-<=4 LPC with shift 0, VERBATIM is order 0 with raw residuals.  Mono streams of <= 16-bit
+// samples whose prediction fits 32 bits (the pipelined decoder's condition); anything else is queued for
+// k_decode_frames_wave_list.  A frame counts as valid when its subframe ends exactly at the CRC-16 footer found
+// by the span check.
+struct LaneReader {
+    const uint8_t *blob;
+    int64_t wb;   // byte offset of the next dword to load (a multiple of 4)
+    int64_t end;  // stream end: loads never touch bytes at or past it
+    uint64_t c;   // left-aligned bit cache
+    int n;        // valid bits in c (> 32 between calls)
+    bool bad;
+    __device__ inline void refill() {  // n <= 32
+        c |= (uint64_t)__builtin_bswap32(load_word_guarded(blob, wb >> 2, end)) << (32 - n);
+        n += 32;
+        wb += 4;
+    }
+    __device__ inline void init(const uint8_t *b, int64_t pos, int64_t e) {
+        blob = b;
+        end = e;
+        wb = pos & ~(int64_t)3;
+        c = 0;
+        n = 0;
+        bad = false;
+        refill();
+        refill();
+        const int skip = (int)(pos & 3) * 8;
+        c <<= skip;
+        n -= skip;
+    }
+    __device__ inline uint32_t bits(int k) {  // 0 <= k <= 32
+        const uint32_t v = k ? (uint32_t)(c >> (64 - k)) : 0u;
+        c = k ? c << k : c;
+        n -= k;
+        if (n <= 32) refill();
+        return v;
+    }
+    __device__ inline int32_t sbits(int k) {
+        const uint32_t v = bits(k);
+        return (k == 0 || k == 32) ? (int32_t)v : ((int32_t)(v << (32 - k)) >> (32 - k));
+    }
+    __device__ inline uint32_t unary() {  // zeros before the next 1 (consumed)
+        uint32_t q = 0;
+        int z = c ? __builtin_clzll(c) : 64;
+        while (z >= n) {  // rare: a run longer than the cache
+            q += (uint32_t)n;
+            c = 0;
+            n = 0;
+            refill();
+            if (wb > end + 8) {
+                bad = true;
+                return q;
+            }
+            z = c ? __builtin_clzll(c) : 64;
+        }
+        q += (uint32_t)z;
+        c = (z + 1 >= 64) ? 0 : (c << (z + 1));
+        n -= z + 1;
+        if (n <= 32) refill();
+        return q;
+    }
+    __device__ inline int64_t pos() const { return wb * 8 - n; }  // bit position from the blob start
+};
+
+__global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob, const int64_t *soff, int ns,
+                                                           const int64_t *poff, const int64_t *cpos,
+                                                           const int64_t *ends, const int64_t *fbase,
+                                                           const int64_t *frame_cand, int64_t nframes,
+                                                           int stream_bps, int32_t *pcm, int blocksize, int *nvalid,
+                                                           DecOut dout, int32_t *fb_list, int *fb_count) {
+    const int64_t fi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool ok = false;
+    if (fi < nframes) {
+        const int64_t ci = frame_cand[fi];
+        const int64_t fend = ci >= 0 ? ends[ci] : -1;
+        if (fend >= 0) {
+            const int64_t fpos = cpos[ci];
+            const int s = stream_of(soff, ns, fpos);
+            const int64_t send = soff[s + 1];
+            const int64_t nsamp = poff[s + 1] - poff[s];
+            const int64_t kk = fi - fbase[s];
+            const int64_t first = kk * blocksize;
+            const FrameHdr cd = parse_header(blob, fpos, send, 1, stream_bps);
+            if (cd.ok && cd.frame_no == kk && cd.bs <= blocksize && first + cd.bs <= nsamp) {
+                const int bs = cd.bs;
+                const int64_t obase = poff[s] + first;
+                const bool fused = dout.out != nullptr;
+                const float2 dnp = fused ? dout.dn[s] : make_float2(0.f, 0.f);
+                LaneReader br;
+                br.init(blob, fpos + cd.hdr_len, send);
+                br.bits(1);
+                const int t = (int)br.bits(6);
+                int w = 0;
+                if (br.bits(1)) w = (int)br.unary() + 1;
+                const int sbps = cd.bps - w;
+                // layout of the subframe: order, taps, shift, raw residuals
+                int o = 0, shift = 0, prec = 3;
+                bool raw = false, take = cd.bps <= 16 && sbps > 0 && sbps <= 16;
+                if (t == 1) raw = true;
+                else if (t >= 8 && t <= 12) o = t - 8;
+                else if (t >= 32 && t <= 39) o = t - 31;
+                else if (t != 0) take = false;
+                int32_t cq[8], R[8];
+#pragma unroll
+                for (int m = 0; m < 8; m++) {
+                    cq[m] = 0;
+                    R[m] = 0;
+                }
+                if (take && t == 0) {  // CONSTANT
+                    const int32_t v = br.sbits(sbps);
+                    const int32_t xo = (int32_t)((uint32_t)v << w);
+                    for (int i = 0; i < bs; i++) {
+                        if (fused) dn_store(dout, obase + i, xo, dnp);
+                        else pcm[obase + i] = xo;
+                    }
+                    ok = !br.bad && ((br.pos() + 7) >> 3) + 2 == fend;
+                } else if (take) {
+#pragma unroll
+                    for (int m = 0; m < 8; m++)
+                        if (m < o) R[m] = br.sbits(sbps);
+                    if (t >= 32) {
+                        prec = (int)br.bits(4) + 1;
+                        shift = br.sbits(5);
+                        if (prec == 16 || shift < 0) take = false;
+#pragma unroll
+                        for (int m = 0; m < 8; m++)
+                            if (m < o) cq[m] = br.sbits(prec);
+                    } else if (t >= 8) {
+                        cq[0] = o == 1 ? 1 : o == 2 ? 2 : o == 3 ? 3 : o == 4 ? 4 : 0;
+                        cq[1] = o == 2 ? -1 : o == 3 ? -3 : o == 4 ? -6 : 0;
+                        cq[2] = o == 3 ? 1 : o == 4 ? 4 : 0;
+                        cq[3] = o == 4 ? -1 : 0;
+                    }
+                    int lg = 0;
+                    while ((1 << lg) < o) lg++;
+                    if (!(prec + sbps + lg <= 31)) take = false;
+                    int pb = 4, esc = 15, psz = bs, part_end = bs, k = 0, nb = 0;
+                    bool escp = false;
+                    if (take && !raw) {
+                        const int method = (int)br.bits(2);
+                        const int po = (int)br.bits(4);
+                        if (method > 1 || (bs >> po) < o || (bs & ((1 << po) - 1))) {
+                            take = false;  // malformed: the wave decoder reports it
+                        } else {
+                            pb = method == 0 ? 4 : 5;
+                            esc = (1 << pb) - 1;
+                            psz = bs >> po;
+                            part_end = psz;
+                            k = (int)br.bits(pb);
+                            escp = k == esc;
+                            if (escp) nb = (int)br.bits(5);
+                        }
+                    }
+                    if (take) {
+                        // warm-up samples (ring slot m = sample m)
+                        for (int m = 0; m < o; m++) {
+                            const int32_t xo = (int32_t)((uint32_t)R[m] << w);
+                            if (fused) dn_store(dout, obase + m, xo, dnp);
+                            else pcm[obase + m] = xo;
+                        }
+                        // sample i lives in ring slot i & 7; a step handles samples i0 .. i0 + 7
+                        for (int i0 = 0; i0 < bs; i0 += 8) {
+#pragma unroll
+                            for (int u = 0; u < 8; u++) {
+                                const int i = i0 + u;
+                                if (i >= o && i < bs) {
+                                    if (i == part_end) {  // next partition's Rice parameter
+                                        k = (int)br.bits(pb);
+                                        escp = k == esc;
+                                        if (escp) nb = (int)br.bits(5);
+                                        part_end += psz;
+                                    }
+                                    int32_t r;
+                                    if (raw) {
+                                        r = br.sbits(sbps);
+                                    } else if (escp) {
+                                        r = nb ? br.sbits(nb) : 0;
+                                    } else {
+                                        const uint32_t q = br.unary();
+                                        const uint32_t uu = (q << k) | br.bits(k);
+                                        r = (int32_t)((uu >> 1) ^ (uint32_t)(-(int32_t)(uu & 1)));
+                                    }
+                                    int32_t pred = 0;
+#pragma unroll
+                                    for (int m = 0; m < 8; m++) pred += __mul24(cq[m], R[(u + 7 - m) & 7]);
+                                    const int32_t x = r + (pred >> shift);
+                                    R[u] = x;
+                                    const int32_t xo = (int32_t)((uint32_t)x << w);
+                                    if (fused) dn_store(dout, obase + i, xo, dnp);
+                                    else pcm[obase + i] = xo;
+                                }
+                            }
+                        }
+                        ok = !br.bad && ((br.pos() + 7) >> 3) + 2 == fend;
+                    }
+                }
+                if (!take) fb_list[atomicAdd(fb_count, 1)] = (int32_t)fi;
+            }
+        }
+    }
+    const uint64_t m = __ballot(ok);
+    if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(__ballot(1))) atomicAdd(nvalid, __builtin_popcountll(m));
 }
 
 // converter.py:88-110 (fp32, round half to even) after the pyflac/soundfile WAV round trip.
@@ -1422,6 +1657,7 @@ __global__ void k_denormalize(const int32_t *pcm, int64_t n, int shift, float rn
 }
 
 static bool g_dec_tables[64];
+constexpr int64_t kLaneMinFrames = 4096;  // below: the pipelined decoder (C5 queries decode 64 frames)
 
 int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const int64_t *stream_off,
                int32_t nstreams, int32_t channels, int32_t bps, int32_t blocksize, int32_t *pcm_dev,
@@ -1475,7 +1711,11 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     const int64_t max_frame = (int64_t)blocksize * channels * 5 + 4096;
     // FRS_FORCE_GENERIC (tests): every frame through the one-lane wave decoder
     const bool pipe = channels == 1 && bps <= 16 && blocksize <= kDecResMax && !ctx->force_generic;
-    if (fused && !pipe) {  // the wave decoder de-normalises out of an int32 scratch
+    // many mono frames: the lane-per-frame throughput decoder (the pipelined one is latency-optimised: ~2 work-groups
+    // per CU at 62 KB of LDS each); FRS_DECODE_LANE=0/1 overrides for tests
+    bool lane = pipe && frames >= kLaneMinFrames;
+    if (ctx->decode_lane >= 0) lane = pipe && ctx->decode_lane == 1;
+    if (fused && (!pipe || lane)) {  // the wave decoder de-normalises out of an int32 scratch
         const int64_t nsamp = pcm_off[nstreams] - pcm_off[0];
         if (!pcm_dev) {
             FRS_HIP(ctx->dec_pcm.ensure((size_t)nsamp * channels * 4 + 16));
@@ -1555,7 +1795,17 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     dout.dtype = out_dtype;
     dout.shift = bps > 16 ? 16 : 0;
     prof_begin(ctx, "decode_frames", &ev);
-    if (pipe)
+    if (lane) {
+        FRS_HIP(ctx->dec_fb.ensure(sizeof(int32_t) * (size_t)frames + 64));
+        int32_t *fbl = ctx->dec_fb.as<int32_t>();
+        int *fbc = ncand + 3;
+        k_decode_frames_lane<<<(unsigned)((frames + 255) / 256), 256, 0, st>>>(
+            blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, dchain, frames, bps, pcm_dev, blocksize, nvalid, dout,
+            fbl, fbc);
+        k_decode_frames_wave_list<<<(unsigned)std::min<int64_t>(frames, 4 * (int64_t)ctx->num_cus), 64, 0, st>>>(
+            blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, dchain, channels, bps, pcm_dev, blocksize, nvalid,
+            dout, fbl, fbc);
+    } else if (pipe)
         k_decode_frames_pipe<<<(unsigned)frames, 128, 0, st>>>(blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase,
                                                                dchain, frames, channels, bps, pcm_dev, blocksize, nvalid,
                                                                dout);

@@ -1,5 +1,6 @@
-"""GPU decode parity: the mono 16-bit fast decoder (k_decode_frames_pipe: scalar-unit Rice decode + v_dot2 LPC
-restore in two waves) and the lane-0 decoder must both return exactly the oracle's decode of the same frames,
+"""GPU decode parity: the mono 16-bit decoders (k_decode_frames_pipe: scalar-unit Rice decode + v_dot2 LPC restore
+in two waves; k_decode_frames_lane: one lane per frame) and the lane-0 wave decoder must all return exactly the
+oracle's decode of the same frames,
 for every subframe type the encoder emits (CONSTANT, VERBATIM, FIXED, LPC, wasted bits), partial frames,
 Rice windows that hit the 64-code cap and codes longer than a 64-bit candidate window."""
 import numpy as np
@@ -43,11 +44,21 @@ def _bands():
             ("flat", flat, 256), ("spiky", spiky, 256)]
 
 
-@pytest.mark.parametrize("generic", ["0", "1"])  # 1: every frame through the lane-0 wave decoder
-def test_decode_matches_oracle(gpu_ctx, generic, monkeypatch):
+DECODERS = {"pipe": {"FRS_DECODE_LANE": "0"},      # two-wave pipelined decoder (latency; C5 queries)
+            "lane": {"FRS_DECODE_LANE": "1"},      # lane-per-frame decoder (throughput; batched decodes)
+            "wave": {"FRS_FORCE_GENERIC": "1"}}    # one-lane wave decoder (any layout)
+
+
+def _decoder_ctx(kind, monkeypatch):
     from flac_raster_amd import _native
-    monkeypatch.setenv("FRS_FORCE_GENERIC", generic)
-    dctx = _native.Context(0)
+    for k, v in DECODERS[kind].items():
+        monkeypatch.setenv(k, v)
+    return _native.Context(0)
+
+
+@pytest.mark.parametrize("kind", list(DECODERS))
+def test_decode_matches_oracle(gpu_ctx, kind, monkeypatch):
+    dctx = _decoder_ctx(kind, monkeypatch)
     for name, band, tile in _bands():
         H, W = band.shape
         d = gpu_ctx.make_desc(H, W, band.dtype, tile_h=tile, tile_w=tile, sample_rate=44100, bits_per_sample=16)
@@ -69,15 +80,14 @@ def test_decode_matches_oracle(gpu_ctx, generic, monkeypatch):
     dctx.close()
 
 
-@pytest.mark.parametrize("generic", ["0", "1"])
-def test_decode_corrupt_streams_report_errors(gpu_ctx, generic, monkeypatch):
+@pytest.mark.parametrize("kind", list(DECODERS))
+def test_decode_corrupt_streams_report_errors(gpu_ctx, kind, monkeypatch):
     """Damaged data must end in FrsError (CRC-16 span check fails, chain broken, or no sync codes at all), never a
     fault, a stall or a silent wrong decode; the context then still decodes good data (the decode path launches its
     span and frame kernels before the host knows the candidate count, so the unchained frames are skipped on
     device: a frame whose CRC span fails is never handed to a decoder)."""
     from flac_raster_amd import _native
-    monkeypatch.setenv("FRS_FORCE_GENERIC", generic)
-    dctx = _native.Context(0)
+    dctx = _decoder_ctx(kind, monkeypatch)
     band = _bands()[0][1][:256, :256].copy()
     d = gpu_ctx.make_desc(256, 256, band.dtype, tile_h=128, tile_w=128, sample_rate=44100, bits_per_sample=16)
     arena, off, mn, mx, bps = gpu_ctx.encode_tiles_host(band, d)
