@@ -96,14 +96,66 @@ __device__ FrameHdr parse_header(const uint8_t *blob, int64_t p, int64_t end, in
 }
 
 // ---------------------------------------------------------------------------------- candidate selection
-// One pass over the blob: a block takes 4096 bytes (16 per thread, one 16-byte load), flags the bytes that
+// One pass over the blob: a block takes 64 KB (256 contiguous bytes per thread, 16-byte loads), flags the bytes that
 // start a sync code with a parseable CRC-8-correct header, and writes their positions, in order, at its
-// exclusive prefix -- found by decoupled look-back over the blocks' published counts.  Blocks take their
-// ordinal from a ticket (the block that draws the last ticket re-arms the counter for the next call), so a
-// predecessor is always resident or done.  Status word: [63:40] call epoch, [39:38] flag, [37:0] count;
-// words of another epoch read as "not published", so the buffer is never cleared between calls.
-constexpr int kSelThreads = 256, kSelBytes = 4096;
+// exclusive prefix -- found by decoupled look-back over the blocks' published counts, 64 predecessors per step
+// (one wave).  Blocks take their ordinal from a ticket (the block that draws the last ticket re-arms the counter
+// for the next call), so a predecessor is always resident or done.  Status word: [63:40] call epoch, [39:38]
+// flag, [37:0] count; words of another epoch read as "not published", so the buffer is never cleared.
+constexpr int kSelThreads = 256, kSelPerThread = 64, kSelChunks = 4, kSelBytes = kSelThreads * kSelPerThread * kSelChunks;
 constexpr uint64_t kSelAgg = 1ull << 38, kSelIncl = 2ull << 38, kSelVal = (1ull << 38) - 1;
+
+__device__ inline int64_t wave_sum_i64(int64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// Candidate flags of the kSelChunks * 64 bytes at aligned offset qt (byte q of the 16-byte aligned view is
+// blob[q - lead]; a 16-byte line holding a blob byte is mapped): bit j of masks[ch] marks the sync code with a
+// parseable, CRC-8-correct header at qt + 64 ch + j.  Returns the number of candidates.
+__device__ inline int sel_masks(const uint8_t *blob, int64_t nbytes, const int64_t *soff, int ns, int channels,
+                                int stream_bps, int64_t qt, uint64_t *masks) {
+    const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
+    const uint8_t *base = blob - lead;
+    const int64_t qend = nbytes + lead;
+    int cnt = 0;
+#pragma unroll
+    for (int ch = 0; ch < kSelChunks; ch++) {
+        const int64_t q0 = qt + kSelPerThread * ch;
+        uint32_t w[kSelPerThread / 4 + 1];
+#pragma unroll
+        for (int v = 0; v < kSelPerThread / 16; v++) {
+            uint4 x = make_uint4(0, 0, 0, 0);
+            if (q0 + 16 * v < qend) x = *reinterpret_cast<const uint4 *>(base + q0 + 16 * v);
+            w[4 * v] = x.x;
+            w[4 * v + 1] = x.y;
+            w[4 * v + 2] = x.z;
+            w[4 * v + 3] = x.w;
+        }
+        w[kSelPerThread / 4] = (q0 + kSelPerThread < qend) ? base[q0 + kSelPerThread] : 0u;  // the byte after
+        uint64_t mask = 0;
+#pragma unroll
+        for (int k = 0; k < kSelPerThread / 4; k++) {
+            const uint32_t x = w[k];
+            if (((~x) - 0x01010101u) & x & 0x80808080u) {  // some byte is 0xFF
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t b0 = (x >> (8 * j)) & 0xFF;
+                    const uint32_t b1 = j < 3 ? (x >> (8 * j + 8)) & 0xFF : w[k + 1] & 0xFF;
+                    const int64_t p = q0 + 4 * k + j - lead;
+                    if (b0 == 0xFF && (b1 & 0xFE) == 0xF8 && p >= 0 && p + 1 < nbytes) {
+                        const int s = stream_of(soff, ns, p);
+                        if (parse_header(blob, p, soff[s + 1], channels, stream_bps).ok) mask |= 1ull << (4 * k + j);
+                    }
+                }
+            }
+        }
+        masks[ch] = mask;
+        cnt += __builtin_popcountll(mask);
+    }
+    return cnt;
+}
 
 __global__ void __launch_bounds__(kSelThreads) k_sync_select(const uint8_t *blob, int64_t nbytes, const int64_t *soff,
                                                            int ns, int channels, int stream_bps, uint64_t *status,
@@ -119,34 +171,11 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_select(const uint8_t *blob
     }
     __syncthreads();
     const int64_t ord = s_ord;
-    // aligned view: byte q of `base` is blob[q - lead]; a 16-byte line holding a blob byte is mapped
     const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
-    const uint8_t *base = blob - lead;
-    const int64_t q0 = ord * kSelBytes + 16 * t, qend = nbytes + lead;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (q0 < qend) v = *reinterpret_cast<const uint4 *>(base + q0);
-    // the byte after this thread's 16 (the next lane's first byte; the wave's last lane loads it)
-    uint32_t nxt = (uint32_t)__shfl_down((int)(v.x & 0xFF), 1);
-    if (lane == 63) nxt = (q0 + 16 < qend) ? base[q0 + 16] : 0u;
-    uint32_t mask = 0;
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t x = w[k];
-        if (((~x) - 0x01010101u) & x & 0x80808080u) {  // some byte is 0xFF
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t b0 = (x >> (8 * j)) & 0xFF;
-                const uint32_t b1 = j < 3 ? (x >> (8 * j + 8)) & 0xFF : (k < 3 ? w[k + 1] & 0xFF : nxt);
-                const int64_t p = q0 + 4 * k + j - lead;
-                if (b0 == 0xFF && (b1 & 0xFE) == 0xF8 && p >= 0 && p + 1 < nbytes) {
-                    const int s = stream_of(soff, ns, p);
-                    if (parse_header(blob, p, soff[s + 1], channels, stream_bps).ok) mask |= 1u << (4 * k + j);
-                }
-            }
-        }
-    }
-    const int cnt = __builtin_popcount(mask);
+    // thread t owns the contiguous kSelChunks * 64 bytes at ord * kSelBytes + 256 t (its candidates stay in order)
+    const int64_t qt = ord * kSelBytes + (int64_t)(kSelPerThread * kSelChunks) * t;
+    uint64_t masks[kSelChunks];
+    const int cnt = sel_masks(blob, nbytes, soff, ns, channels, stream_bps, qt, masks);
     int x = cnt;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -162,39 +191,141 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_select(const uint8_t *blob
         wbase += k < wv ? sv : 0;
         tot += sv;
     }
-    if (t == 0) {
+    if (wv == 0) {  // publish, then look back 64 predecessors at a time
         const uint64_t tag = (uint64_t)epoch << 40;
         int64_t excl = 0;
         if (ord == 0) {
-            __hip_atomic_store(&status[0], tag | kSelIncl | (uint64_t)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            counts[1] = 0;  // nvalid, bad: zeroed here (the later kernels of this call run after this one)
-            counts[2] = 0;
-            counts[3] = 0;  // frames queued for the wave decoder by the lane decoder
+            if (lane == 0) {
+                __hip_atomic_store(&status[0], tag | kSelIncl | (uint64_t)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                counts[1] = 0;  // nvalid, bad, lane-decoder queue: zeroed here (later kernels run after this one)
+                counts[2] = 0;
+                counts[3] = 0;
+            }
         } else {
-            __hip_atomic_store(&status[ord], tag | kSelAgg | (uint64_t)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            for (int64_t j = ord - 1;;) {
-                const uint64_t sv = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((sv >> 40) != epoch || !(sv & (kSelAgg | kSelIncl))) {
+            if (lane == 0)
+                __hip_atomic_store(&status[ord], tag | kSelAgg | (uint64_t)tot, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            for (int64_t hi = ord - 1;;) {
+                const int64_t j = hi - lane;
+                uint64_t sv = tag | kSelIncl;  // before block 0: inclusive 0
+                if (j >= 0) sv = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const bool valid = (sv >> 40) == epoch && (sv & (kSelAgg | kSelIncl));
+                const uint64_t has = __ballot(valid && (sv & kSelIncl));
+                const int fl = has ? __builtin_ctzll(has) : 64;  // nearest inclusive predecessor
+                const bool need = lane <= fl;
+                if (__ballot(need && !valid)) {
                     __builtin_amdgcn_s_sleep(2);
                     continue;
                 }
-                excl += (int64_t)(sv & kSelVal);
-                if (sv & kSelIncl) break;
-                j--;
+                excl += wave_sum_i64(need ? (int64_t)(sv & kSelVal) : 0);
+                if (fl < 64) break;
+                hi -= 64;
             }
-            __hip_atomic_store(&status[ord], tag | kSelIncl | (uint64_t)(excl + tot), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            if (lane == 0)
+                __hip_atomic_store(&status[ord], tag | kSelIncl | (uint64_t)(excl + tot), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (ord == nblocks - 1) counts[0] = (int)min<int64_t>(excl + tot, (int64_t)0x7FFFFFFF);
-        s_base = excl;
+        if (lane == 0) {
+            if (ord == nblocks - 1) counts[0] = (int)min<int64_t>(excl + tot, (int64_t)0x7FFFFFFF);
+            s_base = excl;
+        }
     }
     __syncthreads();
     int64_t idx = s_base + wbase + x - cnt;
-    while (mask) {  // positions in increasing order; past the cap only counted
-        const int j = __builtin_ctz(mask);
-        mask &= mask - 1;
-        if (idx < cap) cpos[idx] = q0 + j - lead;
-        idx++;
+#pragma unroll
+    for (int ch = 0; ch < kSelChunks; ch++) {
+        uint64_t mask = masks[ch];
+        while (mask) {  // positions in increasing order; past the cap only counted
+            const int j = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            if (idx < cap) cpos[idx] = qt + kSelPerThread * ch + j - lead;
+            idx++;
+        }
+    }
+}
+
+// Large ranges (a whole arena): the single pass above serialises on its look-back (the inclusive prefix advances one
+// 64-block window per status round trip: ~7 ms over a 3.1 GB arena), so large ranges take two passes instead --
+// per-block counts, one work-group's scan of them, and a scatter pass that recomputes the flags (the range is read
+// twice, at streaming rate).
+__global__ void __launch_bounds__(kSelThreads) k_sync_count(const uint8_t *blob, int64_t nbytes, const int64_t *soff,
+                                                          int ns, int channels, int stream_bps, int32_t *bcount) {
+    __shared__ int s_wsum[kSelThreads / 64];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    uint64_t masks[kSelChunks];
+    int c = sel_masks(blob, nbytes, soff, ns, channels, stream_bps,
+                      (int64_t)blockIdx.x * kSelBytes + (int64_t)(kSelPerThread * kSelChunks) * t, masks);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if (lane == 0) s_wsum[wv] = c;
+    __syncthreads();
+    if (t == 0) bcount[blockIdx.x] = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+}
+
+// exclusive scan of the block counts in one work-group (bbase[n] = total -> counts[0]); zeroes the later counters
+__global__ void __launch_bounds__(1024) k_sync_scan(const int32_t *bcount, int64_t *bbase, int64_t n, int *counts) {
+    __shared__ int64_t wsum[16];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int64_t c = (n + 1023) / 1024;
+    const int64_t a = min(n, (int64_t)t * c), b = min(n, a + c);
+    int64_t run = 0;
+    for (int64_t i = a; i < b; i++) run += bcount[i];
+    int64_t x = run;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    int64_t base = 0, total = 0;
+    for (int k = 0; k < 16; k++) {
+        base += k < wv ? wsum[k] : 0;
+        total += wsum[k];
+    }
+    int64_t acc = base + x - run;
+    for (int64_t i = a; i < b; i++) {
+        bbase[i] = acc;
+        acc += bcount[i];
+    }
+    if (t == 0) {
+        counts[0] = (int)min<int64_t>(total, (int64_t)0x7FFFFFFF);
+        counts[1] = 0;
+        counts[2] = 0;
+        counts[3] = 0;
+    }
+}
+
+__global__ void __launch_bounds__(kSelThreads) k_sync_scatter(const uint8_t *blob, int64_t nbytes, const int64_t *soff,
+                                                            int ns, int channels, int stream_bps, const int64_t *bbase,
+                                                            int64_t *cpos, int64_t cap) {
+    __shared__ int s_wsum[kSelThreads / 64];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
+    const int64_t qt = (int64_t)blockIdx.x * kSelBytes + (int64_t)(kSelPerThread * kSelChunks) * t;
+    uint64_t masks[kSelChunks];
+    const int cnt = sel_masks(blob, nbytes, soff, ns, channels, stream_bps, qt, masks);
+    int x = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_wsum[wv] = x;
+    __syncthreads();
+    int wbase = 0;
+#pragma unroll
+    for (int k = 0; k < kSelThreads / 64; k++) wbase += k < wv ? s_wsum[k] : 0;
+    int64_t idx = bbase[blockIdx.x] + wbase + x - cnt;
+#pragma unroll
+    for (int ch = 0; ch < kSelChunks; ch++) {
+        uint64_t mask = masks[ch];
+        while (mask) {
+            const int j = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            if (idx < cap) cpos[idx] = qt + kSelPerThread * ch + j - lead;
+            idx++;
+        }
     }
 }
 
@@ -380,6 +511,70 @@ __global__ void __launch_bounds__(64) k_span_crc_wave(const uint8_t *blob, const
             ends[i] = result;
             nexti[i] = rnext;
         }
+    }
+}
+
+// Span check for batched decodes, one lane per candidate (the wave form above spends a work-group's LDS stage per
+// candidate and runs at ~1.5 waves per SIMD): the lane folds the bytes from its candidate into a CRC-16 with
+// aligned dword loads (slice-by-4 tables in LDS) and compares it at every later candidate start (and the stream
+// end).  Same outputs as k_span_crc_wave.
+__global__ void __launch_bounds__(256) k_span_crc_lane(const uint8_t *blob, const int64_t *soff, int ns,
+                                                      const int64_t *cpos, const int *ncand, int cand_cap,
+                                                      int64_t max_frame, int64_t *ends, int32_t *nexti) {
+    __shared__ uint16_t t4[4][256];
+    for (int k = threadIdx.x; k < 256; k += blockDim.x) {
+        uint16_t c = d_crc16[k];
+        t4[0][k] = c;
+#pragma unroll
+        for (int j = 1; j < 4; j++) {
+            c = (uint16_t)(((c << 8) & 0xFFFF) ^ d_crc16[c >> 8]);
+            t4[j][k] = c;
+        }
+    }
+    __syncthreads();
+    const int nc = *ncand;
+    if (nc > cand_cap) return;
+    const int64_t lead = (int64_t)(reinterpret_cast<uintptr_t>(blob) & 15);
+    const uint8_t *abase = blob - lead;  // 16-byte aligned view: blob[b] = abase[b + lead]
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nc; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t p = cpos[i];
+    const int s = stream_of(soff, ns, p);
+    const int64_t send = soff[s + 1];
+    const int64_t lim = min(send, p + max_frame);
+    uint32_t crc = 0;  // CRC-16 of [p, b)
+    int64_t b = p, result = -1;
+    int32_t rnext = -1;
+    for (int64_t j = i + 1;; j++) {
+        int64_t e = j < nc ? cpos[j] : send;
+        if (e > send) e = send;
+        if (e > lim) break;
+        if (e >= p + 7) {
+            const int64_t stop = e - 2;
+            auto fold4 = [&](uint32_t w) {  // bytes of w (little-endian) in order
+                crc = (uint32_t)t4[3][((crc >> 8) ^ (w & 0xFF)) & 0xFF] ^ t4[2][((crc & 0xFF) ^ ((w >> 8) & 0xFF)) & 0xFF] ^
+                      t4[1][(w >> 16) & 0xFF] ^ t4[0][w >> 24];
+            };
+            for (; b < stop && ((b + lead) & 3); b++) crc = ((crc << 8) & 0xFFFFu) ^ t4[0][((crc >> 8) ^ blob[b]) & 0xFF];
+            for (; b + 4 <= stop && ((b + lead) & 15); b += 4) fold4(*reinterpret_cast<const uint32_t *>(abase + b + lead));
+            for (; b + 16 <= stop; b += 16) {  // one 16-byte load per four dwords
+                const uint4 v = *reinterpret_cast<const uint4 *>(abase + b + lead);
+                fold4(v.x);
+                fold4(v.y);
+                fold4(v.z);
+                fold4(v.w);
+            }
+            for (; b + 4 <= stop; b += 4) fold4(*reinterpret_cast<const uint32_t *>(abase + b + lead));
+            for (; b < stop; b++) crc = ((crc << 8) & 0xFFFFu) ^ t4[0][((crc >> 8) ^ blob[b]) & 0xFF];
+            if (crc == (((uint32_t)blob[e - 2] << 8) | blob[e - 1])) {
+                result = e;
+                rnext = (j < nc && cpos[j] < send) ? (int32_t)j : -2;
+                break;
+            }
+        }
+        if (e >= send) break;
+    }
+    ends[i] = result;
+    nexti[i] = rnext;
     }
 }
 
@@ -1430,44 +1625,102 @@ __global__ void __launch_bounds__(64) k_decode_frames_wave_list(const uint8_t *b
 }
 
 // ------------------------------------------------------------------ lane-per-frame decoder (batched decodes)
-// Throughput form for decodes of many frames (a whole arena, FLAC -> TIFF of a large raster): one lane per frame.
-// Each lane walks its own frame with a 64-bit bit cache refilled one big-endian dword at a time from global memory
-// (a lane's successive loads hit the same cache lines) and restores the samples with the LPC recurrence on an
-// eight-register ring, eight samples per unrolled step (compile-time ring slots: no register indexing); FIXED
-// predictors are order-<=4 LPC with shift 0, VERBATIM is order 0 with raw residuals.  Mono streams of <= 16-bit
-// samples whose prediction fits 32 bits (the pipelined decoder's condition); anything else is queued for
-// k_decode_frames_wave_list.  A frame counts as valid when its subframe ends exactly at the CRC-16 footer found
-// by the span check.
+// Throughput form for decodes of many frames (a whole arena, FLAC -> TIFF of a large raster): one lane per frame,
+// eight samples per step.  Each lane walks its own frame with a 64-bit bit cache fed from a six-dword queue of
+// big-endian words; the queue is topped up once per step from a 16-byte chunk whose load was issued a step earlier
+// (so loads rarely stall), and cache refills inside a step are branch-free selects.  Partition boundaries are
+// consumed by conditional shifts, the LPC recurrence runs on an eight-register ring with compile-time slots (no
+// register indexing), and each step's eight outputs leave in one vector store (8 to 32 bytes; scattered 2-byte
+// stores from 64 lanes cost ~13x the bytes in partial-line writes).  The output kind is a template parameter, so
+// the per-sample work has no dtype switch.  Taken: mono streams of <= 16-bit samples, FIXED / LPC (order <= 8,
+// 32-bit-safe prediction), VERBATIM and CONSTANT subframes; an escaped partition or anything else sends the frame to
+// k_decode_frames_wave_list (which rewrites all of its samples).  A frame counts as valid when its
+// subframe ends exactly at the CRC-16 footer found by the span check.
+constexpr int kOutPcm = 0, kOutI16 = 1, kOutU16 = 2, kOutU8 = 3, kOutAny = 4;
+
 struct LaneReader {
-    const uint8_t *blob;
-    int64_t wb;   // byte offset of the next dword to load (a multiple of 4)
-    int64_t end;  // stream end: loads never touch bytes at or past it
-    uint64_t c;   // left-aligned bit cache
-    int n;        // valid bits in c (> 32 between calls)
+    const uint8_t *abase;  // blob aligned down to 16 bytes; chunk q covers abase[q, q + 16)
+    int64_t lead;          // blob - abase
+    int64_t next;          // aligned offset of the next chunk to load
+    int64_t end;           // stream end (blob bytes)
+    uint64_t c;            // left-aligned bit cache
+    int n;                 // valid bits in c
+    uint64_t qa, qb, qc;   // queued big-endian dwords, left-aligned (qa's high half first)
+    int qw;                // dwords queued (<= 6)
+    uint64_t pa, pb;       // the chunk loaded a step ahead
     bool bad;
-    __device__ inline void refill() {  // n <= 32
-        c |= (uint64_t)__builtin_bswap32(load_word_guarded(blob, wb >> 2, end)) << (32 - n);
-        n += 32;
-        wb += 4;
+    __device__ inline void load_chunk(int64_t q, uint64_t &a, uint64_t &b) const {
+        uint4 x;
+        if (q - lead + 16 <= end) {
+            x = *reinterpret_cast<const uint4 *>(abase + q);
+        } else {  // the stream's (and maybe the allocation's) last bytes: byte loads below `end` only
+            uint32_t v[4] = {0, 0, 0, 0};
+            for (int k = 0; k < 16; k++) {
+                const int64_t bpos = q - lead + k;
+                if (bpos >= 0 && bpos < end) v[k >> 2] |= (uint32_t)abase[q + k] << (8 * (k & 3));
+            }
+            x = make_uint4(v[0], v[1], v[2], v[3]);
+        }
+        a = ((uint64_t)__builtin_bswap32(x.x) << 32) | __builtin_bswap32(x.y);
+        b = ((uint64_t)__builtin_bswap32(x.z) << 32) | __builtin_bswap32(x.w);
+    }
+    // queue <- queue ++ prefetched chunk when at most two dwords are left (branch-free merge), next chunk in flight
+    __device__ inline void top_up() {
+        if (qw <= 2) {
+            const uint64_t a1 = (qa & 0xFFFFFFFF00000000ull) | (pa >> 32);
+            const uint64_t na = qw == 2 ? qa : qw == 1 ? a1 : pa;
+            const uint64_t nb = qw == 2 ? pa : qw == 1 ? ((pa << 32) | (pb >> 32)) : pb;
+            const uint64_t nc = qw == 2 ? pb : qw == 1 ? (pb << 32) : 0ull;
+            qa = na;
+            qb = nb;
+            qc = nc;
+            qw += 4;
+            load_chunk(next, pa, pb);
+            next += 16;
+            if (next - lead > end + 64) bad = true;  // runaway walk (corrupt data)
+        }
+    }
+    __device__ inline void take(bool need) {  // branch-free: one dword into the cache when `need` (n <= 32)
+        const uint32_t w = (uint32_t)(qa >> 32);
+        c |= need ? ((uint64_t)w << (32 - n)) : 0ull;
+        n += need ? 32 : 0;
+        const uint64_t na = (qa << 32) | (qb >> 32), nb = (qb << 32) | (qc >> 32), nc = qc << 32;
+        qa = need ? na : qa;
+        qb = need ? nb : qb;
+        qc = need ? nc : qc;
+        qw -= need ? 1 : 0;
+    }
+    __device__ inline void ensure() {
+        if (qw == 0) top_up();  // rare inside a step: the step used more than the queue held
+        take(n <= 32);
     }
     __device__ inline void init(const uint8_t *b, int64_t pos, int64_t e) {
-        blob = b;
         end = e;
-        wb = pos & ~(int64_t)3;
+        lead = (int64_t)(reinterpret_cast<uintptr_t>(b) & 15);
+        abase = b - lead;
+        const int64_t q = (pos + lead) & ~(int64_t)15;
+        load_chunk(q, qa, qb);
+        qc = 0;
+        qw = 4;
+        load_chunk(q + 16, pa, pb);
+        next = q + 32;
+        bad = false;
+        const int r = (int)((pos + lead) & 15);
         c = 0;
         n = 0;
-        bad = false;
-        refill();
-        refill();
-        const int skip = (int)(pos & 3) * 8;
-        c <<= skip;
-        n -= skip;
+        for (int k = 0; k < (r >> 2); k++) take(true), c = 0, n = 0;  // skip whole dwords
+        top_up();
+        take(true);
+        top_up();
+        take(true);
+        c <<= 8 * (r & 3);
+        n -= 8 * (r & 3);
     }
     __device__ inline uint32_t bits(int k) {  // 0 <= k <= 32
         const uint32_t v = k ? (uint32_t)(c >> (64 - k)) : 0u;
         c = k ? c << k : c;
         n -= k;
-        if (n <= 32) refill();
+        ensure();
         return v;
     }
     __device__ inline int32_t sbits(int k) {
@@ -1477,33 +1730,65 @@ struct LaneReader {
     __device__ inline uint32_t unary() {  // zeros before the next 1 (consumed)
         uint32_t q = 0;
         int z = c ? __builtin_clzll(c) : 64;
-        while (z >= n) {  // rare: a run longer than the cache
+        while (z >= n && !bad) {  // rare: a run longer than the cache
             q += (uint32_t)n;
             c = 0;
             n = 0;
-            refill();
-            if (wb > end + 8) {
-                bad = true;
-                return q;
-            }
+            ensure();
             z = c ? __builtin_clzll(c) : 64;
         }
         q += (uint32_t)z;
         c = (z + 1 >= 64) ? 0 : (c << (z + 1));
         n -= z + 1;
-        if (n <= 32) refill();
+        ensure();
         return q;
     }
-    __device__ inline int64_t pos() const { return wb * 8 - n; }  // bit position from the blob start
+    __device__ inline uint32_t rice(int k) {  // Rice code, parameter k <= 30
+        const int z = c ? __builtin_clzll(c) : 64;
+        if (z + 1 + k > n) {  // rare: longer than the cached bits
+            const uint32_t q = unary();
+            return (q << k) | bits(k);
+        }
+        const uint32_t low = k ? (uint32_t)(((c << z) << 1) >> (64 - k)) : 0u;
+        const int used = z + 1 + k;
+        c = used >= 64 ? 0 : (c << used);
+        n -= used;
+        ensure();
+        return ((uint32_t)z << k) | low;
+    }
+    __device__ inline int64_t pos() const {  // bit position of the next unread bit from the blob start
+        // loaded bytes end at next; the prefetched chunk (128 bits), the queued dwords and the cache are unread
+        return (next - lead) * 8 - 128 - (int64_t)qw * 32 - n;
+    }
 };
 
+// converter.py:88-110 value of one decoded sample as the bits of a <= 4-byte output element
+template <int OUT>
+__device__ inline uint32_t dn_bits_t(const DecOut &o, int32_t pcm, float2 p) {
+    if constexpr (OUT == kOutPcm) {
+        return (uint32_t)pcm;
+    } else {
+        const float v = (float)(pcm >> o.shift) * (1.0f / 32768.0f);
+        float a = __fadd_rn(v, 1.0f);
+        a = __fmul_rn(a, 0.5f);  // == __fdiv_rn(a, 2.0f): scaling by a power of two
+        a = __fmul_rn(a, p.x);
+        a = __fadd_rn(a, p.y);
+        const int64_t r = (int64_t)rintf(a);
+        if constexpr (OUT == kOutU8) return (uint32_t)(uint8_t)r;
+        else return (uint32_t)(uint16_t)r;
+    }
+}
+
+template <int OUT>
 __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob, const int64_t *soff, int ns,
                                                            const int64_t *poff, const int64_t *cpos,
                                                            const int64_t *ends, const int64_t *fbase,
                                                            const int64_t *frame_cand, int64_t nframes,
                                                            int stream_bps, int32_t *pcm, int blocksize, int *nvalid,
                                                            DecOut dout, int32_t *fb_list, int *fb_count) {
+    constexpr int es = OUT == kOutPcm ? 4 : OUT == kOutU8 ? 1 : 2;  // kOutAny: per-sample dn_store
     const int64_t fi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint8_t *obytes = OUT == kOutPcm ? reinterpret_cast<uint8_t *>(pcm) : static_cast<uint8_t *>(dout.out);
     bool ok = false;
     if (fi < nframes) {
         const int64_t ci = frame_cand[fi];
@@ -1519,8 +1804,7 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
             if (cd.ok && cd.frame_no == kk && cd.bs <= blocksize && first + cd.bs <= nsamp) {
                 const int bs = cd.bs;
                 const int64_t obase = poff[s] + first;
-                const bool fused = dout.out != nullptr;
-                const float2 dnp = fused ? dout.dn[s] : make_float2(0.f, 0.f);
+                const float2 dnp = OUT != kOutPcm ? dout.dn[s] : make_float2(0.f, 0.f);
                 LaneReader br;
                 br.init(blob, fpos + cd.hdr_len, send);
                 br.bits(1);
@@ -1528,106 +1812,125 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
                 int w = 0;
                 if (br.bits(1)) w = (int)br.unary() + 1;
                 const int sbps = cd.bps - w;
-                // layout of the subframe: order, taps, shift, raw residuals
                 int o = 0, shift = 0, prec = 3;
-                bool raw = false, take = cd.bps <= 16 && sbps > 0 && sbps <= 16;
-                if (t == 1) raw = true;
-                else if (t >= 8 && t <= 12) o = t - 8;
+                bool take = cd.bps <= 16 && sbps > 0 && sbps <= 16;
+                const bool raw = t == 1;  // VERBATIM: order 0, raw residuals
+                if (t >= 8 && t <= 12) o = t - 8;
                 else if (t >= 32 && t <= 39) o = t - 31;
-                else if (t != 0) take = false;
+                else if (t > 1) take = false;  // reserved: the wave decoder reports it
                 int32_t cq[8], R[8];
 #pragma unroll
                 for (int m = 0; m < 8; m++) {
                     cq[m] = 0;
                     R[m] = 0;
                 }
-                if (take && t == 0) {  // CONSTANT
-                    const int32_t v = br.sbits(sbps);
-                    const int32_t xo = (int32_t)((uint32_t)v << w);
-                    for (int i = 0; i < bs; i++) {
-                        if (fused) dn_store(dout, obase + i, xo, dnp);
-                        else pcm[obase + i] = xo;
-                    }
-                    ok = !br.bad && ((br.pos() + 7) >> 3) + 2 == fend;
-                } else if (take) {
+                int32_t cval = 0;
+                if (take && t == 0) cval = br.sbits(sbps);  // CONSTANT
+#pragma unroll
+                for (int m = 0; m < 8; m++)
+                    if (take && m < o) R[m] = br.sbits(sbps);  // warm-up: ring slot m = sample m
+                if (take && t >= 32) {
+                    prec = (int)br.bits(4) + 1;
+                    shift = br.sbits(5);
+                    if (prec == 16 || shift < 0) take = false;
 #pragma unroll
                     for (int m = 0; m < 8; m++)
-                        if (m < o) R[m] = br.sbits(sbps);
-                    if (t >= 32) {
-                        prec = (int)br.bits(4) + 1;
-                        shift = br.sbits(5);
-                        if (prec == 16 || shift < 0) take = false;
-#pragma unroll
-                        for (int m = 0; m < 8; m++)
-                            if (m < o) cq[m] = br.sbits(prec);
-                    } else if (t >= 8) {
-                        cq[0] = o == 1 ? 1 : o == 2 ? 2 : o == 3 ? 3 : o == 4 ? 4 : 0;
-                        cq[1] = o == 2 ? -1 : o == 3 ? -3 : o == 4 ? -6 : 0;
-                        cq[2] = o == 3 ? 1 : o == 4 ? 4 : 0;
-                        cq[3] = o == 4 ? -1 : 0;
+                        if (m < o) cq[m] = br.sbits(prec);
+                } else if (t >= 8 && t <= 12) {
+                    cq[0] = o == 1 ? 1 : o == 2 ? 2 : o == 3 ? 3 : o == 4 ? 4 : 0;
+                    cq[1] = o == 2 ? -1 : o == 3 ? -3 : o == 4 ? -6 : 0;
+                    cq[2] = o == 3 ? 1 : o == 4 ? 4 : 0;
+                    cq[3] = o == 4 ? -1 : 0;
+                }
+                int lg = 0;
+                while ((1 << lg) < o) lg++;
+                if (!(prec + sbps + lg <= 31)) take = false;
+                int pb = 4, esc = 15, psz = bs, part_end = bs, k = 0;
+                if (take && t >= 8) {
+                    const int method = (int)br.bits(2);
+                    const int po = (int)br.bits(4);
+                    if (method > 1 || (bs >> po) < o || (bs & ((1 << po) - 1))) {
+                        take = false;  // malformed: the wave decoder reports it
+                    } else {
+                        pb = method == 0 ? 4 : 5;
+                        esc = (1 << pb) - 1;
+                        psz = bs >> po;
+                        part_end = psz;
+                        k = (int)br.bits(pb);
+                        if (k == esc) take = false;  // escaped partition: the wave decoder
                     }
-                    int lg = 0;
-                    while ((1 << lg) < o) lg++;
-                    if (!(prec + sbps + lg <= 31)) take = false;
-                    int pb = 4, esc = 15, psz = bs, part_end = bs, k = 0, nb = 0;
-                    bool escp = false;
-                    if (take && !raw) {
-                        const int method = (int)br.bits(2);
-                        const int po = (int)br.bits(4);
-                        if (method > 1 || (bs >> po) < o || (bs & ((1 << po) - 1))) {
-                            take = false;  // malformed: the wave decoder reports it
-                        } else {
-                            pb = method == 0 ? 4 : 5;
-                            esc = (1 << pb) - 1;
-                            psz = bs >> po;
-                            part_end = psz;
-                            k = (int)br.bits(pb);
-                            escp = k == esc;
-                            if (escp) nb = (int)br.bits(5);
-                        }
-                    }
-                    if (take) {
-                        // warm-up samples (ring slot m = sample m)
-                        for (int m = 0; m < o; m++) {
-                            const int32_t xo = (int32_t)((uint32_t)R[m] << w);
-                            if (fused) dn_store(dout, obase + m, xo, dnp);
-                            else pcm[obase + m] = xo;
-                        }
-                        // sample i lives in ring slot i & 7; a step handles samples i0 .. i0 + 7
-                        for (int i0 = 0; i0 < bs; i0 += 8) {
+                }
+                if (take) {
+                    const bool vec = OUT != kOutAny && (obase & 7) == 0;  // 8-element groups aligned
+                    const bool cst = t == 0;
+                    for (int i0 = 0; i0 < bs && take; i0 += 8) {
+                        br.top_up();
+                        uint32_t ob[8];
 #pragma unroll
-                            for (int u = 0; u < 8; u++) {
-                                const int i = i0 + u;
-                                if (i >= o && i < bs) {
-                                    if (i == part_end) {  // next partition's Rice parameter
-                                        k = (int)br.bits(pb);
-                                        escp = k == esc;
-                                        if (escp) nb = (int)br.bits(5);
-                                        part_end += psz;
-                                    }
-                                    int32_t r;
-                                    if (raw) {
-                                        r = br.sbits(sbps);
-                                    } else if (escp) {
-                                        r = nb ? br.sbits(nb) : 0;
-                                    } else {
-                                        const uint32_t q = br.unary();
-                                        const uint32_t uu = (q << k) | br.bits(k);
-                                        r = (int32_t)((uu >> 1) ^ (uint32_t)(-(int32_t)(uu & 1)));
-                                    }
-                                    int32_t pred = 0;
+                        for (int u = 0; u < 8; u++) {
+                            const int i = i0 + u;
+                            int32_t x = cst ? cval : R[u];  // CONSTANT, or the warm-up sample (i < o)
+                            if (!cst && i >= o && i < bs) {
+                                // a partition boundary consumes the next Rice parameter (conditional shift)
+                                const bool bnd = i == part_end && !raw;
+                                const int kp = (int)(br.c >> (64 - pb));
+                                k = bnd ? kp : k;
+                                const int adv = bnd ? pb : 0;
+                                br.c <<= adv;
+                                br.n -= adv;
+                                part_end += bnd ? psz : 0;
+                                if (bnd && k == esc) take = false;
+                                int32_t r;
+                                if (raw) {
+                                    r = br.sbits(sbps);
+                                } else {
+                                    const uint32_t uu = br.rice(k);
+                                    r = (int32_t)((uu >> 1) ^ (uint32_t)(-(int32_t)(uu & 1)));
+                                }
+                                int32_t pred = 0;
 #pragma unroll
-                                    for (int m = 0; m < 8; m++) pred += __mul24(cq[m], R[(u + 7 - m) & 7]);
-                                    const int32_t x = r + (pred >> shift);
-                                    R[u] = x;
-                                    const int32_t xo = (int32_t)((uint32_t)x << w);
-                                    if (fused) dn_store(dout, obase + i, xo, dnp);
-                                    else pcm[obase + i] = xo;
+                                for (int m = 0; m < 8; m++) pred += __mul24(cq[m], R[(u + 7 - m) & 7]);
+                                x = r + (pred >> shift);
+                                R[u] = x;
+                            }
+                            const int32_t xo = (int32_t)((uint32_t)x << w);
+                            if constexpr (OUT == kOutAny) {
+                                if (i < bs) dn_store(dout, obase + i, xo, dnp);
+                                ob[u] = 0;
+                            } else {
+                                ob[u] = dn_bits_t<OUT>(dout, xo, dnp);
+                            }
+                        }
+                        if constexpr (OUT != kOutAny) {
+                            const int nout = min(8, bs - i0);
+                            uint8_t *dst = obytes + (obase + i0) * es;
+                            if (vec && nout == 8) {
+                                if constexpr (es == 2) {
+                                    *reinterpret_cast<uint4 *>(dst) =
+                                        make_uint4(ob[0] | (ob[1] << 16), ob[2] | (ob[3] << 16), ob[4] | (ob[5] << 16),
+                                                   ob[6] | (ob[7] << 16));
+                                } else if constexpr (es == 1) {
+                                    *reinterpret_cast<uint2 *>(dst) =
+                                        make_uint2(ob[0] | (ob[1] << 8) | (ob[2] << 16) | (ob[3] << 24),
+                                                   ob[4] | (ob[5] << 8) | (ob[6] << 16) | (ob[7] << 24));
+                                } else {
+                                    reinterpret_cast<uint4 *>(dst)[0] = make_uint4(ob[0], ob[1], ob[2], ob[3]);
+                                    reinterpret_cast<uint4 *>(dst)[1] = make_uint4(ob[4], ob[5], ob[6], ob[7]);
+                                }
+                            } else {
+#pragma unroll
+                                for (int u = 0; u < 8; u++) {
+                                    if (u < nout) {
+                                        if constexpr (es == 4) reinterpret_cast<uint32_t *>(dst)[u] = ob[u];
+                                        else if constexpr (es == 2) reinterpret_cast<uint16_t *>(dst)[u] = (uint16_t)ob[u];
+                                        else dst[u] = (uint8_t)ob[u];
+                                    }
                                 }
                             }
                         }
-                        ok = !br.bad && ((br.pos() + 7) >> 3) + 2 == fend;
+                        if (br.bad) break;
                     }
+                    ok = take && !br.bad && ((br.pos() + 7) >> 3) + 2 == fend;
                 }
                 if (!take) fb_list[atomicAdd(fb_count, 1)] = (int32_t)fi;
             }
@@ -1657,7 +1960,8 @@ __global__ void k_denormalize(const int32_t *pcm, int64_t n, int shift, float rn
 }
 
 static bool g_dec_tables[64];
-constexpr int64_t kLaneMinFrames = 4096;  // below: the pipelined decoder (C5 queries decode 64 frames)
+constexpr int64_t kLaneMinFrames = 4096;
+constexpr int64_t kSelOnePassBlocks = 256;  // up to 16 MB: the one-pass selection (latency: C5 queries)  // below: the pipelined decoder (C5 queries decode 64 frames)
 
 int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const int64_t *stream_off,
                int32_t nstreams, int32_t channels, int32_t bps, int32_t blocksize, int32_t *pcm_dev,
@@ -1739,7 +2043,7 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     }
     {
         void *before = ctx->dec_status.ptr;
-        FRS_HIP(ctx->dec_status.ensure(sizeof(uint64_t) * (size_t)nblocks));
+        FRS_HIP(ctx->dec_status.ensure(sizeof(uint64_t) * (size_t)std::min<int64_t>(nblocks, kSelOnePassBlocks)));
         if (ctx->dec_status.ptr != before) FRS_HIP(hipMemsetAsync(ctx->dec_status.ptr, 0, ctx->dec_status.bytes, st));
     }
     if (++ctx->dec_epoch >= (1u << 24)) ctx->dec_epoch = 1;
@@ -1748,7 +2052,7 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     const size_t tab = sizeof(int64_t) * (size_t)(nstreams + 1);
     const size_t dn_bytes = fused ? sizeof(float2) * (size_t)nstreams : 0;
     FRS_HIP(ctx->dec_soff.ensure(3 * tab + dn_bytes + sizeof(int64_t) * frames + 64));
-    FRS_HIP(ctx->pin.ensure(3 * tab + dn_bytes + 64));
+    FRS_HIP(ctx->pin.ensure(3 * tab + dn_bytes + 96));
     int64_t *htab = ctx->pin.at<int64_t>(0);
     memcpy(htab, stream_off, tab);
     memcpy(htab + (nstreams + 1), fbase.data(), tab);
@@ -1772,14 +2076,29 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     int32_t *nexti = ctx->dec_next.as<int32_t>();
     hipEvent_t ev;
     prof_begin(ctx, "decode", &ev);
-    k_sync_select<<<(unsigned)nblocks, kSelThreads, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams, channels, bps,
-                                                             ctx->dec_status.as<uint64_t>(), ticket, ctx->dec_epoch,
-                                                             nblocks, cpos, cand_cap, ncand);
+    if (nblocks <= kSelOnePassBlocks) {
+        k_sync_select<<<(unsigned)nblocks, kSelThreads, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams, channels, bps,
+                                                                 ctx->dec_status.as<uint64_t>(), ticket,
+                                                                 ctx->dec_epoch, nblocks, cpos, cand_cap, ncand);
+    } else {
+        // (its own buffer: the one-pass status words must keep their epoch tags)
+        FRS_HIP(ctx->dec_sel.ensure(sizeof(int64_t) * (size_t)(2 * nblocks + 4)));
+        int32_t *bcount = ctx->dec_sel.as<int32_t>();
+        int64_t *bbase = ctx->dec_sel.as<int64_t>() + (nblocks + 1) / 2 + 1;
+        k_sync_count<<<(unsigned)nblocks, kSelThreads, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams, channels, bps,
+                                                                bcount);
+        k_sync_scan<<<1, 1024, 0, st>>>(bcount, bbase, nblocks, ncand);
+        k_sync_scatter<<<(unsigned)nblocks, kSelThreads, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams, channels, bps,
+                                                                  bbase, cpos, cand_cap);
+    }
     prof_end(ctx, "decode", ev);
     prof_begin(ctx, "decode_span", &ev);
     // launched before the host knows the candidate count (no mid-query sync): an upper-bound grid strides over
     // *ncand on the device; an overflowing selection makes every later kernel a no-op and is reported below
-    if (max_frame < (int64_t)4096 * 256) {  // x^(8m) table range of the wave CRC
+    if (lane) {  // batched: one lane per candidate, over an upper-bound grid (no mid-call sync)
+        k_span_crc_lane<<<(unsigned)((std::min<int64_t>(cand_cap, 2 * frames + 256) + 255) / 256), 256, 0, st>>>(
+            blob_dev, dsoff, nstreams, cpos, ncand, (int)cand_cap, max_frame, ends, nexti);
+    } else if (max_frame < (int64_t)4096 * 256) {  // x^(8m) table range of the wave CRC
         const int64_t grid = std::min<int64_t>(cand_cap, std::min<int64_t>(2 * frames + 256, (int64_t)ctx->num_cus * 64));
         k_span_crc_wave<<<(unsigned)grid, 64, 0, st>>>(blob_dev, dsoff, nstreams, cpos, ncand, (int)cand_cap,
                                                        max_frame, ends, nexti);
@@ -1799,9 +2118,19 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         FRS_HIP(ctx->dec_fb.ensure(sizeof(int32_t) * (size_t)frames + 64));
         int32_t *fbl = ctx->dec_fb.as<int32_t>();
         int *fbc = ncand + 3;
-        k_decode_frames_lane<<<(unsigned)((frames + 255) / 256), 256, 0, st>>>(
-            blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, dchain, frames, bps, pcm_dev, blocksize, nvalid, dout,
-            fbl, fbc);
+        const unsigned lg = (unsigned)((frames + 255) / 256);
+        const int okind = !fused ? kOutPcm : out_dtype == FRS_DT_I16 ? kOutI16 : out_dtype == FRS_DT_U16 ? kOutU16
+                                   : out_dtype == FRS_DT_U8 ? kOutU8 : kOutAny;
+#define FRS_LANE(K) k_decode_frames_lane<K><<<lg, 256, 0, st>>>(blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, \
+                                                              dchain, frames, bps, pcm_dev, blocksize, nvalid, dout, fbl, fbc)
+        switch (okind) {
+        case kOutPcm: FRS_LANE(kOutPcm); break;
+        case kOutI16: FRS_LANE(kOutI16); break;
+        case kOutU16: FRS_LANE(kOutU16); break;
+        case kOutU8: FRS_LANE(kOutU8); break;
+        default: FRS_LANE(kOutAny); break;
+        }
+#undef FRS_LANE
         k_decode_frames_wave_list<<<(unsigned)std::min<int64_t>(frames, 4 * (int64_t)ctx->num_cus), 64, 0, st>>>(
             blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, dchain, channels, bps, pcm_dev, blocksize, nvalid,
             dout, fbl, fbc);
@@ -1816,9 +2145,14 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     prof_end(ctx, "decode_frames", ev);
     FRS_HIP(hipGetLastError());
     int *hv = reinterpret_cast<int *>(reinterpret_cast<char *>(htab) + ((3 * tab + dn_bytes + 15) & ~(size_t)15));
-    FRS_HIP(hipMemcpyAsync(hv, ncand, sizeof(int) * 3, hipMemcpyDeviceToHost, st));
+    FRS_HIP(hipMemcpyAsync(hv, ncand, sizeof(int) * 4, hipMemcpyDeviceToHost, st));
     FRS_HIP(hipStreamSynchronize(st));
     prof_collect(ctx);
+    if (ctx->prof && lane) {  // frames the lane decoder handed to the wave decoder (profile_avg_ms of this name)
+        ProfEntry &e = ctx->prof_tab["lane_fallback_frames"];
+        e.total_ms += hv[3];
+        e.count += 1;
+    }
     if ((int64_t)hv[0] > cand_cap) {
         ctx->err = "too many frame sync candidates (" + std::to_string(hv[0]) + " > " + std::to_string(cand_cap) +
                    "): not a FLAC stream of the expected layout";

@@ -31,7 +31,8 @@ def main():
                                 out=out)
         ctx.sync()
         print(f"rep {r}: {(time.perf_counter() - t0) * 1e3:.2f} ms", flush=True)
-    print({k: round(ctx.profile_avg_ms(k), 3) for k in ("decode", "decode_span", "decode_frames")})
+    print({k: round(ctx.profile_avg_ms(k), 3) for k in ("decode", "decode_span", "decode_frames",
+                                                          "lane_fallback_frames")})
     back = np.empty(H * W, np.int16)
     out.download(H * W * 2, 0, out=back.view(np.uint8))
     band = np.empty(H * W, np.int16)
