@@ -50,6 +50,8 @@ struct SubAnalysis {
     int32_t fixed_order; // fixed predictor guess
     int32_t lpc_order, lpc_prec, lpc_shift;
     int32_t q[kMaxLpc];  // quantised LPC coefficients
+    uint32_t fixed_tg;   // fast path: fixed-predictor total of the guessed order (samples 4..n-1, shifted by wasted)
+    uint32_t fixed_t1;   // fast path: the order-1 total (constant test: libFLAC's fixed bits[1] == 0)
 };
 constexpr int kFlagConstant = 1;  // CONSTANT subframe (all samples equal and fixed bits[1] == 0)
 constexpr int kFlagFixedOk = 2;   // fixed estimate < subframe bps -> evaluate FIXED

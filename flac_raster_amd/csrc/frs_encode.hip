@@ -1442,7 +1442,8 @@ __device__ inline void norm_block8(const Chunk64<DT> &ch, int b, const TileNorm 
 
 // wasted bits, LPC order choice (expected bits), Levinson coefficients and quantisation of one frame from its
 // windowed autocorrelation sums (stream_encoder.c process_subframe_ / lpc.c)
-__device__ inline SubAnalysis analysis_finish(const double *acc, uint32_t or_acc, int n, const EncodeParams &P) {
+__device__ inline SubAnalysis analysis_finish(const double *acc, uint32_t or_acc, int n, const EncodeParams &P,
+                                              const uint32_t *ft) {
     SubAnalysis A;
     A.n = n;
     int w = or_acc ? __builtin_ctz(or_acc) : 0;
@@ -1450,7 +1451,20 @@ __device__ inline SubAnalysis analysis_finish(const double *acc, uint32_t or_acc
     const int sbps = P.bps - w;
     A.wasted = w;
     A.flags = 0;
-    A.fixed_order = 0;
+    {
+        // fixed.c FLAC__fixed_compute_best_predictor on the shifted samples: every e_k is a multiple of 2^w, so the
+        // shifted totals are the unshifted ones >> w exactly; first minimum under <= comparisons
+        const uint32_t T0 = ft[0] >> w, T1 = ft[1] >> w, T2 = ft[2] >> w, T3 = ft[3] >> w, T4 = ft[4] >> w;
+        int guess;
+        if (T0 <= min(min(T1, T2), min(T3, T4))) guess = 0;
+        else if (T1 <= min(min(T2, T3), T4)) guess = 1;
+        else if (T2 <= min(T3, T4)) guess = 2;
+        else if (T3 <= T4) guess = 3;
+        else guess = 4;
+        A.fixed_order = guess;
+        A.fixed_tg = guess == 0 ? T0 : guess == 1 ? T1 : guess == 2 ? T2 : guess == 3 ? T3 : T4;
+        A.fixed_t1 = T1;
+    }
     A.lpc_order = 0;
     A.lpc_prec = 0;
     A.lpc_shift = 0;
@@ -1570,10 +1584,16 @@ __device__ inline int32_t ana_norm(typename Elem<DT>::T x, const TileNorm &tn, c
     }
 }
 
+__device__ inline uint32_t ana_sad(uint32_t a, uint32_t b, uint32_t c) {  // |a - b| + c (v_sad_u32)
+    uint32_t d;
+    asm("v_sad_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
 template <int DT, int KIND, int kAnaChunk>
 __device__ inline void ana_autoc(const typename Elem<DT>::T *base, const EncodeParams &P, const TileGeom &g,
                                  int64_t s0, const TileNorm &tn, const int16_t *slut, const int16_t *glut,
-                                 const float *__restrict__ swin, bool vec, double *acc, uint32_t &or_acc) {
+                                 const float *__restrict__ swin, bool vec, double *acc, uint32_t &or_acc, uint32_t *ft) {
     using Ch = ChunkN<DT, kAnaChunk>;
     const uint32_t r0 = udiv_inv((uint32_t)s0, (uint32_t)g.w, 1.0 / (double)g.w);
     int64_t crow = r0;
@@ -1581,6 +1601,10 @@ __device__ inline void ana_autoc(const typename Elem<DT>::T *base, const EncodeP
     double prev[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) prev[j] = 0.0;
+    // fixed-predictor totals (fixed.c FLAC__fixed_compute_best_predictor: sum of |e_k(i)| over samples 4..n-1) on the
+    // unshifted samples; the first four samples' terms are subtracted at the end (snapshot after sample 3)
+    uint32_t x1 = 0x80000000u, e1p = 0x80000000u, e2p = 0x80000000u, e3p = 0x80000000u;  // biased zeros
+    uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0, s0t = 0, s1t = 0, s2t = 0, s3t = 0, s4t = 0;
     for (int c = 0; c < kMaxBlock / kAnaChunk; c++) {
         const int i0 = c * kAnaChunk;
         Ch ch;
@@ -1598,6 +1622,25 @@ __device__ inline void ana_autoc(const typename Elem<DT>::T *base, const EncodeP
                 const int32_t x = ana_norm<DT, KIND>(ch.get(8 * b + j), tn, slut, glut);
                 or_acc |= (uint32_t)x;
                 cur[j] = (double)((float)x * swin[i0 + 8 * b + j]);  // lpc.c window_data: float product
+                // sign-flipped differences (y = e ^ 2^31): |e_{k+1}| = v_sad_u32(y_k(i), y_k(i-1)) in one op
+                const uint32_t y0 = (uint32_t)x ^ 0x80000000u;
+                const uint32_t y1 = (y0 - x1) ^ 0x80000000u, y2 = (y1 - e1p) ^ 0x80000000u, y3 = (y2 - e2p) ^ 0x80000000u;
+                t0 = ana_sad(y0, 0x80000000u, t0);
+                t1 = ana_sad(y0, x1, t1);
+                t2 = ana_sad(y1, e1p, t2);
+                t3 = ana_sad(y2, e2p, t3);
+                t4 = ana_sad(y3, e3p, t4);
+                x1 = y0;
+                e1p = y1;
+                e2p = y2;
+                e3p = y3;
+                if (b == 0 && j == 3 && c == 0) {
+                    s0t = t0;
+                    s1t = t1;
+                    s2t = t2;
+                    s3t = t3;
+                    s4t = t4;
+                }
             }
 #pragma unroll
             for (int j = 0; j < 8; j++) {
@@ -1608,6 +1651,11 @@ __device__ inline void ana_autoc(const typename Elem<DT>::T *base, const EncodeP
             for (int j = 0; j < 8; j++) prev[j] = cur[j];
         }
     }
+    ft[0] = t0 - s0t;
+    ft[1] = t1 - s1t;
+    ft[2] = t2 - s2t;
+    ft[3] = t3 - s3t;
+    ft[4] = t4 - s4t;
 }
 
 // min/max of a whole tile by one wave (16-bit samples, 16-B aligned rows): 16-B loads, kStatsLoads in flight per lane,
@@ -1711,7 +1759,7 @@ __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *
     double acc[kMaxLpc + 1];
 #pragma unroll
     for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
-    uint32_t or_acc = 0;
+    uint32_t or_acc = 0, ft[5];
     if constexpr (!SLOW) {
         int16_t *wl = slut[wave];
         if (mode == kNormLut) {
@@ -1727,18 +1775,18 @@ __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *
             }
             __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's LUT stores have landed (each wave reads only its own)
             __builtin_amdgcn_wave_barrier();
-            ana_autoc<DT, kAnaKindLds, kChunk>(base, P, g, s0, tn, wl, glut, window, vec, acc, or_acc);
+            ana_autoc<DT, kAnaKindLds, kChunk>(base, P, g, s0, tn, wl, glut, window, vec, acc, or_acc, ft);
         } else {
-            ana_autoc<DT, kAnaKindZero, kChunk>(base, P, g, s0, tn, wl, glut, window, vec, acc, or_acc);
+            ana_autoc<DT, kAnaKindZero, kChunk>(base, P, g, s0, tn, wl, glut, window, vec, acc, or_acc, ft);
         }
     } else {
         if (mode == kNormFastDiv)
-            ana_autoc<DT, kAnaKindFastDiv, kChunk>(base, P, g, s0, tn, nullptr, glut, window, vec, acc, or_acc);
+            ana_autoc<DT, kAnaKindFastDiv, kChunk>(base, P, g, s0, tn, nullptr, glut, window, vec, acc, or_acc, ft);
         else
-            ana_autoc<DT, kAnaKindGeneric, kChunk>(base, P, g, s0, tn, nullptr, glut, window, vec, acc, or_acc);
+            ana_autoc<DT, kAnaKindGeneric, kChunk>(base, P, g, s0, tn, nullptr, glut, window, vec, acc, or_acc, ft);
     }
     if (!live) return;
-    out[f] = analysis_finish(acc, or_acc, n, P);
+    out[f] = analysis_finish(acc, or_acc, n, P, ft);
 }
 
 // ---- wave helpers (64 lanes)
@@ -2165,6 +2213,41 @@ __device__ inline void resolve_and_store(const EncodeParams &P, PendingFrame &pf
     pf.f = -1;
 }
 
+// Sum of |e_K(j)| (order-K fixed residual) over a lane's 64 samples, packed as int16 pairs E[4 + m] = (x[2m],
+// x[2m+1]) with E[2..3] = the previous lane's last four samples; lane 0 starts at j = K (the warm-up).  Differences
+// are carried sign-flipped (y = e ^ 2^31) so |e_{k+1}| = v_sad_u32(y_k(i), y_k(i-1)) in one op.
+template <int K>
+__device__ inline uint32_t fixed_lane_sum(const uint32_t *E, bool l0) {
+    constexpr uint32_t M = 0x80000000u;
+    const int32_t h1 = (int32_t)E[3] >> 16, h2 = (int16_t)(E[3] & 0xFFFFu);
+    const int32_t h3 = (int32_t)E[2] >> 16, h4 = (int16_t)(E[2] & 0xFFFFu);
+    uint32_t p0 = (uint32_t)h1 ^ M, p1 = (uint32_t)(h1 - h2) ^ M, p2 = (uint32_t)((h1 - h2) - (h2 - h3)) ^ M;
+    uint32_t p3 = (uint32_t)(((h1 - h2) - (h2 - h3)) - ((h2 - h3) - (h3 - h4))) ^ M;
+    uint32_t s = 0;
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+        const uint32_t v = E[4 + (j >> 1)];
+        const int32_t x = (j & 1) ? ((int32_t)v >> 16) : (int32_t)(int16_t)(v & 0xFFFFu);
+        const uint32_t y0 = (uint32_t)x ^ M;
+        uint32_t y1 = 0, y2 = 0, y3 = 0, a, b;
+        if constexpr (K >= 2) y1 = (y0 - p0) ^ M;
+        if constexpr (K >= 3) y2 = (y1 - p1) ^ M;
+        if constexpr (K >= 4) y3 = (y2 - p2) ^ M;
+        if constexpr (K == 0) { a = y0; b = M; }
+        else if constexpr (K == 1) { a = y0; b = p0; }
+        else if constexpr (K == 2) { a = y1; b = p1; }
+        else if constexpr (K == 3) { a = y2; b = p2; }
+        else { a = y3; b = p3; }
+        if (j < K) s = l0 ? s : sad_u32(a, b, s);
+        else s = sad_u32(a, b, s);
+        p0 = y0;
+        if constexpr (K >= 2) p1 = y1;
+        if constexpr (K >= 3) p2 = y2;
+        if constexpr (K >= 4) p3 = y3;
+    }
+    return s;
+}
+
 template <int DT>
 __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const EncodeParams &P,
                                        const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
@@ -2238,70 +2321,13 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     };
     const bool l0 = lane == 0;
 
-    // ---- fixed predictor totals over samples 4..n-1 (fixed.c FLAC__fixed_compute_best_predictor) and
-    //      lane 0's warm-up extras wk = sum_{i=k}^{3} |e_k(i)| for the fixed partition sums.  Differences are
-    //      carried sign-flipped (y = e ^ 2^31) so |e_{k+1}| = v_sad_u32(y_k(i), y_k(i-1)) in one op.
-    uint32_t lt[5] = {0, 0, 0, 0, 0}, wx[5] = {0, 0, 0, 0, 0};
-    {
-        constexpr uint32_t M = 0x80000000u;
-        const int32_t h1 = (int32_t)E[3] >> 16, h2 = (int16_t)(E[3] & 0xFFFFu);
-        const int32_t h3 = (int32_t)E[2] >> 16, h4 = (int16_t)(E[2] & 0xFFFFu);
-        // biased state of sample i-1: y0 = x, y1 = e1, y2 = e2, y3 = e3
-        uint32_t p0 = (uint32_t)h1 ^ M, p1 = (uint32_t)(h1 - h2) ^ M, p2 = (uint32_t)((h1 - h2) - (h2 - h3)) ^ M;
-        uint32_t p3 = (uint32_t)(((h1 - h2) - (h2 - h3)) - ((h2 - h3) - (h3 - h4))) ^ M;
-#pragma unroll
-        for (int j = 0; j < 64; j++) {
-            if (j % 8 == 0 && j) {  // bound the scheduler's look-ahead (VGPR peak)
-#pragma unroll
-                for (int k = 0; k < 5; k++) asm volatile("" : "+v"(lt[k]));
-                asm volatile("" : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3));
-            }
-            const uint32_t y0 = (uint32_t)X(j) ^ M;
-            const uint32_t y1 = (y0 - p0) ^ M;
-            const uint32_t y2 = (y1 - p1) ^ M;
-            const uint32_t y3 = (y2 - p2) ^ M;
-            if (j >= 4) {
-                lt[0] = sad_u32(y0, M, lt[0]);
-                lt[1] = sad_u32(y0, p0, lt[1]);
-                lt[2] = sad_u32(y1, p1, lt[2]);
-                lt[3] = sad_u32(y2, p2, lt[3]);
-                lt[4] = sad_u32(y3, p3, lt[4]);
-            } else {
-                const uint32_t ae[5] = {sad_u32(y0, M, 0), sad_u32(y0, p0, 0), sad_u32(y1, p1, 0), sad_u32(y2, p2, 0),
-                                        sad_u32(y3, p3, 0)};
-#pragma unroll
-                for (int k = 0; k < 5; k++) {
-                    lt[k] += l0 ? 0u : ae[k];
-                    if (j >= k) wx[k] += l0 ? ae[k] : 0u;
-                }
-            }
-            p0 = y0;
-            p1 = y1;
-            p2 = y2;
-            p3 = y3;
-        }
-    }
-    reg_fence(E);
-    uint32_t tt[5];
-    dpp_wave_sum_multi<5>(lt, tt);
-    int guess;
-    {
-        const uint32_t m = min(min(tt[1], tt[2]), min(tt[3], tt[4]));
-        if (tt[0] <= m) guess = 0;
-        else if (tt[1] <= min(min(tt[2], tt[3]), tt[4])) guess = 1;
-        else if (tt[2] <= min(tt[3], tt[4])) guess = 2;
-        else if (tt[3] <= tt[4]) guess = 3;
-        else guess = 4;
-    }
+    // ---- fixed predictor: the order guess and its totals come from the analysis (fixed.c over samples 4..n-1);
+    //      here only the fixed candidate's lane partition sum of |e_guess(i)| is formed, below, when it is a
+    //      candidate at all
+    const int guess = A.fixed_order;
+    const uint32_t tg = A.fixed_tg;
     const double dn = (double)(n - 4);
-    uint32_t tg = tt[0], sf = lt[0] + wx[0];
-#pragma unroll
-    for (int k = 1; k < 5; k++)
-        if (guess == k) {
-            tg = tt[k];
-            sf = lt[k] + wx[k];
-        }
-    const float fb1 = (float)(tt[1] > 0 ? log(M_LN2 * (double)tt[1] / dn) / M_LN2 : 0.0);
+    const float fb1 = (float)(A.fixed_t1 > 0 ? log(M_LN2 * (double)A.fixed_t1 / dn) / M_LN2 : 0.0);
     const float fbg = (float)(tg > 0 ? log(M_LN2 * (double)tg / dn) / M_LN2 : 0.0);
     // constant test (all samples equal) only where libFLAC reaches it: fixed bits[1] == 0
     bool constant = false;
@@ -2317,6 +2343,16 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     const bool cand_fixed = !constant && !(fbg >= (float)sbps);
     const bool cand_lpc = !constant && (A.flags & kFlagLpcOk);
     const int of = guess, ol = A.lpc_order, lshift = A.lpc_shift;
+    uint32_t sf = 0;  // the lane's sum of |e_of(i)| (lane 0 from i = of)
+    if (cand_fixed) {
+        switch (of) {  // wave-uniform
+        case 0: sf = fixed_lane_sum<0>(E, l0); break;
+        case 1: sf = fixed_lane_sum<1>(E, l0); break;
+        case 2: sf = fixed_lane_sum<2>(E, l0); break;
+        case 3: sf = fixed_lane_sum<3>(E, l0); break;
+        default: sf = fixed_lane_sum<4>(E, l0); break;
+        }
+    }
 
     uint32_t CL[4];
 #pragma unroll
