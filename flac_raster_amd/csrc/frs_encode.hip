@@ -1987,14 +1987,14 @@ constexpr uint64_t kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62, kValMask = (1u
 // the fixed candidate's partition sums fall out of the fixed-predictor totals pass.
 constexpr int kFrameWordsV3 = 2176;  // 69632 bits >= worst exact frame (estimate < verbatim)
 constexpr int kXpowBytes = kFrameWordsV3 * 4 + 64;  // multiple of 64 (LDS split tables)
-__constant__ uint16_t c_crc16x4[4][256];           // T_k[v] = CRC-16 of byte v followed by k zero bytes
+__constant__ uint16_t c_crc16x8[8][256];           // T_k[v] = CRC-16 of byte v followed by k zero bytes
 __device__ uint16_t g_xpow_bytes[kXpowBytes];      // x^(8m) mod P for m bytes
 
 constexpr int kXpowHi = (kXpowBytes + 63) / 64;
 struct EncV3Shared {
     uint32_t bits[4][kFrameWordsV3];
     int16_t lut[kLutCap];
-    uint16_t crc4[4][256];
+    uint16_t crc8x[8][256];  // slice-by-8 tables (T_0..T_3 serve the slice-by-4 / byte steps)
     uint16_t xlo[64];       // x^(8m) mod P, m = 0..63
     uint16_t xhi[kXpowHi];  // x^(8*64*m) mod P
     uint8_t crc8[256];
@@ -2647,26 +2647,33 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         const int typecode = type == 0 ? 0 : type == 1 ? 1 : type == 2 ? 8 + of : 32 + ol - 1;
         lds_put_bits2(fbuf, M, hdr_bits, (uint32_t)(typecode << 1) | (w ? 1u : 0u), 8);
         if (w) lds_put_bits2(fbuf, M, hdr_bits + 8 + (uint32_t)(w - 1), 1, 1);
-        const uint32_t smask = (1u << sbps) - 1u;
-        if (type == 0) lds_put_bits2(fbuf, M, pos0, (uint32_t)X(0) & smask, sbps);
+        if (type == 0) lds_put_bits2(fbuf, M, pos0, (uint32_t)X(0) & ((1u << sbps) - 1u), sbps);
         if (type >= 2) {
-            uint32_t q = pos0;
-#pragma unroll
-            for (int i = 0; i < kMaxLpc; i++)
-                if (i < o) lds_put_bits2(fbuf, M, q + (uint32_t)i * sbps, (uint32_t)X(i) & smask, sbps);
-            q += (uint32_t)o * sbps;
+            uint32_t q = pos0 + (uint32_t)o * sbps;
             if (type == 3) {
                 lds_put_bits2(fbuf, M, q, (uint32_t)(A.lpc_prec - 1), 4);
                 lds_put_bits2(fbuf, M, q + 4, (uint32_t)lshift & 31u, 5);
-#pragma unroll
-                for (int i = 0; i < kMaxLpc; i++)
-                    if (i < o)
-                        lds_put_bits2(fbuf, M, q + 9 + (uint32_t)i * A.lpc_prec,
-                                      (uint32_t)A.q[i] & ((1u << A.lpc_prec) - 1u), A.lpc_prec);
                 q += 9 + (uint32_t)o * A.lpc_prec;
             }
             lds_put_bits2(fbuf, M, q, (uint32_t)po, 6);  // RICE (00) + partition order (4 bits)
         }
+    }
+    if (type >= 2) {
+        // warm-up samples and quantised coefficients in parallel: lane i < o writes lane 0's sample i, lane 8 + i
+        // (LPC) coefficient i
+        const int i = lane & 7;
+        uint32_t w01 = (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 0], 0);
+        w01 = (i >> 1) == 1 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 1], 0) : w01;
+        w01 = (i >> 1) == 2 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 2], 0) : w01;
+        w01 = (i >> 1) == 3 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 3], 0) : w01;
+        const uint32_t xi = (i & 1) ? (w01 >> 16) : (w01 & 0xFFFFu);
+        const int32_t qi = ana[f].q[i];  // (a lane-indexed load: a select chain over A.q costs registers)
+        const bool warm = lane < 8 && i < o, coef = type == 3 && lane >= 8 && lane < 16 && i < o;
+        if (warm)
+            lds_put_bits2(fbuf, M, pos0 + (uint32_t)i * sbps, xi & ((1u << sbps) - 1u), sbps);
+        if (coef)
+            lds_put_bits2(fbuf, M, pos0 + (uint32_t)o * sbps + 9 + (uint32_t)i * A.lpc_prec,
+                          (uint32_t)qi & ((1u << A.lpc_prec) - 1u), A.lpc_prec);
     }
     if (type >= 2 && ok && (lane & (lanes_per - 1)) == 0) lds_put_bits2(fbuf, M, run - 4u, (uint32_t)k, 4);
     if (type == 1) {
@@ -2708,17 +2715,27 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         const uint32_t wb = min(nfw, (uint32_t)lane * M.c), we = min(nfw, wb + M.c);
         uint32_t c = 0;
         const uint32_t *colp = fbuf + lane;
-        for (uint32_t i = wb; i < we; i++, colp += 64) {
+        // slice-by-8 (two words per step: the table lookups that depend on the running CRC, and so the
+        // latency chain, are halved), then one slice-by-4 step for an odd word
+        const uint16_t(*T)[256] = S.crc8x;
+        uint32_t i = wb;
+        for (; i + 1 < we; i += 2, colp += 128) {
+            const uint32_t w0 = colp[0], w1 = colp[64];
+            c = (uint32_t)T[7][((c >> 8) ^ (w0 >> 24)) & 0xFF] ^ T[6][((c & 0xFF) ^ (w0 >> 16)) & 0xFF] ^
+                T[5][(w0 >> 8) & 0xFF] ^ T[4][w0 & 0xFF] ^ T[3][w1 >> 24] ^ T[2][(w1 >> 16) & 0xFF] ^
+                T[1][(w1 >> 8) & 0xFF] ^ T[0][w1 & 0xFF];
+        }
+        if (i < we) {
             const uint32_t word = *colp;
-            c = (uint32_t)S.crc4[3][((c >> 8) ^ (word >> 24)) & 0xFF] ^ S.crc4[2][((c & 0xFF) ^ (word >> 16)) & 0xFF] ^
-                S.crc4[1][(word >> 8) & 0xFF] ^ S.crc4[0][word & 0xFF];
+            c = (uint32_t)T[3][((c >> 8) ^ (word >> 24)) & 0xFF] ^ T[2][((c & 0xFF) ^ (word >> 16)) & 0xFF] ^
+                T[1][(word >> 8) & 0xFF] ^ T[0][word & 0xFF];
         }
         uint32_t end = we * 4;
         if (lane == (int)M.col(nfw - 1)) {
             const uint32_t word = fbuf[M(nfw)];
             for (uint32_t b = 0; b < tail; b++) {
                 const uint32_t byte = (word >> (24 - 8 * b)) & 0xFF;
-                c = ((c << 8) & 0xFFFFu) ^ S.crc4[0][((c >> 8) ^ byte) & 0xFF];
+                c = ((c << 8) & 0xFFFFu) ^ S.crc8x[0][((c >> 8) ^ byte) & 0xFF];
             }
             end += tail;
         }
@@ -2742,7 +2759,7 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
                                                   const int64_t *__restrict__ pbytes) {
     __shared__ EncV3Shared S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int i = threadIdx.x; i < 1024; i += blockDim.x) (&S.crc4[0][0])[i] = (&c_crc16x4[0][0])[i];
+    for (int i = threadIdx.x; i < 2048; i += blockDim.x) (&S.crc8x[0][0])[i] = (&c_crc16x8[0][0])[i];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) S.crc8[i] = c_crc8[i];
     for (int i = threadIdx.x; i < 64; i += blockDim.x) S.xlo[i] = g_xpow_bytes[i];
     for (int i = threadIdx.x; i < kXpowHi; i += blockDim.x) S.xhi[i] = g_xpow_bytes[64 * i];
@@ -2829,11 +2846,11 @@ static int upload_tables(frs_ctx *ctx) {
     FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_crc8), t8, sizeof(t8), 0, hipMemcpyHostToDevice, ctx->stream));
     FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_crc16), t16, sizeof(t16), 0, hipMemcpyHostToDevice, ctx->stream));
     FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_xpow8), xp, sizeof(xp), 0, hipMemcpyHostToDevice, ctx->stream));
-    // slice-by-4 tables: T_k[v] = T_{k-1}[v] advanced by one zero byte
-    static uint16_t t4[4][256];
+    // slice-by-8 tables: T_k[v] = T_{k-1}[v] advanced by one zero byte
+    static uint16_t t4[8][256];
     static uint16_t xb[kXpowBytes];
     for (int i = 0; i < 256; i++) t4[0][i] = t16[i];
-    for (int k = 1; k < 4; k++)
+    for (int k = 1; k < 8; k++)
         for (int i = 0; i < 256; i++) {
             const uint16_t c = t4[k - 1][i];
             t4[k][i] = (uint16_t)(((c << 8) & 0xFFFF) ^ t16[c >> 8]);
@@ -2843,7 +2860,7 @@ static int upload_tables(frs_ctx *ctx) {
         xb[m] = (uint16_t)pw;
         pw = mulmod(pw, 0x100);
     }
-    FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_crc16x4), t4, sizeof(t4), 0, hipMemcpyHostToDevice, ctx->stream));
+    FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_crc16x8), t4, sizeof(t4), 0, hipMemcpyHostToDevice, ctx->stream));
     FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xpow_bytes), xb, sizeof(xb), 0, hipMemcpyHostToDevice, ctx->stream));
     FRS_HIP(hipStreamSynchronize(ctx->stream));
     g_tables_ready[ctx->device] = true;
