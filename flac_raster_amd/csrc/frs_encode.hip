@@ -2008,19 +2008,18 @@ struct EncV3Shared {
 // bank is the column.  Lane L's codes fill roughly column L, so the 64 lanes' concurrent bit-writer atomics
 // land in distinct banks whatever each lane's progress (in the plain layout they hit banks
 // (base_L + progress_L) mod 32: a birthday-problem 3-4 way conflict).  w / C = (w * ceil(2^20 / C)) >> 20,
-// exact for w < 2400 and C <= 34, and the column of bit position b is mulhi(b, ceil(2^32 / 32 C)), exact for
-// b < 2^17 (both checked exhaustively), so phys costs a multiply and a 24-bit mad.
+// exact for w < 2400 and C <= 34 (checked exhaustively): full-rate 24-bit multiplies only (a 32-bit mulhi is a
+// quarter-rate op, and the compiler widened it to a 64-bit product).
 struct FbMap {
-    uint32_t c, magic, k, bmagic;  // C, ceil(2^20 / C), 64 C - 1, ceil(2^32 / 32 C)
+    uint32_t c, magic, k;  // C, ceil(2^20 / C), 64 C - 1
     __device__ inline uint32_t col(uint32_t w) const { return __umul24(w, magic) >> 20; }
     __device__ inline uint32_t operator()(uint32_t w) const {
         return (uint32_t)__mul24((int)col(w), -(int)k) + (w << 6);
     }
-    __device__ inline uint32_t bitcol(uint32_t b) const { return __umulhi(b, bmagic); }
 };
 __device__ inline FbMap fb_map(uint32_t words) {  // words the frame may touch (<= kFrameWordsV3)
     const uint32_t c = max(1u, (words + 63) >> 6);
-    return FbMap{c, ((1u << 20) + c - 1) / c, 64 * c - 1, (uint32_t)((0x100000000ull + 32 * c - 1) / (32 * c))};
+    return FbMap{c, ((1u << 20) + c - 1) / c, 64 * c - 1};
 }
 
 // bit writer without branches: the (up to 32-bit) code at [pos, pos + nbits) straddles at most 2 words
@@ -2050,9 +2049,9 @@ __device__ inline void lds_put_left(uint32_t *buf, const FbMap &M, uint32_t pos,
     const uint32_t hi = __builtin_amdgcn_alignbit(0u, codeL, pos);  // codeL >> (pos & 31)
     const uint32_t lo = __builtin_amdgcn_alignbit(codeL, 0u, pos);  // codeL << (32 - (pos & 31)); 0 if aligned
     // phys(wi + 1) = (wi << 6) - col(wi + 1) (64 C - 1) + 64; the + 64 folds into the ds offset
-    const uint32_t base = (pos >> 5) << 6;
-    atomicOr(buf + ((uint32_t)__mul24((int)M.bitcol(pos), -(int)M.k) + base), hi);
-    atomicOr(buf + ((uint32_t)__mul24((int)M.bitcol(pos + 32), -(int)M.k) + base) + 64, lo);
+    const uint32_t wi = pos >> 5, base = wi << 6;
+    atomicOr(buf + ((uint32_t)__mul24((int)M.col(wi), -(int)M.k) + base), hi);
+    atomicOr(buf + ((uint32_t)__mul24((int)M.col(wi + 1), -(int)M.k) + base) + 64, lo);
 }
 
 __device__ inline uint32_t zigzag(int32_t r) { return ((uint32_t)r << 1) ^ (uint32_t)(r >> 31); }

@@ -105,6 +105,29 @@ VARIANTS["lb3_rf"] = chain(LB3, RESOLVE_FIRST)
 VARIANTS["rf"] = RESOLVE_FIRST
 
 
+def hist(src):
+    """(subframe type, order) histogram of the fast encoder's frames, printed to stderr after each launch"""
+    s = src
+    rep = [
+        ("template <int DT>\n__device__ inline void encode_frame_v3(",
+         "__device__ unsigned int g_hist[64];\ntemplate <int DT>\n__device__ inline void encode_frame_v3("),
+        ("    // ---- phase A: sizes only", "    if (l0) atomicAdd(&g_hist[type * 16 + (type == 2 ? of : type == 3 ? ol : 0)], 1u);\n"
+         "    // ---- phase A: sizes only"),
+        ("        prof_end(ctx, \"encode\", ev);\n",
+         "        prof_end(ctx, \"encode\", ev);\n        if (getenv(\"FRS_HIST\")) {\n            unsigned h[64];\n"
+         "            hipStreamSynchronize(st);\n            hipMemcpyFromSymbol(h, HIP_SYMBOL(g_hist), sizeof(h));\n"
+         "            fprintf(stderr, \"HIST\");\n            for (int i = 0; i < 64; i++) if (h[i]) fprintf(stderr, \" %d:%u\", i, h[i]);\n"
+         "            fprintf(stderr, \"\\n\");\n            memset(h, 0, sizeof(h));\n            hipMemcpyToSymbol(HIP_SYMBOL(g_hist), h, sizeof(h));\n        }\n"),
+    ]
+    for a, b in rep:
+        assert a in s, a[:70]
+        s = s.replace(a, b, 1)
+    return s
+
+
+VARIANTS["hist"] = hist
+
+
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
     for n in names:
