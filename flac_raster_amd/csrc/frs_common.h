@@ -70,7 +70,7 @@ struct EncodeParams {
     int64_t nframes;
     int32_t ntiles;
     int32_t norm_mode;    // 0 converter.py:56-86, 1 spatial_encoder.py:229-248
-    int32_t vec_ok;       // rows 16-B aligned and tile widths multiples of 64 (fast loads)
+    int32_t vec_ok;       // alignment class of the row segments: 16, 8 or 4 bytes (vector loads), 0 = gather
 };
 
 __host__ __device__ inline int ilog2_u32(uint32_t v) { return 31 - __builtin_clz(v); }

@@ -1400,9 +1400,28 @@ template <int DT, int N> struct ChunkN {
             }
         }
     }
-    __device__ inline void load(const T *base, int64_t row_stride, int width, int64_t row, int col, bool vec,
+    // 8- / 4-byte loads of one row segment (rows only 8- or 4-byte aligned, e.g. a 10980-sample int16 row)
+    __device__ inline void load_vec8(const T *p_) {
+        const uint2 *p = reinterpret_cast<const uint2 *>(p_);
+#pragma unroll
+        for (int k = 0; k < kWords / 2; k++) {
+            const uint2 v = p[k];
+            w[2 * k] = v.x;
+            w[2 * k + 1] = v.y;
+        }
+    }
+    __device__ inline void load_vec4(const T *p_) {
+        const uint32_t *p = reinterpret_cast<const uint32_t *>(p_);
+#pragma unroll
+        for (int k = 0; k < kWords; k++) w[k] = p[k];
+    }
+    // vec = the row segments' alignment class (EncodeParams::vec_ok): 16, 8 or 4 bytes, 0 = element gather
+    __device__ inline void load(const T *base, int64_t row_stride, int width, int64_t row, int col, int vec,
                                 int nvalid) {
-        if (vec) load_vec(base + row * row_stride + col);
+        const T *p = base + row * row_stride + col;
+        if (vec == 16) load_vec(p);
+        else if (vec == 8) load_vec8(p);
+        else if (vec == 4) load_vec4(p);
         else load_gather(base, row_stride, width, row, col, nvalid);
     }
 };
@@ -1593,7 +1612,7 @@ __device__ inline uint32_t ana_sad(uint32_t a, uint32_t b, uint32_t c) {  // |a 
 template <int DT, int KIND, int kAnaChunk>
 __device__ inline void ana_autoc(const typename Elem<DT>::T *base, const EncodeParams &P, const TileGeom &g,
                                  int64_t s0, const TileNorm &tn, const int16_t *slut, const int16_t *glut,
-                                 const float *__restrict__ swin, bool vec, double *acc, uint32_t &or_acc, uint32_t *ft) {
+                                 const float *__restrict__ swin, int vec, double *acc, uint32_t &or_acc, uint32_t *ft) {
     using Ch = ChunkN<DT, kAnaChunk>;
     const uint32_t r0 = udiv_inv((uint32_t)s0, (uint32_t)g.w, 1.0 / (double)g.w);
     int64_t crow = r0;
@@ -1755,7 +1774,7 @@ __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *
     const int64_t tile_px = (int64_t)g.h * g.w;
     const int n = live ? (int)min((int64_t)P.blocksize, tile_px - s0) : 0;
     constexpr int kChunk = SLOW ? 16 : 64;  // samples per lane load (SLOW: fewer VGPRs beside the fp64 division)
-    const bool vec = P.vec_ok && (g.w % kChunk) == 0;
+    const int vec = (g.w % kChunk) == 0 ? P.vec_ok : 0;
     double acc[kMaxLpc + 1];
 #pragma unroll
     for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
@@ -2304,7 +2323,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         Chunk64<DT> ch;
         const uint32_t sl0 = (uint32_t)s0 + 64u * (uint32_t)lane;  // tile pixels < 2^31
         const uint32_t row = udiv_inv(sl0, (uint32_t)g.w, 1.0 / (double)g.w);
-        ch.load(base, P.row_stride, g.w, row, (int)(sl0 - row * (uint32_t)g.w), P.vec_ok && (g.w % 64) == 0, 64);
+        ch.load(base, P.row_stride, g.w, row, (int)(sl0 - row * (uint32_t)g.w), (g.w % 64) == 0 ? P.vec_ok : 0, 64);
         int32_t lo = 0;
         norm_chunk<DT>(ch, tn, lut, [&](int j, int32_t x) {
             if (j & 1) E[4 + (j >> 1)] = pack2(lo, x >> w);
@@ -3061,8 +3080,13 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     }
     if constexpr (!Elem<DT>::is_float) if (fast) {
         const int es = (int)sizeof(T);
-        P.vec_ok = ((d->row_stride * es) % 16 == 0) && (d->tile_w % 64 == 0) &&
-                   ((reinterpret_cast<uintptr_t>(raster_dev) + (size_t)d->band0 * d->band_stride * es) % 16 == 0);
+        // alignment class of the 64-sample row segments (tiles whose width is a multiple of 64): the widest of 16,
+        // 8, 4 bytes dividing the band base, the row stride and the tile width in bytes
+        const uintptr_t b0 = reinterpret_cast<uintptr_t>(raster_dev) + (size_t)d->band0 * d->band_stride * es;
+        P.vec_ok = 0;
+        for (int a : {16, 8, 4})
+            if (P.vec_ok == 0 && (d->row_stride * es) % a == 0 && b0 % a == 0 && ((int64_t)d->tile_w * es) % a == 0)
+                P.vec_ok = a;
         FRS_HIP(ctx->luts.ensure(sizeof(int16_t) * (size_t)kLutCap * ntiles));
         FRS_HIP(ctx->status.ensure(sizeof(uint64_t) * (nframes + 1) + 64));
         if (!fuse_stats) k_build_lut<DT><<<ntiles, 256, 0, st>>>(dnorms, ctx->luts.as<int16_t>());

@@ -163,6 +163,7 @@ def test_c5_bbox_queries_match_linear_scan_and_oracle(gpu_ctx, c4):
     ((10980, 10980), 1024, np.uint16),  # the reference's Sentinel-2 B04 example (FLAC-SPATIAL.md:82-88): last tile 740^2
     ((512, 512), 200, np.int16),        # sample_dem at tile 200: every tile ends in a partial frame
     ((1000, 1000), 30, np.int16),       # tiles smaller than one frame (900 px: a single partial frame each)
+    ((1030, 4098), 128, np.int16),      # rows only 4-byte aligned (8196-B stride): dword chunk loads
 ])
 def test_partial_frame_tiles_take_the_fast_path(gpu_ctx, shape, tile, dtype):
     """Tiles whose pixel count is not a multiple of 4096 keep the fast kernels (their partial last frames are coded
