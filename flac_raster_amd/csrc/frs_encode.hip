@@ -338,88 +338,14 @@ __device__ inline double expected_bits(double lpc_error, double error_scale) {
 
 // ------------------------------------------------------------------------------------ k_analyze
 // One lane per subframe; lanes of a wave walk their blocks in lockstep so the window sample is uniform.
-template <int DT, bool WIDE>
-__global__ void __launch_bounds__(128) k_analyze(const typename Elem<DT>::T *raster, EncodeParams P,
-                                                const TileGeom *tiles, const TileNorm *norms,
-                                                const float *__restrict__ window, SubAnalysis *out,
-                                                const int64_t *__restrict__ flist, int64_t nlist) {
-    // flist: the frames to analyse (the fast path's partial last frames), nullptr = every frame of the job
-    using T = typename Elem<DT>::T;
-    const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t nsub = (flist ? nlist : P.nframes) * P.nch;
-    const bool live = li < nsub;
-    const int64_t fi = live ? li / P.nch : 0;
-    const int ch = live ? (int)(li - fi * P.nch) : 0;
-    const int64_t f = flist ? flist[fi] : fi;
-    const int64_t sub = f * P.nch + ch;
-    const int t = tile_of_frame(tiles, P.ntiles, f);
-    const TileGeom g = tiles[t];
-    const int64_t s0 = (f - g.frame_base) * P.blocksize;
-    const int64_t tile_px = (int64_t)g.h * g.w;
-    const int n = live ? (int)((tile_px - s0) < P.blocksize ? (tile_px - s0) : P.blocksize) : 0;
-    const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits, P.norm_mode);
-
-    int64_t row = s0 / g.w;
-    int col = (int)(s0 - row * g.w);
-    const T *rowp = raster + (int64_t)(P.band0 + ch) * P.band_stride + (g.r0 + row) * P.row_stride + g.c0;
-
-    uint32_t or_acc = 0, diff = 0;
-    int32_t x0 = 0, x1 = 0, p1 = 0, p2 = 0, p3 = 0;
-    uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
-    double acc[kMaxLpc + 1];
-#pragma unroll
-    for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
-    double prev[8], cur[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) prev[j] = 0.0;
-
-    const int nloop = P.blocksize;  // uniform trip count; lanes with shorter blocks are predicated off
-    for (int i0 = 0; i0 < nloop; i0 += 8) {
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const int i = i0 + j;
-            int32_t x = 0;
-            if (i < n) {
-                x = nz(rowp[col]);
-                if (++col == g.w) {
-                    col = 0;
-                    rowp += P.row_stride;
-                }
-                if (i == 0) x0 = x;
-                or_acc |= (uint32_t)x;
-                diff |= (uint32_t)(x ^ x0);
-                if constexpr (!WIDE) {
-                    // 16-bit streams: |e_k| < 2^20, totals over samples 4..n-1 (fixed.c, data+4)
-                    const int32_t e1 = x - x1, e2 = e1 - p1, e3 = e2 - p2, e4 = e3 - p3;
-                    if (i >= 4) {
-                        t0 += (uint32_t)abs(x);
-                        t1 += (uint32_t)abs(e1);
-                        t2 += (uint32_t)abs(e2);
-                        t3 += (uint32_t)abs(e3);
-                        t4 += (uint32_t)abs(e4);
-                    }
-                    p3 = e3;
-                    p2 = e2;
-                    p1 = e1;
-                    x1 = x;
-                }
-            }
-            // inactive lanes have x == 0 -> contribute exact zeros; window index is wave-uniform
-            cur[j] = (double)((float)x * window[i]);
-        }
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-#pragma unroll
-            for (int l = 0; l <= kMaxLpc; l++) {
-                const double other = (j - l >= 0) ? cur[j - l] : prev[8 + j - l];
-                acc[l] = fma(cur[j], other, acc[l]);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 8; j++) prev[j] = cur[j];
-    }
-    if (!live) return;
-
+// The level-5 decisions of one subframe from its sums (stream_encoder.c process_subframe_ up to the encode):
+// wasted bits, constant test, fixed-predictor guess (fixed.c, totals over samples 4..n-1), LPC order by expected
+// bits, Levinson coefficients and their quantisation (lpc.c).  acc = windowed autocorrelation lags 0..8, t = fixed
+// totals of orders 0..4, or_acc = OR of the samples, diff = OR of (x ^ x[0]).
+template <bool WIDE>
+__device__ inline SubAnalysis generic_decide(const double *acc, const uint64_t *tt, uint32_t or_acc, uint32_t diff,
+                                             int n, const EncodeParams &P) {
+    const uint64_t t0 = tt[0], t1 = tt[1], t2 = tt[2], t3 = tt[3], t4 = tt[4];
     SubAnalysis A;
     A.n = n;
     int w = 0;
@@ -564,7 +490,189 @@ __global__ void __launch_bounds__(128) k_analyze(const typename Elem<DT>::T *ras
             }
         }
     }
-    out[sub] = A;
+    return A;
+}
+
+template <int DT, bool WIDE>
+__global__ void __launch_bounds__(128) k_analyze(const typename Elem<DT>::T *raster, EncodeParams P,
+                                                const TileGeom *tiles, const TileNorm *norms,
+                                                const float *__restrict__ window, SubAnalysis *out,
+                                                const int64_t *__restrict__ flist, int64_t nlist) {
+    // flist: the frames to analyse (the fast path's partial last frames), nullptr = every frame of the job
+    using T = typename Elem<DT>::T;
+    const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nsub = (flist ? nlist : P.nframes) * P.nch;
+    const bool live = li < nsub;
+    const int64_t fi = live ? li / P.nch : 0;
+    const int ch = live ? (int)(li - fi * P.nch) : 0;
+    const int64_t f = flist ? flist[fi] : fi;
+    const int64_t sub = f * P.nch + ch;
+    const int t = tile_of_frame(tiles, P.ntiles, f);
+    const TileGeom g = tiles[t];
+    const int64_t s0 = (f - g.frame_base) * P.blocksize;
+    const int64_t tile_px = (int64_t)g.h * g.w;
+    const int n = live ? (int)((tile_px - s0) < P.blocksize ? (tile_px - s0) : P.blocksize) : 0;
+    const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits, P.norm_mode);
+
+    int64_t row = s0 / g.w;
+    int col = (int)(s0 - row * g.w);
+    const T *rowp = raster + (int64_t)(P.band0 + ch) * P.band_stride + (g.r0 + row) * P.row_stride + g.c0;
+
+    uint32_t or_acc = 0, diff = 0;
+    int32_t x0 = 0, x1 = 0, p1 = 0, p2 = 0, p3 = 0;
+    uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+    double acc[kMaxLpc + 1];
+#pragma unroll
+    for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
+    double prev[8], cur[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) prev[j] = 0.0;
+
+    const int nloop = P.blocksize;  // uniform trip count; lanes with shorter blocks are predicated off
+    // raw sample i (< n) at the row cursor, which then advances
+    auto fetch = [&](int i) -> T {
+        T v = T(0);
+        if (i < n) {
+            v = rowp[col];
+            if (++col == g.w) {
+                col = 0;
+                rowp += P.row_stride;
+            }
+        }
+        return v;
+    };
+    auto block8 = [&](int i0, const T *raw) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const int i = i0 + j;
+            int32_t x = 0;
+            if (i < n) {
+                x = nz(raw[j]);
+                if (i == 0) x0 = x;
+                or_acc |= (uint32_t)x;
+                diff |= (uint32_t)(x ^ x0);
+                if constexpr (!WIDE) {
+                    // 16-bit streams: |e_k| < 2^20, totals over samples 4..n-1 (fixed.c, data+4)
+                    const int32_t e1 = x - x1, e2 = e1 - p1, e3 = e2 - p2, e4 = e3 - p3;
+                    if (i >= 4) {
+                        t0 += (uint32_t)abs(x);
+                        t1 += (uint32_t)abs(e1);
+                        t2 += (uint32_t)abs(e2);
+                        t3 += (uint32_t)abs(e3);
+                        t4 += (uint32_t)abs(e4);
+                    }
+                    p3 = e3;
+                    p2 = e2;
+                    p1 = e1;
+                    x1 = x;
+                }
+            }
+            // inactive lanes have x == 0 -> contribute exact zeros; window index is wave-uniform
+            cur[j] = (double)((float)x * window[i]);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+#pragma unroll
+            for (int l = 0; l <= kMaxLpc; l++) {
+                const double other = (j - l >= 0) ? cur[j - l] : prev[8 + j - l];
+                acc[l] = fma(cur[j], other, acc[l]);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) prev[j] = cur[j];
+    };
+    for (int i0 = 0; i0 < nloop; i0 += 8) {
+        T raw[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) raw[j] = fetch(i0 + j);
+        block8(i0, raw);
+    }
+    if (!live) return;
+
+    const uint64_t tt[5] = {t0, t1, t2, t3, t4};
+    out[sub] = generic_decide<WIDE>(acc, tt, or_acc, diff, n, P);
+}
+
+// The fast path's partial last frames (n < blocksize, at most one per tile, 16-bit mono streams): one work-group per
+// frame instead of one lane (k_analyze's lane walks 4096 samples with fp64 divisions: ~0.75 ms for any number of
+// frames).  The frame is normalised and windowed in parallel into LDS; lag l of the autocorrelation is summed by
+// thread l in libFLAC's sequential order (the same fma sequence as k_analyze's lane, so bit-identical); the fixed
+// totals, the OR and the constant test are integer reductions (order-free); thread 0 makes the decisions.
+constexpr int kPartThreads = 256;
+template <int DT>
+__global__ void __launch_bounds__(kPartThreads) k_analyze_partial(const typename Elem<DT>::T *raster, EncodeParams P,
+                                                                 const TileGeom *tiles, const TileNorm *norms,
+                                                                 const float *__restrict__ window, SubAnalysis *out,
+                                                                 const int64_t *__restrict__ flist) {
+    using T = typename Elem<DT>::T;
+    __shared__ int32_t xs[kMaxBlock];
+    __shared__ double xw[kMaxBlock];
+    __shared__ unsigned long long red_t[5];
+    __shared__ uint32_t red_or, red_diff;
+    __shared__ double red_acc[kMaxLpc + 1];
+    const int64_t f = flist[blockIdx.x];
+    const int t = tile_of_frame(tiles, P.ntiles, f);
+    const TileGeom g = tiles[t];
+    const int64_t s0 = (f - g.frame_base) * P.blocksize;
+    const int64_t tile_px = (int64_t)g.h * g.w;
+    const int n = (int)((tile_px - s0) < P.blocksize ? (tile_px - s0) : P.blocksize);
+    const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits, P.norm_mode);
+    const T *tb = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
+    if (threadIdx.x < 5) red_t[threadIdx.x] = 0;
+    if (threadIdx.x == 0) red_or = red_diff = 0;
+    // 1. normalise + window (samples past n are zeros, as in k_analyze)
+    for (int i = threadIdx.x; i < P.blocksize; i += kPartThreads) {
+        int32_t x = 0;
+        if (i < n) {
+            const int64_t q = s0 + i, r = q / g.w;
+            x = nz(tb[r * P.row_stride + (q - r * g.w)]);
+        }
+        xs[i] = x;
+        xw[i] = (double)((float)x * window[i]);
+    }
+    __syncthreads();
+    // 2. integer reductions over the frame: OR (wasted bits), OR of x ^ x[0] (constant), fixed totals over 4..n-1
+    const int32_t x0 = xs[0];
+    uint32_t o = 0, d = 0;
+    uint64_t tk[5] = {0, 0, 0, 0, 0};
+    for (int i = threadIdx.x; i < n; i += kPartThreads) {
+        const int32_t x = xs[i];
+        o |= (uint32_t)x;
+        d |= (uint32_t)(x ^ x0);
+        if (i >= 4) {
+            const int32_t a = xs[i - 1], b = xs[i - 2], c = xs[i - 3], e = xs[i - 4];
+            const int32_t e1 = x - a, e2 = e1 - (a - b), e3 = e2 - ((a - b) - (b - c));
+            const int32_t e4 = e3 - (((a - b) - (b - c)) - ((b - c) - (c - e)));
+            tk[0] += (uint32_t)abs(x);
+            tk[1] += (uint32_t)abs(e1);
+            tk[2] += (uint32_t)abs(e2);
+            tk[3] += (uint32_t)abs(e3);
+            tk[4] += (uint32_t)abs(e4);
+        }
+    }
+    atomicOr(&red_or, o);
+    atomicOr(&red_diff, d);
+#pragma unroll
+    for (int k = 0; k < 5; k++) atomicAdd(&red_t[k], (unsigned long long)tk[k]);
+    // 3. autocorrelation: lag l by thread l, i ascending (k_analyze's order)
+    if (threadIdx.x <= kMaxLpc) {
+        const int l = threadIdx.x;
+        double a = 0.0;
+        int i = 0;
+        for (; i < kMaxLpc; i++) a = fma(xw[i], i >= l ? xw[i - l] : 0.0, a);
+        // (LDS reads of later terms issue ahead of the fma chain)
+#pragma unroll 16
+        for (; i < P.blocksize; i++) a = fma(xw[i], xw[i - l], a);
+        red_acc[l] = a;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double acc[kMaxLpc + 1];
+#pragma unroll
+        for (int l = 0; l <= kMaxLpc; l++) acc[l] = red_acc[l];
+        const uint64_t tt[5] = {red_t[0], red_t[1], red_t[2], red_t[3], red_t[4]};
+        out[f] = generic_decide<false>(acc, tt, red_or, red_diff, n, P);
+    }
 }
 
 // 32-bit streams (bits_per_sample 24 -> pyflac bps 32) use libFLAC's limit_residual fixed estimator;
@@ -1376,7 +1484,52 @@ template <int DT, int N> struct ChunkN {
             w[4 * k + 3] = v.w;
         }
     }
-    // element gather with a row cursor starting at (row, col) (frames that cross rows mid-chunk)
+    // element gather with a row cursor starting at (row, col): tiles whose width is not a multiple of the chunk
+    // (edge tiles, odd tile sizes).  Fully unrolled: the cursor advances by per-lane selects, so all N loads issue
+    // before the first wait; 16-bit samples land pairwise in the halves of one register (d16 / d16_hi loads).
+    // The fast paths only load whole chunks of full frames (nvalid == N).
+    __device__ inline void load_gather_unrolled(const T *base, int64_t row_stride, int width, int64_t row, int col,
+                                                int nvalid) {
+        (void)nvalid;
+        const T *rp = base + row * row_stride;
+        auto next = [&]() {
+            if (++col == width) {
+                col = 0;
+                rp += row_stride;
+            }
+        };
+        if constexpr (sizeof(T) == 2) {
+            typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+            for (int k = 0; k < kWords; k++) {
+                u16x2 pr;
+                pr.x = __builtin_bit_cast(unsigned short, rp[col]);
+                next();
+                pr.y = __builtin_bit_cast(unsigned short, rp[col]);
+                next();
+                w[k] = __builtin_bit_cast(uint32_t, pr);
+            }
+        } else if constexpr (sizeof(T) == 4) {
+#pragma unroll
+            for (int k = 0; k < kWords; k++) {
+                w[k] = __builtin_bit_cast(uint32_t, rp[col]);
+                next();
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kWords; k++) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int b = 0; b < 4; b++) {
+                    v |= (uint32_t)(uint8_t)rp[col] << (8 * b);
+                    next();
+                }
+                w[k] = v;
+            }
+        }
+    }
+    // compact element gather (the encoder's: the unrolled form above costs it registers and scheduling freedom even
+    // where no tile needs it -- C4's encode 4.2 -> 5.0 ms)
     __device__ inline void load_gather(const T *base, int64_t row_stride, int width, int64_t row, int col,
                                        int nvalid) {
 #pragma unroll
@@ -1416,12 +1569,14 @@ template <int DT, int N> struct ChunkN {
         for (int k = 0; k < kWords; k++) w[k] = p[k];
     }
     // vec = the row segments' alignment class (EncodeParams::vec_ok): 16, 8 or 4 bytes, 0 = element gather
+    template <bool UNROLLED_GATHER = false>
     __device__ inline void load(const T *base, int64_t row_stride, int width, int64_t row, int col, int vec,
                                 int nvalid) {
         const T *p = base + row * row_stride + col;
         if (vec == 16) load_vec(p);
         else if (vec == 8) load_vec8(p);
         else if (vec == 4) load_vec4(p);
+        else if constexpr (UNROLLED_GATHER) load_gather_unrolled(base, row_stride, width, row, col, nvalid);
         else load_gather(base, row_stride, width, row, col, nvalid);
     }
 };
@@ -1627,7 +1782,7 @@ __device__ inline void ana_autoc(const typename Elem<DT>::T *base, const EncodeP
     for (int c = 0; c < kMaxBlock / kAnaChunk; c++) {
         const int i0 = c * kAnaChunk;
         Ch ch;
-        ch.load(base, P.row_stride, g.w, crow, ccol, vec, kAnaChunk);
+        ch.template load<true>(base, P.row_stride, g.w, crow, ccol, vec, kAnaChunk);
         ccol += kAnaChunk;
         while (ccol >= g.w) {
             ccol -= g.w;
@@ -3126,8 +3281,8 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                                    st));
             FRS_HIP(ctx->slots.ensure((size_t)npartial * P.slot_words * 4));
             const int64_t *dpl = ctx->plist.as<int64_t>();
-            k_analyze<DT, false><<<(unsigned)((npartial + 127) / 128), 128, 0, st>>>(
-                raster, P, dtiles, dnorms, ctx->window.as<float>(), dana, dpl, npartial);
+            k_analyze_partial<DT><<<(unsigned)npartial, kPartThreads, 0, st>>>(raster, P, dtiles, dnorms,
+                                                                             ctx->window.as<float>(), dana, dpl);
             k_encode_frames<DT><<<(unsigned)npartial, kEncThreads, 0, st>>>(raster, P, dtiles, dnorms, dana,
                                                                            ctx->slots.as<uint32_t>(), dpbytes,
                                                                            err_flag, dpl);
