@@ -1424,9 +1424,13 @@ __device__ inline void norm_chunk(const Chunk64<DT> &ch, const TileNorm &tn, con
         }
         break;
     }
-    default:
+    default:  // kNormSlow: the exact IEEE division (norm_fast's last case, without its per-element mode switch)
 #pragma unroll
-        for (int j = 0; j < 64; j++) emit(j, norm_fast<DT>(ch.get(j), tn, lut));
+        for (int j = 0; j < 64; j++) {
+            using T = typename Elem<DT>::T;
+            const T dd = (T)((int64_t)ch.get(j) - tn.imin);
+            emit(j, (int32_t)(int16_t)cast_f64_i32_x86(((2.0 * (double)dd) / tn.den - 1.0) * 32767.0));
+        }
         break;
     }
 }
