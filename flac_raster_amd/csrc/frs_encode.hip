@@ -65,10 +65,12 @@ template <int DT> struct Normalizer {
     using T = typename Elem<DT>::T;
     T mn;
     double den;
+    double rinv;  // 1 / den for the fast exact division (tiles in kNormLut / kNormFastDiv mode)
     double scale;
     int has_range;
     int bps16;
     int spatial;
+    int fastdiv;
     __device__ inline int32_t operator()(T x) const {
         if (spatial) return spatial_norm<DT>(x);
         if constexpr (DT == FRS_DT_F32) {
@@ -79,7 +81,14 @@ template <int DT> struct Normalizer {
         } else {
             if (!has_range) return 0;
             T d = (T)((int64_t)x - (int64_t)mn);
-            double v = (2.0 * (double)d) / den - 1.0;
+            double v;
+            if (fastdiv) {  // RN(2d / den) by reciprocal + two FMAs: exhaustively exact for d <= den <= 65535
+                const double a = 2.0 * (double)d;
+                const double q0 = a * rinv;
+                v = fma(fma(-q0, den, a), rinv, q0) - 1.0;
+            } else {
+                v = (2.0 * (double)d) / den - 1.0;
+            }
             v = v * scale;
             int32_t c = cast_f64_i32_x86(v);
             return bps16 ? (int32_t)(int16_t)c : c;
@@ -94,6 +103,8 @@ template <int DT> __device__ inline Normalizer<DT> make_norm(const TileNorm &tn,
     if constexpr (!Elem<DT>::is_float) nz.mn = (T)tn.imin;
     else nz.mn = (T)0;
     nz.den = tn.den;
+    nz.rinv = tn.rinv;
+    nz.fastdiv = tn.mode == kNormLut || tn.mode == kNormFastDiv;
     nz.scale = scale_bits == 16 ? 32767.0 : 8388607.0;
     nz.has_range = tn.has_range;
     nz.bps16 = scale_bits == 16;
@@ -1263,29 +1274,76 @@ __device__ inline uint32_t xpow8(uint64_t m) {  // x^(8m) mod P
     return r;
 }
 
-__global__ void __launch_bounds__(256) k_compact(const uint32_t *slots, int slot_words, const int64_t *frame_bytes,
-                                                const int64_t *frame_off, int64_t nframes, uint8_t *arena) {
-    const int64_t f = blockIdx.x;
-    if (f >= nframes) return;
-    const uint8_t *src = reinterpret_cast<const uint8_t *>(slots + (size_t)f * slot_words);
-    const int64_t S = frame_bytes[f];
-    const int64_t L = S - 2;  // CRC covers everything before the footer
-    const int64_t D = frame_off[f];
-    // CRC-16: chunked, each chunk's CRC shifted to the end of the frame, XOR-combined (linear, init 0)
-    const int64_t ch = (L + 255) / 256;
-    const int64_t b0 = min(L, (int64_t)threadIdx.x * ch), b1 = min(L, b0 + ch);
+constexpr int kFrameWordsV3 = 2176;  // 69632 bits >= worst exact frame (DESIGN.md: estimate < verbatim)
+constexpr int kXpowBytes = kFrameWordsV3 * 4 + 64;  // multiple of 64 (LDS split tables)
+__constant__ uint16_t c_crc16x8[8][256];           // T_k[v] = CRC-16 of byte v followed by k zero bytes
+__device__ uint16_t g_xpow_bytes[kXpowBytes];      // x^(8m) mod P for m bytes
+
+// CRC-16 (init 0) of bytes [0, L) of a 4-byte aligned frame image, by one 256-thread work-group: thread t folds a
+// contiguous word range with slice-by-4 tables in LDS (T), shifts it to the end of the frame by x^(8m) (one
+// multiply from the byte-power table; the square-and-multiply loop only past it) and the ranges are XOR-combined.
+__device__ inline uint32_t wg_crc16(const uint8_t *src, int64_t L, const uint16_t (*T)[256], uint32_t *wc) {
+    const uint32_t *sw = reinterpret_cast<const uint32_t *>(src);
+    const int64_t nw = L >> 2;
+    const int64_t ch = (nw + 255) / 256;
+    const int64_t w0 = min(nw, (int64_t)threadIdx.x * ch), w1 = min(nw, w0 + ch);
     uint32_t c = 0;
-    for (int64_t i = b0; i < b1; i++) c = ((c << 8) & 0xFFFFu) ^ c_crc16[((c >> 8) ^ src[i]) & 0xFF];
-    if (b1 > b0 && b1 < L) c = gf_mulmod(c, xpow8((uint64_t)(L - b1)));
+    for (int64_t i = w0; i < w1; i++) {
+        const uint32_t v = sw[i];  // bytes b0..b3 = v & 0xFF .. v >> 24 (stream order)
+        c = (uint32_t)T[3][((c >> 8) ^ v) & 0xFF] ^ T[2][((c & 0xFF) ^ (v >> 8)) & 0xFF] ^ T[1][(v >> 16) & 0xFF] ^
+            T[0][v >> 24];
+    }
+    int64_t end = w1 << 2;
+    const bool last = (nw == 0) ? threadIdx.x == 0 : (w1 == nw && w1 > w0);
+    if (last) {  // the L & 3 tail bytes
+        for (int64_t i = nw << 2; i < L; i++) c = ((c << 8) & 0xFFFFu) ^ T[0][((c >> 8) ^ src[i]) & 0xFF];
+        end = L;
+    }
+    const int64_t m = L - end;
+    if (c && m > 0) c = gf_mulmod(c, m < kXpowBytes ? (uint32_t)g_xpow_bytes[m] : xpow8((uint64_t)m));
     for (int o = 32; o > 0; o >>= 1) c ^= __shfl_xor(c, o);
-    __shared__ uint32_t wc[4];
     if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
     __syncthreads();
-    const uint32_t crc = wc[0] ^ wc[1] ^ wc[2] ^ wc[3];
-    for (int64_t i = threadIdx.x; i < L; i += 256) arena[D + i] = src[i];
+    return wc[0] ^ wc[1] ^ wc[2] ^ wc[3];
+}
+
+__device__ inline void wg_load_crc_tables(uint16_t (*T)[256]) {
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) (&T[0][0])[i] = (&c_crc16x8[0][0])[i];
+    __syncthreads();
+}
+
+// Generic path: frame f's bytes move from its slot to the arena at frame_off[f] with the CRC-16 footer appended.
+// The copy writes aligned 4-byte words assembled by v_alignbyte (byte stores only for the partial words at either
+// end, which neighbouring frames share).
+__global__ void __launch_bounds__(256) k_compact(const uint32_t *slots, int slot_words, const int64_t *frame_bytes,
+                                                const int64_t *frame_off, int64_t nframes, uint8_t *arena) {
+    __shared__ uint16_t T[4][256];
+    __shared__ uint32_t wc[4];
+    const int64_t f = blockIdx.x;
+    if (f >= nframes) return;
+    wg_load_crc_tables(T);
+    const uint32_t *sw = slots + (size_t)f * slot_words;
+    const uint8_t *src = reinterpret_cast<const uint8_t *>(sw);
+    const int64_t S = frame_bytes[f];
+    const int64_t L = S - 2;  // CRC covers everything before the footer
+    uint8_t *dst = arena + frame_off[f];
+    const int h = (int)((4 - (reinterpret_cast<uintptr_t>(dst) & 3)) & 3);  // bytes before dst's first aligned word
+    const int64_t hb = min((int64_t)h, L);
+    if ((int64_t)threadIdx.x < hb) dst[threadIdx.x] = src[threadIdx.x];
+    const int64_t nbw = (L - hb) >> 2;  // whole aligned destination words
+    uint32_t *dw = reinterpret_cast<uint32_t *>(dst + hb);
+    const int sh = (int)(hb & 3);
+    const int64_t swords = slot_words;
+    for (int64_t k = threadIdx.x; k < nbw; k += 256) {
+        const int64_t sbyte = hb + 4 * k, si = sbyte >> 2;
+        const uint32_t lo = sw[si], hi = (sh && si + 1 < swords) ? sw[si + 1] : 0u;
+        dw[k] = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)sh);
+    }
+    for (int64_t i = hb + 4 * nbw + threadIdx.x; i < L; i += 256) dst[i] = src[i];
+    const uint32_t crc = wg_crc16(src, L, T, wc);
     if (threadIdx.x == 0) {
-        arena[D + L] = (uint8_t)(crc >> 8);
-        arena[D + L + 1] = (uint8_t)crc;
+        dst[L] = (uint8_t)(crc >> 8);
+        dst[L + 1] = (uint8_t)crc;
     }
 }
 
@@ -1293,21 +1351,15 @@ __global__ void __launch_bounds__(256) k_compact(const uint32_t *slots, int slot
 // [0, S - 2) -> [S - 2, S)), so k_encode_v3 copies finished frames.
 __global__ void __launch_bounds__(256) k_seal_partial(uint32_t *slots, int slot_words, const int64_t *frame_bytes,
                                                      int64_t nlist) {
+    __shared__ uint16_t T[4][256];
+    __shared__ uint32_t wc[4];
     const int64_t si = blockIdx.x;
     if (si >= nlist) return;
+    wg_load_crc_tables(T);
     uint8_t *src = reinterpret_cast<uint8_t *>(slots + (size_t)si * slot_words);
     const int64_t L = frame_bytes[si] - 2;
-    const int64_t ch = (L + 255) / 256;
-    const int64_t b0 = min(L, (int64_t)threadIdx.x * ch), b1 = min(L, b0 + ch);
-    uint32_t c = 0;
-    for (int64_t i = b0; i < b1; i++) c = ((c << 8) & 0xFFFFu) ^ c_crc16[((c >> 8) ^ src[i]) & 0xFF];
-    if (b1 > b0 && b1 < L) c = gf_mulmod(c, xpow8((uint64_t)(L - b1)));
-    for (int o = 32; o > 0; o >>= 1) c ^= __shfl_xor(c, o);
-    __shared__ uint32_t wc[4];
-    if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
-    __syncthreads();
+    const uint32_t crc = wg_crc16(src, L, T, wc);
     if (threadIdx.x == 0) {
-        const uint32_t crc = wc[0] ^ wc[1] ^ wc[2] ^ wc[3];
         src[L] = (uint8_t)(crc >> 8);
         src[L + 1] = (uint8_t)crc;
     }
@@ -2163,10 +2215,6 @@ constexpr uint64_t kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62, kValMask = (1u
 // per-sample validity predicates exist: only lane 0's first `order` (<= 8) samples are masked, by
 // selects.  LPC residuals stay in registers between the partition-sum, code-length and packing passes;
 // the fixed candidate's partition sums fall out of the fixed-predictor totals pass.
-constexpr int kFrameWordsV3 = 2176;  // 69632 bits >= worst exact frame (DESIGN.md: estimate < verbatim)
-constexpr int kXpowBytes = kFrameWordsV3 * 4 + 64;  // multiple of 64 (LDS split tables)
-__constant__ uint16_t c_crc16x8[8][256];           // T_k[v] = CRC-16 of byte v followed by k zero bytes
-__device__ uint16_t g_xpow_bytes[kXpowBytes];      // x^(8m) mod P for m bytes
 
 constexpr int kXpowHi = (kXpowBytes + 63) / 64;
 struct EncV3Shared {
