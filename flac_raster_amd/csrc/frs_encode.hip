@@ -874,8 +874,12 @@ __device__ inline void put_bits(uint32_t *buf, uint64_t pos, uint32_t val, int n
 
 __device__ inline uint32_t mask_bits(int64_t v, int n) { return n >= 32 ? (uint32_t)v : (uint32_t)v & ((1u << n) - 1u); }
 
+// LDS index of sample i in EncShared::xs: one pad word per 16 samples, so the 256 threads' contiguous 16-sample
+// chunks start in distinct banks (unpadded, thread t's chunk starts at bank 16 t mod 32: 16-way conflicts)
+__device__ inline int xsi(int i) { return i + (i >> 4); }
+
 struct EncShared {
-    int32_t xs[kMaxBlock];
+    int32_t xs[kMaxBlock + kMaxBlock / 16];
     uint32_t bits[kBitWords];
     uint64_t psum[2][32];
     uint32_t scan[kEncThreads];
@@ -994,7 +998,7 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
                 const int64_t p = s0 + i;
                 const int64_t r = p / g.w;
                 const int cc = (int)(p - r * g.w);
-                S.xs[i] = nz(base[r * P.row_stride + cc]) >> w;
+                S.xs[xsi(i)] = nz(base[r * P.row_stride + cc]) >> w;
             }
         }
         if (tid < 64) {
@@ -1029,19 +1033,19 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
             for (int i = max(i_beg, o); i < i_end; i++) {
                 int64_t r;
                 if (cand == 0) {
-                    const int64_t x = S.xs[i];
+                    const int64_t x = S.xs[xsi(i)];
                     switch (o) {
                     case 0: r = x; break;
-                    case 1: r = x - S.xs[i - 1]; break;
-                    case 2: r = x - 2 * (int64_t)S.xs[i - 1] + S.xs[i - 2]; break;
-                    case 3: r = x - 3 * (int64_t)S.xs[i - 1] + 3 * (int64_t)S.xs[i - 2] - S.xs[i - 3]; break;
-                    default: r = x - 4 * (int64_t)S.xs[i - 1] + 6 * (int64_t)S.xs[i - 2] - 4 * (int64_t)S.xs[i - 3] + S.xs[i - 4]; break;
+                    case 1: r = x - S.xs[xsi(i - 1)]; break;
+                    case 2: r = x - 2 * (int64_t)S.xs[xsi(i - 1)] + S.xs[xsi(i - 2)]; break;
+                    case 3: r = x - 3 * (int64_t)S.xs[xsi(i - 1)] + 3 * (int64_t)S.xs[xsi(i - 2)] - S.xs[xsi(i - 3)]; break;
+                    default: r = x - 4 * (int64_t)S.xs[xsi(i - 1)] + 6 * (int64_t)S.xs[xsi(i - 2)] - 4 * (int64_t)S.xs[xsi(i - 3)] + S.xs[xsi(i - 4)]; break;
                     }
                     r = (int32_t)r;  // libFLAC stores fixed residuals as int32
                 } else {
                     int64_t s = 0;
-                    for (int j = 0; j < o; j++) s += (int64_t)A.q[j] * S.xs[i - 1 - j];
-                    r = (int64_t)S.xs[i] - (s >> A.lpc_shift);
+                    for (int j = 0; j < o; j++) s += (int64_t)A.q[j] * S.xs[xsi(i - 1 - j)];
+                    r = (int64_t)S.xs[xsi(i)] - (s >> A.lpc_shift);
                     if (r <= INT32_MIN || r > INT32_MAX) S.lpc_bad = 1;
                 }
                 const int p = i / ps;
@@ -1111,16 +1115,16 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
         }
         uint64_t sub_end;
         if (type == 0) {
-            if (tid == 0) put_bits(S.bits, pos, mask_bits(S.xs[0], sbps), sbps);
+            if (tid == 0) put_bits(S.bits, pos, mask_bits(S.xs[xsi(0)], sbps), sbps);
             sub_end = pos + (uint64_t)sbps;
         } else if (type == 1) {
             for (int i = tid; i < n; i += kEncThreads)
-                put_bits(S.bits, pos + (uint64_t)i * sbps, mask_bits(S.xs[i], sbps), sbps);
+                put_bits(S.bits, pos + (uint64_t)i * sbps, mask_bits(S.xs[xsi(i)], sbps), sbps);
             sub_end = pos + (uint64_t)n * sbps;
         } else {
             const int o = type == 2 ? A.fixed_order : A.lpc_order;
             const RiceChoice &rc = S.rc[type == 2 ? 0 : 1];
-            for (int i = tid; i < o; i++) put_bits(S.bits, pos + (uint64_t)i * sbps, mask_bits(S.xs[i], sbps), sbps);
+            for (int i = tid; i < o; i++) put_bits(S.bits, pos + (uint64_t)i * sbps, mask_bits(S.xs[xsi(i)], sbps), sbps);
             pos += (uint64_t)o * sbps;
             if (type == 3) {
                 if (tid == 0) {
@@ -1145,18 +1149,18 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
             for (int i = max(i_beg, o); i < i_end; i++) {
                 int64_t r;
                 if (type == 2) {
-                    const int64_t x = S.xs[i];
+                    const int64_t x = S.xs[xsi(i)];
                     switch (o) {
                     case 0: r = x; break;
-                    case 1: r = x - S.xs[i - 1]; break;
-                    case 2: r = x - 2 * (int64_t)S.xs[i - 1] + S.xs[i - 2]; break;
-                    case 3: r = x - 3 * (int64_t)S.xs[i - 1] + 3 * (int64_t)S.xs[i - 2] - S.xs[i - 3]; break;
-                    default: r = x - 4 * (int64_t)S.xs[i - 1] + 6 * (int64_t)S.xs[i - 2] - 4 * (int64_t)S.xs[i - 3] + S.xs[i - 4]; break;
+                    case 1: r = x - S.xs[xsi(i - 1)]; break;
+                    case 2: r = x - 2 * (int64_t)S.xs[xsi(i - 1)] + S.xs[xsi(i - 2)]; break;
+                    case 3: r = x - 3 * (int64_t)S.xs[xsi(i - 1)] + 3 * (int64_t)S.xs[xsi(i - 2)] - S.xs[xsi(i - 3)]; break;
+                    default: r = x - 4 * (int64_t)S.xs[xsi(i - 1)] + 6 * (int64_t)S.xs[xsi(i - 2)] - 4 * (int64_t)S.xs[xsi(i - 3)] + S.xs[xsi(i - 4)]; break;
                     }
                 } else {
                     int64_t s = 0;
-                    for (int j = 0; j < o; j++) s += (int64_t)A.q[j] * S.xs[i - 1 - j];
-                    r = (int64_t)S.xs[i] - (s >> A.lpc_shift);
+                    for (int j = 0; j < o; j++) s += (int64_t)A.q[j] * S.xs[xsi(i - 1 - j)];
+                    r = (int64_t)S.xs[xsi(i)] - (s >> A.lpc_shift);
                 }
                 const int32_t r32 = (int32_t)r;
                 const uint32_t u = ((uint32_t)r32 << 1) ^ (uint32_t)(r32 >> 31);
@@ -1192,18 +1196,18 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
             for (int i = max(i_beg, o); i < i_end; i++) {
                 int64_t r;
                 if (type == 2) {
-                    const int64_t x = S.xs[i];
+                    const int64_t x = S.xs[xsi(i)];
                     switch (o) {
                     case 0: r = x; break;
-                    case 1: r = x - S.xs[i - 1]; break;
-                    case 2: r = x - 2 * (int64_t)S.xs[i - 1] + S.xs[i - 2]; break;
-                    case 3: r = x - 3 * (int64_t)S.xs[i - 1] + 3 * (int64_t)S.xs[i - 2] - S.xs[i - 3]; break;
-                    default: r = x - 4 * (int64_t)S.xs[i - 1] + 6 * (int64_t)S.xs[i - 2] - 4 * (int64_t)S.xs[i - 3] + S.xs[i - 4]; break;
+                    case 1: r = x - S.xs[xsi(i - 1)]; break;
+                    case 2: r = x - 2 * (int64_t)S.xs[xsi(i - 1)] + S.xs[xsi(i - 2)]; break;
+                    case 3: r = x - 3 * (int64_t)S.xs[xsi(i - 1)] + 3 * (int64_t)S.xs[xsi(i - 2)] - S.xs[xsi(i - 3)]; break;
+                    default: r = x - 4 * (int64_t)S.xs[xsi(i - 1)] + 6 * (int64_t)S.xs[xsi(i - 2)] - 4 * (int64_t)S.xs[xsi(i - 3)] + S.xs[xsi(i - 4)]; break;
                     }
                 } else {
                     int64_t s = 0;
-                    for (int j = 0; j < o; j++) s += (int64_t)A.q[j] * S.xs[i - 1 - j];
-                    r = (int64_t)S.xs[i] - (s >> A.lpc_shift);
+                    for (int j = 0; j < o; j++) s += (int64_t)A.q[j] * S.xs[xsi(i - 1 - j)];
+                    r = (int64_t)S.xs[xsi(i)] - (s >> A.lpc_shift);
                 }
                 const int32_t r32 = (int32_t)r;
                 const uint32_t u = ((uint32_t)r32 << 1) ^ (uint32_t)(r32 >> 31);
