@@ -628,7 +628,8 @@ __global__ void __launch_bounds__(kPartThreads) k_analyze_partial(const typename
     const int64_t tile_px = (int64_t)g.h * g.w;
     const int n = (int)((tile_px - s0) < P.blocksize ? (tile_px - s0) : P.blocksize);
     const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits, P.norm_mode);
-    const T *tb = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
+    const int chn = blockIdx.y;  // channel (multi-channel jobs: grid.y = nch)
+    const T *tb = raster + (int64_t)(P.band0 + chn) * P.band_stride + g.r0 * P.row_stride + g.c0;
     if (threadIdx.x < 5) red_t[threadIdx.x] = 0;
     if (threadIdx.x == 0) red_or = red_diff = 0;
     // 1. normalise + window (samples past n are zeros, as in k_analyze)
@@ -682,7 +683,7 @@ __global__ void __launch_bounds__(kPartThreads) k_analyze_partial(const typename
 #pragma unroll
         for (int l = 0; l <= kMaxLpc; l++) acc[l] = red_acc[l];
         const uint64_t tt[5] = {red_t[0], red_t[1], red_t[2], red_t[3], red_t[4]};
-        out[f] = generic_decide<false>(acc, tt, red_or, red_diff, n, P);
+        out[f * P.nch + chn] = generic_decide<false>(acc, tt, red_or, red_diff, n, P);
     }
 }
 
@@ -1963,9 +1964,9 @@ __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *
     const int wv = blockIdx.x * 4 + wave;
     if (wv >= nwaves) return;
     const int2 wt = wtab[wv];  // (tile, first frame of the tile handled by this wave)
-    const int t = wt.x;
+    const int t = wt.x, k0w = wt.y & 0xFFFFFF, chn = wt.y >> 24;  // (tile, first frame | channel << 24)
     const TileGeom g = tiles[t];
-    const typename Elem<DT>::T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
+    const typename Elem<DT>::T *base = raster + (int64_t)(P.band0 + chn) * P.band_stride + g.r0 * P.row_stride + g.c0;
     int16_t *glut = luts + (int64_t)t * kLutCap;
     TileNorm tn;
     if constexpr (STATS) {
@@ -1982,8 +1983,8 @@ __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *
     if (lean == SLOW) return;
     const int nfull = g.nframes - (g.partial ? 1 : 0);  // a partial last frame is analysed by k_analyze
     if (nfull == 0) return;                              // (wave-uniform) only its stats were needed here
-    const bool live = wt.y + lane < nfull;
-    const int64_t fk = live ? wt.y + lane : nfull - 1;  // dead lanes re-read the tile's last full frame
+    const bool live = k0w + lane < nfull;
+    const int64_t fk = live ? k0w + lane : nfull - 1;  // dead lanes re-read the tile's last full frame
     const int64_t f = g.frame_base + fk;
     const int64_t s0 = fk * P.blocksize;
     const int64_t tile_px = (int64_t)g.h * g.w;
@@ -2020,7 +2021,7 @@ __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *
             ana_autoc<DT, kAnaKindGeneric, kChunk>(base, P, g, s0, tn, nullptr, glut, window, vec, acc, or_acc, ft);
     }
     if (!live) return;
-    out[f] = analysis_finish(acc, or_acc, n, P, ft);
+    out[f * P.nch + chn] = analysis_finish(acc, or_acc, n, P, ft);
 }
 
 // ---- wave helpers (64 lanes)
@@ -2477,18 +2478,22 @@ __device__ inline uint32_t fixed_lane_sum(const uint32_t *E, bool l0) {
     return s;
 }
 
-template <int DT>
+// SUB = true (multi-channel streams, >= 3 independent channels): the wave codes ONE subframe (channel chn of frame f)
+// from bit 0 of its buffer -- no frame header, no look-back, no CRC -- and stores its words to sub_slots[f * nch +
+// chn] with its bit length in sub_bits; k_mc_assemble joins a frame's subframes behind the frame header.
+template <int DT, bool SUB = false>
 __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const EncodeParams &P,
                                        const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
                                        const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap, int64_t *frame_off,
                                        uint64_t *status, int *err, EncV3Shared &S, int want, int64_t f, int lane,
                                        const int32_t *ftile, PendingFrame &prev, const uint4 *hdr_tab, int hdr_n,
-                                       const uint32_t *pslots, const int64_t *pbytes) {
+                                       const uint32_t *pslots, const int64_t *pbytes, int chn = 0,
+                                       uint32_t *sub_slots = nullptr, int32_t *sub_bits = nullptr) {
     using T = typename Elem<DT>::T;
     uint32_t *fbuf = S.bits[threadIdx.x >> 6];
     const int t = ftile[f];
     const TileGeom g = tiles[t];
-    if (g.partial && f - g.frame_base == g.nframes - 1) {
+    if (!SUB && g.partial && f - g.frame_base == g.nframes - 1) {
         // (wave-uniform) the tile's partial last frame: already coded and sealed by the generic kernels, so it
         // only joins the look-back chain -- publish its size, finish the previous frame, and stage its bytes in
         // the bit buffer for resolve_and_store like a frame coded here
@@ -2522,10 +2527,11 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     const int64_t fk = f - g.frame_base;
     const int64_t s0 = fk * kMaxBlock;
     constexpr int n = kMaxBlock;
-    const SubAnalysis A = ana[f];
+    const int64_t sub = SUB ? f * P.nch + chn : f;
+    const SubAnalysis A = ana[sub];
     const int w = A.wasted;
     const int sbps = 16 - w;
-    const T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
+    const T *base = raster + (int64_t)(P.band0 + chn) * P.band_stride + g.r0 * P.row_stride + g.c0;
 
     // ---- this lane's 64 samples, normalised and shifted, packed as int16 pairs E[4 + m] = (x[2m], x[2m+1]);
     //      E[0..3] = the previous lane's last 8 samples (zeros on lane 0)
@@ -2763,10 +2769,10 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     int src, srx;
     sample_rate_code(P.sample_rate, src, srx);
     // frame header bytes: host table by frame number within the stream (words MSB-first; .w = length)
-    const bool tab = fk < hdr_n;
+    const bool tab = !SUB && fk < hdr_n;
     uint4 hrow = make_uint4(0, 0, 0, 0);
     if (tab) hrow = hdr_tab[fk];
-    const uint32_t hb = tab ? (hrow.w & 0xFFu) : frame_header_bytes((uint32_t)fk, srx);
+    const uint32_t hb = SUB ? 0u : tab ? (hrow.w & 0xFFu) : frame_header_bytes((uint32_t)fk, srx);
     const uint32_t hdr_bits = hb << 3;
     const uint32_t pos0 = hdr_bits + 8 + (uint32_t)w;  // after the subframe header
     uint32_t pos = pos0;
@@ -2832,13 +2838,14 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     const uint32_t body = (end_bits + 7) >> 3;  // bytes before the CRC-16 footer
     const uint64_t fbytes = ok ? (uint64_t)body + 2 : 0;
     const FbMap M = fb_map(((end_bits + 23) >> 5) + 2);  // words written: body, CRC-16 (byte aligned), one spare
-    if (l0) {  // publish our aggregate
+    if (!SUB && l0) {  // publish our aggregate
         const uint64_t v = (f == 0 ? kFlagIncl : kFlagAgg) | fbytes;
         __hip_atomic_store(&status[f], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // ---- the previous frame of this wave: its predecessors have had a whole phase A to publish, so the
     //      look-back rarely waits; store it and free the bit buffer
-    if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
+    if constexpr (!SUB)
+        if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
     reg_fence(E);
     // ---- phase B: every bit of this frame into the (zeroed) buffer, then the CRC-16
     if (l0 && tab) {
@@ -2856,7 +2863,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
             hbits += 8;
         };
         const int sr = P.sample_rate;
-        if (!tab) {
+        if (!SUB && !tab) {
         put8(0xFF);
         put8(0xF8);
         put8((uint32_t)((12 << 4) | src));  // block size code 12 = 4096
@@ -2896,7 +2903,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         w01 = (i >> 1) == 2 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 2], 0) : w01;
         w01 = (i >> 1) == 3 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 3], 0) : w01;
         const uint32_t xi = (i & 1) ? (w01 >> 16) : (w01 & 0xFFFFu);
-        const int32_t qi = ana[f].q[i];  // (a lane-indexed load: a select chain over A.q costs registers)
+        const int32_t qi = ana[sub].q[i];  // (a lane-indexed load: a select chain over A.q costs registers)
         const bool warm = lane < 8 && i < o, coef = type == 3 && lane >= 8 && lane < 16 && i < o;
         if (warm)
             lds_put_bits2(fbuf, M, pos0 + (uint32_t)i * sbps, xi & ((1u << sbps) - 1u), sbps);
@@ -2936,7 +2943,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS atomics have landed
     __builtin_amdgcn_wave_barrier();
     uint32_t crc = 0;
-    if (ok) {
+    if (!SUB && ok) {
         // slice-by-4 over 32-bit words, one contiguous word range per lane, combined with x^(8m) factors
         const uint32_t nfw = body >> 2, tail = body & 3;
         // lane L takes column L of the buffer (words L C .. L C + C - 1), so at each step the lanes read one row:
@@ -2972,20 +2979,38 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         crc = dpp_wave_xor_u32(gf_mulmod(gf_mulmod(c, S.xlo[m & 63]), S.xhi[m >> 6]));
         if (l0) lds_put_bits2(fbuf, M, body << 3, crc, 16);
     }
+    if constexpr (SUB) {
+        // the subframe's words (bits past end_bits are zeros) to its slot, then re-zero the buffer
+        if (ok) {
+            uint32_t *dst = sub_slots + (size_t)sub * kFrameWordsV3;
+            const uint32_t nw = (end_bits + 31) >> 5;
+            for (uint32_t wi = (uint32_t)lane; wi < nw; wi += 64) dst[wi] = fbuf[M(wi)];
+            for (uint32_t i = 0; i < M.c; i++) fbuf[(i << 6) | (uint32_t)lane] = 0;
+        } else {
+            for (uint32_t i = (uint32_t)lane; i < (uint32_t)kFrameWordsV3; i += 64) fbuf[i] = 0;
+        }
+        if (l0) sub_bits[sub] = ok ? (int32_t)end_bits : -1;
+        (void)fbytes;
+        (void)crc;
+        return;
+    }
     prev.f = f;
     prev.fbytes = fbytes;
     prev.ok = ok;
     prev.map = M;
 }
 
-template <int DT>
+// SUB = true: the units are the subframes (frame, channel) of a multi-channel job (encode_frame_v3<DT, true>); the
+// tile's partial last frame is coded whole by the generic kernels and skipped here.
+template <int DT, bool SUB = false>
 __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *raster, EncodeParams P,
                                                   const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
                                                   const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap,
                                                   int64_t *frame_off, uint64_t *status, int *ticket_ctr, int *err,
                                                   const int32_t *__restrict__ ftile, const uint4 *__restrict__ hdr_tab,
                                                   int hdr_n, const uint32_t *__restrict__ pslots,
-                                                  const int64_t *__restrict__ pbytes) {
+                                                  const int64_t *__restrict__ pbytes, uint32_t *sub_slots = nullptr,
+                                                  int32_t *sub_bits = nullptr) {
     __shared__ EncV3Shared S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int i = threadIdx.x; i < 2048; i += blockDim.x) (&S.crc8x[0][0])[i] = (&c_crc16x8[0][0])[i];
@@ -2998,14 +3023,15 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
     uint32_t *fbuf = S.bits[wave];
     while (true) {
         __syncthreads();  // previous ticket's readers of S.ticket / S.lut are done
+        const int64_t nunits = SUB ? P.nframes * P.nch : P.nframes;
         if (threadIdx.x == 0) {
             const int tk = atomicAdd(ticket_ctr, 1);
             S.ticket = tk;
-            S.want = ((int64_t)tk * 4 < P.nframes) ? ftile[(int64_t)tk * 4] : -1;
+            S.want = ((int64_t)tk * 4 < nunits) ? ftile[SUB ? (int64_t)tk * 4 / P.nch : (int64_t)tk * 4] : -1;
         }
         __syncthreads();
         const int64_t fbase = (int64_t)S.ticket * 4;
-        if (fbase >= P.nframes) break;
+        if (fbase >= nunits) break;
         const int want = S.want;
         if (want != S.lut_tile) {  // WG-uniform
             const TileNorm tw = norms[want];
@@ -3017,12 +3043,167 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
             __syncthreads();
             if (threadIdx.x == 0) S.lut_tile = want;
         }
-        const int64_t f = fbase + wave;
-        if (f < P.nframes)
-            encode_frame_v3<DT>(raster, P, tiles, norms, luts, ana, arena, arena_cap, frame_off, status, err, S, want, f,
-                                lane, ftile, prev, hdr_tab, hdr_n, pslots, pbytes);
+        if constexpr (SUB) {
+            const int64_t v = fbase + wave;
+            if (v < nunits) {
+                const int64_t f = v / P.nch;
+                const int chn = (int)(v - f * P.nch);
+                const TileGeom g = tiles[ftile[f]];
+                if (!(g.partial && f - g.frame_base == g.nframes - 1))
+                    encode_frame_v3<DT, true>(raster, P, tiles, norms, luts, ana, arena, arena_cap, frame_off, status,
+                                              err, S, want, f, lane, ftile, prev, hdr_tab, hdr_n, pslots, pbytes, chn,
+                                              sub_slots, sub_bits);
+            }
+        } else {
+            const int64_t f = fbase + wave;
+            if (f < P.nframes)
+                encode_frame_v3<DT>(raster, P, tiles, norms, luts, ana, arena, arena_cap, frame_off, status, err, S,
+                                    want, f, lane, ftile, prev, hdr_tab, hdr_n, pslots, pbytes);
+        }
     }
-    if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
+    if constexpr (!SUB)
+        if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
+}
+
+// ---------------------------------------------------------------- multi-channel streams (>= 3 channels, 16-bit)
+// libFLAC codes the channels of a >= 3-channel frame independently (no stereo decorrelation), so the subframes are
+// the fast encoder's units (k_encode_v3<DT, true>); a frame is then its header, the subframes' bit strings back to
+// back, zero padding to a byte and the CRC-16.  k_mc_frame_bytes sizes the frames, k_scan_sizes places them and
+// k_mc_assemble writes them (the tile's partial last frame comes sealed from the generic kernels).
+
+// frame header of a full 4096-sample frame (RFC 9639 9.1, as k_encode_frames writes it); returns its bytes
+__device__ inline int mc_frame_header(uint8_t *h, uint32_t v, int nch, int sr) {
+    int src, srx;
+    sample_rate_code(sr, src, srx);
+    int hb = 0;
+    h[hb++] = 0xFF;
+    h[hb++] = 0xF8;
+    h[hb++] = (uint8_t)((12 << 4) | src);
+    h[hb++] = (uint8_t)(((nch - 1) << 4) | (4 << 1));
+    if (v < 0x80) h[hb++] = (uint8_t)v;
+    else if (v < 0x800) { h[hb++] = (uint8_t)(0xC0 | (v >> 6)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+    else if (v < 0x10000) { h[hb++] = (uint8_t)(0xE0 | (v >> 12)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+    else if (v < 0x200000) { h[hb++] = (uint8_t)(0xF0 | (v >> 18)); h[hb++] = (uint8_t)(0x80 | ((v >> 12) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+    else if (v < 0x4000000) { h[hb++] = (uint8_t)(0xF8 | (v >> 24)); h[hb++] = (uint8_t)(0x80 | ((v >> 18) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 12) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+    else { h[hb++] = (uint8_t)(0xFC | (v >> 30)); h[hb++] = (uint8_t)(0x80 | ((v >> 24) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 18) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 12) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+    if (srx == 12) h[hb++] = (uint8_t)(sr / 1000);
+    else if (srx == 13) { h[hb++] = (uint8_t)(sr >> 8); h[hb++] = (uint8_t)sr; }
+    else if (srx == 14) { h[hb++] = (uint8_t)((sr / 10) >> 8); h[hb++] = (uint8_t)(sr / 10); }
+    uint8_t c = 0;
+    for (int i = 0; i < hb; i++) c = c_crc8[c ^ h[i]];
+    h[hb++] = c;
+    return hb;
+}
+
+__global__ void k_mc_frame_bytes(const EncodeParams P, const TileGeom *tiles, const int32_t *ftile,
+                                 const int32_t *sub_bits, const int64_t *pbytes, int64_t *frame_bytes, int *err) {
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= P.nframes) return;
+    const TileGeom g = tiles[ftile[f]];
+    const int64_t fk = f - g.frame_base;
+    if (g.partial && fk == g.nframes - 1) {
+        frame_bytes[f] = pbytes[g.partial - 1];
+        return;
+    }
+    uint8_t h[16];
+    int64_t bits = 8 * mc_frame_header(h, (uint32_t)fk, P.nch, P.sample_rate);
+    for (int c = 0; c < P.nch; c++) {
+        const int32_t b = sub_bits[f * P.nch + c];
+        if (b < 0) atomicOr(err, 2);
+        bits += b < 0 ? 0 : b;
+    }
+    frame_bytes[f] = ((bits + 7) >> 3) + 2;
+}
+
+// one work-group per frame: the frame image in LDS (big-endian bit order words), then its bytes to the arena
+__global__ void __launch_bounds__(256) k_mc_assemble(const EncodeParams P, const TileGeom *tiles, const int32_t *ftile,
+                                                    const uint32_t *sub_slots, const int32_t *sub_bits,
+                                                    const uint32_t *pslots, const int64_t *pbytes,
+                                                    const int64_t *frame_off, uint8_t *arena) {
+    extern __shared__ uint32_t W[];  // nch * kFrameWordsV3 + 16 words
+    __shared__ uint16_t T[4][256];
+    __shared__ uint32_t wc[4];
+    const int64_t f = blockIdx.x;
+    const TileGeom g = tiles[ftile[f]];
+    const int64_t fk = f - g.frame_base;
+    uint8_t *dst = arena + frame_off[f];
+    const int tid = threadIdx.x;
+    if (g.partial && fk == g.nframes - 1) {  // sealed by the generic kernels: copy
+        const int64_t si = g.partial - 1, nb = pbytes[si];
+        const uint8_t *src = reinterpret_cast<const uint8_t *>(pslots + (size_t)si * P.slot_words);
+        for (int64_t i = tid; i < nb; i += 256) dst[i] = src[i];
+        return;
+    }
+    const int nwmax = P.nch * kFrameWordsV3 + 16;
+    for (int i = tid; i < nwmax; i += 256) W[i] = 0;
+    wg_load_crc_tables(T);  // (syncs: W is zeroed)
+    uint8_t h[16];
+    const int hb = mc_frame_header(h, (uint32_t)fk, P.nch, P.sample_rate);
+    if (tid == 0)
+        for (int i = 0; i < hb; i++) W[i >> 2] |= (uint32_t)h[i] << (24 - 8 * (i & 3));
+    __syncthreads();
+    int64_t o = 8 * hb;
+    for (int c = 0; c < P.nch; c++) {
+        const int32_t nbits = sub_bits[f * P.nch + c];
+        const uint32_t *sw = sub_slots + (size_t)(f * P.nch + c) * kFrameWordsV3;
+        const int nw = (nbits + 31) >> 5, sh = (int)(o & 31);
+        const int64_t w0 = o >> 5;
+        for (int k = tid; k < nw; k += 256) {
+            const uint32_t v = sw[k];
+            atomicOr(&W[w0 + k], v >> sh);
+            if (sh) atomicOr(&W[w0 + k + 1], v << (32 - sh));
+        }
+        o += nbits;
+    }
+    __syncthreads();
+    const int64_t B = (o + 7) >> 3;  // body bytes (zero-padded)
+    // CRC-16 over bytes [0, B): words hold bytes big-endian
+    {
+        const int64_t nw = B >> 2;
+        const int64_t ch = (nw + 255) / 256;
+        const int64_t a0 = min(nw, (int64_t)tid * ch), a1 = min(nw, a0 + ch);
+        uint32_t c = 0;
+        for (int64_t i = a0; i < a1; i++) {
+            const uint32_t v = W[i];
+            c = (uint32_t)T[3][((c >> 8) ^ (v >> 24)) & 0xFF] ^ T[2][((c & 0xFF) ^ (v >> 16)) & 0xFF] ^
+                T[1][(v >> 8) & 0xFF] ^ T[0][v & 0xFF];
+        }
+        int64_t end = a1 << 2;
+        const bool last = (nw == 0) ? tid == 0 : (a1 == nw && a1 > a0);
+        if (last) {
+            for (int64_t i = nw << 2; i < B; i++) {
+                const uint32_t byte = (W[i >> 2] >> (24 - 8 * (i & 3))) & 0xFF;
+                c = ((c << 8) & 0xFFFFu) ^ T[0][((c >> 8) ^ byte) & 0xFF];
+            }
+            end = B;
+        }
+        const int64_t m = B - end;
+        if (c && m > 0) c = gf_mulmod(c, m < kXpowBytes ? (uint32_t)g_xpow_bytes[m] : xpow8((uint64_t)m));
+        for (int d = 32; d > 0; d >>= 1) c ^= __shfl_xor(c, d);
+        if ((tid & 63) == 0) wc[tid >> 6] = c;
+        __syncthreads();
+        const uint32_t crc = wc[0] ^ wc[1] ^ wc[2] ^ wc[3];
+        if (tid == 0) {
+            W[B >> 2] |= ((crc >> 8) & 0xFF) << (24 - 8 * (B & 3));
+            W[(B + 1) >> 2] |= (crc & 0xFF) << (24 - 8 * ((B + 1) & 3));
+        }
+        __syncthreads();
+    }
+    // bytes [0, B + 2) to dst: aligned 4-byte stores assembled from byte-swapped words
+    const int64_t S = B + 2;
+    const int hh = (int)((4 - (reinterpret_cast<uintptr_t>(dst) & 3)) & 3);
+    const int64_t hbytes = min((int64_t)hh, S);
+    auto byte_at = [&](int64_t i) -> uint8_t { return (uint8_t)(W[i >> 2] >> (24 - 8 * (i & 3))); };
+    if (tid < hbytes) dst[tid] = byte_at(tid);
+    const int64_t nbw = (S - hbytes) >> 2;
+    uint32_t *dw = reinterpret_cast<uint32_t *>(dst + hbytes);
+    const int sh = (int)(hbytes & 3);
+    for (int64_t k = tid; k < nbw; k += 256) {
+        const int64_t si = (hbytes + 4 * k) >> 2;
+        const uint32_t lo = __builtin_bswap32(W[si]), hi = sh ? __builtin_bswap32(W[si + 1]) : 0u;
+        dw[k] = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)sh);
+    }
+    for (int64_t i = hbytes + 4 * nbw + tid; i < S; i += 256) dst[i] = byte_at(i);
 }
 
 // results of the fast path packed for one D2H copy: tile offsets [ntiles + 1], (dmin, dmax) per tile, error flags
@@ -3207,7 +3388,7 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     FRS_HIP(ctx->tile_sizes.ensure(sizeof(int64_t) * (ntiles + 1) + 64));
     // pinned staging: tiles | wave table | packed results (the previous call has synchronised, so it is free)
     const size_t pin_tiles = 0, pin_wt = (sizeof(TileGeom) * ntiles + 255) & ~(size_t)255;
-    const size_t wt_cap = (size_t)(nframes / 64 + ntiles + 1);
+    const size_t wt_cap = (size_t)(nframes / 64 + ntiles + 1) * (size_t)std::max(1, d->nbands);
     const size_t pin_res = (pin_wt + sizeof(int2) * wt_cap + 255) & ~(size_t)255;
     const size_t res_bytes = sizeof(int64_t) * (3 * (size_t)ntiles + 2);
     const size_t pin_pl = (pin_res + res_bytes + 255) & ~(size_t)255;  // partial-frame list of the fast path
@@ -3217,9 +3398,14 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     // the fast encoder copies them into the arena in stream order
     const bool fast = allow_fast && !ctx->force_generic && P.bps == 16 && P.nch == 1 && P.norm_mode == 0 &&
                       d->blocksize == 4096 && !Elem<DT>::is_float;
+    // multi-channel streams of >= 3 channels (plain convert of a multi-band raster): libFLAC codes their channels
+    // independently, so the fast kernels code the subframes and k_mc_assemble joins them (2 channels: libFLAC's
+    // stereo decorrelation, generic kernels; <= 7 channels: the assembly's LDS frame image)
+    const bool mc = allow_fast && !ctx->force_generic && P.bps == 16 && P.nch >= 3 && P.nch <= 7 &&
+                    P.norm_mode == 0 && d->blocksize == 4096 && !Elem<DT>::is_float;
     int64_t npartial = 0;
     int64_t *hplist = ctx->pin.at<int64_t>(pin_pl);
-    if (fast)
+    if (fast || mc)
         for (TileGeom &tg : tiles)
             if (((int64_t)tg.h * tg.w) % d->blocksize != 0) {
                 hplist[npartial] = tg.frame_base + tg.nframes - 1;
@@ -3289,7 +3475,7 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         k_tile_finalize<DT><<<(ntiles + 255) / 256, 256, 0, st>>>(dnorms, ntiles, P.norm_mode, P.scale_bits);
         prof_end(ctx, "stats", ev);
     }
-    if constexpr (!Elem<DT>::is_float) if (fast) {
+    if constexpr (!Elem<DT>::is_float) if (fast || mc) {
         const int es = (int)sizeof(T);
         // alignment class of the 64-sample row segments (tiles whose width is a multiple of 64): the widest of 16,
         // 8, 4 bytes dividing the band base, the row stride and the tile width in bytes
@@ -3309,7 +3495,8 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
             int2 *wt = ctx->pin.at<int2>(pin_wt);
             int nwaves = 0;
             for (int ti = 0; ti < ntiles; ti++)
-                for (int k0 = 0; k0 < tiles[ti].nframes; k0 += 64) wt[nwaves++] = make_int2(ti, k0);
+                for (int c = 0; c < P.nch; c++)  // (tile, first frame | channel << 24)
+                    for (int k0 = 0; k0 < tiles[ti].nframes; k0 += 64) wt[nwaves++] = make_int2(ti, k0 | (c << 24));
             FRS_HIP(ctx->wave_tab.ensure(sizeof(int2) * nwaves));
             FRS_HIP(hipMemcpyAsync(ctx->wave_tab.ptr, wt, sizeof(int2) * nwaves, hipMemcpyHostToDevice, st));
             const unsigned wgrid = (unsigned)((nwaves + 3) / 4);
@@ -3337,8 +3524,8 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                                    st));
             FRS_HIP(ctx->slots.ensure((size_t)npartial * P.slot_words * 4));
             const int64_t *dpl = ctx->plist.as<int64_t>();
-            k_analyze_partial<DT><<<(unsigned)npartial, kPartThreads, 0, st>>>(raster, P, dtiles, dnorms,
-                                                                             ctx->window.as<float>(), dana, dpl);
+            k_analyze_partial<DT><<<dim3((unsigned)npartial, (unsigned)P.nch), kPartThreads, 0, st>>>(
+                raster, P, dtiles, dnorms, ctx->window.as<float>(), dana, dpl);
             k_encode_frames<DT><<<(unsigned)npartial, kEncThreads, 0, st>>>(raster, P, dtiles, dnorms, dana,
                                                                            ctx->slots.as<uint32_t>(), dpbytes,
                                                                            err_flag, dpl);
@@ -3348,6 +3535,64 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         }
         uint64_t *dstatus = ctx->status.as<uint64_t>();
         int *ticket = reinterpret_cast<int *>(dstatus + nframes);
+        if (mc) {
+            const int64_t nsub = nframes * P.nch;
+            FRS_HIP(ctx->sub_slots.ensure(sizeof(uint32_t) * (size_t)nsub * kFrameWordsV3));
+            FRS_HIP(ctx->sub_bits.ensure(sizeof(int32_t) * (size_t)nsub));
+            FRS_HIP(ctx->mc_bytes.ensure(sizeof(int64_t) * (size_t)(nframes + 1)));
+            FRS_HIP(hipMemsetAsync(ticket, 0, sizeof(int), st));
+            uint32_t *dsub = ctx->sub_slots.as<uint32_t>();
+            int32_t *dsbits = ctx->sub_bits.as<int32_t>();
+            int64_t *dmcb = ctx->mc_bytes.as<int64_t>();
+            prof_begin(ctx, "encode", &ev);
+            {
+                int nwg_max = 0;
+                FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nwg_max, k_encode_v3<DT, true>, 256, 0));
+                int64_t grid = (int64_t)std::max(1, nwg_max) * ctx->num_cus;
+                grid = std::min<int64_t>(grid, (nsub + 3) / 4);
+                k_encode_v3<DT, true><<<(unsigned)grid, 256, 0, st>>>(
+                    raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(), dana, reinterpret_cast<uint8_t *>(arena_dev),
+                    arena_cap, ctx->frame_off.as<int64_t>(), dstatus, ticket, err_flag, ctx->frame_tile.as<int32_t>(),
+                    ctx->hdr_tab.as<uint4>(), 0, ctx->slots.as<uint32_t>(), dpbytes, dsub, dsbits);
+            }
+            k_mc_frame_bytes<<<(unsigned)((nframes + 255) / 256), 256, 0, st>>>(P, dtiles, ctx->frame_tile.as<int32_t>(),
+                                                                               dsbits, dpbytes, dmcb, err_flag);
+            prof_end(ctx, "encode", ev);
+            k_scan_sizes<<<1, kScanThreads, 0, st>>>(dmcb, ctx->frame_off.as<int64_t>(), nframes);
+            int64_t total = 0;
+            int errv = 0;
+            FRS_HIP(hipMemcpyAsync(&total, ctx->frame_off.as<int64_t>() + nframes, sizeof(int64_t),
+                                   hipMemcpyDeviceToHost, st));
+            FRS_HIP(hipMemcpyAsync(&errv, err_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+            FRS_HIP(hipStreamSynchronize(st));
+            if (errv) {
+                ctx->err = "fast encode declined, flags " + std::to_string(errv);
+                return kFastDeclined;
+            }
+            if (total > arena_cap) {
+                tile_off[ntiles] = total;
+                ctx->err = "arena too small";
+                return FRS_E_NOSPACE;
+            }
+            prof_begin(ctx, "assemble", &ev);
+            k_mc_assemble<<<(unsigned)nframes, 256, sizeof(uint32_t) * (size_t)(P.nch * kFrameWordsV3 + 16), st>>>(
+                P, dtiles, ctx->frame_tile.as<int32_t>(), dsub, dsbits, ctx->slots.as<uint32_t>(), dpbytes,
+                ctx->frame_off.as<int64_t>(), reinterpret_cast<uint8_t *>(arena_dev));
+            prof_end(ctx, "assemble", ev);
+            k_gather_tile_off<<<(ntiles + 1 + 255) / 256, 256, 0, st>>>(ctx->frame_off.as<int64_t>(), dtiles, ntiles,
+                                                                       total, ctx->tile_sizes.as<int64_t>());
+            std::vector<TileNorm> hn(ntiles);
+            FRS_HIP(hipMemcpyAsync(tile_off, ctx->tile_sizes.ptr, sizeof(int64_t) * (ntiles + 1), hipMemcpyDeviceToHost,
+                                   st));
+            FRS_HIP(hipMemcpyAsync(hn.data(), dnorms, sizeof(TileNorm) * ntiles, hipMemcpyDeviceToHost, st));
+            FRS_HIP(hipStreamSynchronize(st));
+            prof_collect(ctx);
+            for (int t = 0; t < ntiles; t++) {
+                tile_min[t] = hn[t].dmin;
+                tile_max[t] = hn[t].dmax;
+            }
+            return FRS_OK;
+        }
         FRS_HIP(hipMemsetAsync(dstatus, 0, sizeof(uint64_t) * (nframes + 1), st));
         // frame-header table by frame number within a stream (fast path: mono, 16-bit, blocksize 4096)
         int hdr_n = 0;

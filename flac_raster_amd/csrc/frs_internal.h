@@ -68,7 +68,7 @@ struct frs_ctx {
     std::string err;
     // encode scratch
     DevBuf tiles, norms, analysis, slots, frame_bytes, frame_off, window, tile_sizes, luts, status, frame_tile,
-        hdr_tab, wave_tab, plist;
+        hdr_tab, wave_tab, plist, sub_slots, sub_bits, mc_bytes;
     int hdr_tab_n = -1, hdr_tab_sr = -1;  // cached frame-header table (fast encode path)
     bool force_generic = false;  // testing: route every job through the generic kernels
     // host staging (pinned)

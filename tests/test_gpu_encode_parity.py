@@ -183,3 +183,36 @@ def test_fast_path_stats_modes(dtype, lo, hi, tile, monkeypatch):
                 assert list(mn) == list(o_mn) and list(mx) == list(o_mx), ablate
         finally:
             ctx.close()
+
+
+@pytest.mark.parametrize("dtype,bands,shape,seed", [
+    (np.uint8, 3, (300, 500), 1),       # sample_rgb-like, partial last frame
+    (np.int16, 4, (1024, 1024), 2),     # whole frames only
+    (np.uint16, 5, (640, 701), 3),
+    (np.int16, 7, (256, 300), 4),       # the widest the multi-channel fast path takes
+])
+def test_multichannel_fast_path_matches_oracle(gpu_ctx, dtype, bands, shape, seed):
+    """Plain convert of a >= 3-band raster (converter.py:185-216: one stream, channels interleaved): the fast kernels
+    code the subframes and k_mc_assemble joins them; bytes equal the oracle's libFLAC restatement."""
+    H, W = shape
+    rng = np.random.default_rng(seed)
+    y, x = np.meshgrid(np.linspace(0, 20, H), np.linspace(0, 20, W), indexing="ij")
+    data = np.stack([1000 + 300 * np.sin(x * (0.5 + 0.1 * b)) * np.cos(y * 0.3) + 40 * rng.random((H, W))
+                     for b in range(bands)])
+    if dtype == np.uint8:
+        data = data / 8
+    data = data.astype(dtype)
+    data[:, 5:9, 5:40] = data[:, 5:6, 5:6]  # flat patches
+    sr = O.sample_rate_for(bands, H)
+    gpu_ctx.profile(True)
+    gpu_ctx.profile_reset()
+    d = gpu_ctx.make_desc(H, W, dtype, nbands=bands, tile_h=H, tile_w=W, sample_rate=sr, bits_per_sample=16)
+    arena, off, mn, mx, bps = gpu_ctx.encode_tiles_host(data, d)
+    assembled = gpu_ctx.profile_avg_ms("assemble")
+    gpu_ctx.profile(False)
+    assert assembled > 0, "expected the multi-channel fast path"
+    pcm, o_mn, o_mx, o_bps = O.normalize(data.transpose(1, 2, 0).reshape(-1, bands))
+    ref = O.encode_frames(pcm, o_bps, sr)
+    assert bps == o_bps == 16
+    assert arena[:off[-1]].tobytes() == ref
+    assert (mn[0], mx[0]) == (o_mn, o_mx)
