@@ -173,6 +173,7 @@ def main():
     if world == 1 and not args.no_extras:
         result["batched_decode"] = batched_decode(ctx, arena, off, mn, mx, rows, W, T)
         result["sentinel2"] = sentinel2(ctx)
+        result["convert_multiband"] = convert_multiband(ctx)
         result["end_to_end"] = end_to_end(ctx, raster, arena, off, rows, W, T, args)
     if rank == 0 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(ctx, raster, rows, W, T, off, arena, args)
@@ -294,6 +295,34 @@ def sentinel2(ctx, steps=5):
     buf.close()
     return {"raster": f"{H}x{W} uint16", "tile_size": T, "tiles": 121, "ms_per_step": round(dt * 1e3, 3),
             "Mpixels_s": round(H * W / dt / 1e6, 1), "fast_path": kern["partial"] > 0 and kern["compact"] < 0,
+            "kernels_ms": {k: v for k, v in kern.items() if v > 0}}
+
+
+def convert_multiband(ctx, steps=3):
+    """Plain `convert` of a C3-shaped multispectral raster (16384 x 16384 x 4 int16, converter.py:185-216): ONE
+    stream with the 4 bands interleaved, device-resident -- the multi-channel fast path (subframes by the fast
+    encoder, frames joined by k_mc_assemble)."""
+    B, H, W = 4, 16384, 16384
+    buf = ctx.alloc(B * H * W * 2)
+    ctx.synth_raster(buf, B, H, W, seed=5)
+    d = ctx.make_desc(H, W, np.int16, nbands=B, tile_h=H, tile_w=W, sample_rate=44100, bits_per_sample=16)
+    arena = ctx.alloc(ctx.arena_bound(d))
+    ctx.encode_tiles_device(buf.ptr, d, arena)
+    ctx.profile(True)
+    ctx.profile_reset()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        off, _, _, _ = ctx.encode_tiles_device(buf.ptr, d, arena)
+    ctx.sync()
+    dt = (time.perf_counter() - t0) / steps
+    ctx.profile(False)
+    kern = {k: round(ctx.profile_avg_ms(k), 4) for k in ("stats", "analyze", "partial", "encode", "assemble", "compact")}
+    arena.close()
+    buf.close()
+    return {"raster": f"{H}x{W}x{B} int16", "streams": 1, "channels": B, "ms_per_step": round(dt * 1e3, 3),
+            "Mpixels_s": round(H * W / dt / 1e6, 1), "Msamples_s": round(B * H * W / dt / 1e6, 1),
+            "compressed_bytes": int(off[-1]), "fast_path": kern["assemble"] > 0,
             "kernels_ms": {k: v for k, v in kern.items() if v > 0}}
 
 

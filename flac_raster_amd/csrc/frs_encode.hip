@@ -3400,8 +3400,8 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                       d->blocksize == 4096 && !Elem<DT>::is_float;
     // multi-channel streams of >= 3 channels (plain convert of a multi-band raster): libFLAC codes their channels
     // independently, so the fast kernels code the subframes and k_mc_assemble joins them (2 channels: libFLAC's
-    // stereo decorrelation, generic kernels; <= 7 channels: the assembly's LDS frame image)
-    const bool mc = allow_fast && !ctx->force_generic && P.bps == 16 && P.nch >= 3 && P.nch <= 7 &&
+    // stereo decorrelation, generic kernels)
+    const bool mc = allow_fast && !ctx->force_generic && P.bps == 16 && P.nch >= 3 && P.nch <= 8 &&
                     P.norm_mode == 0 && d->blocksize == 4096 && !Elem<DT>::is_float;
     int64_t npartial = 0;
     int64_t *hplist = ctx->pin.at<int64_t>(pin_pl);
@@ -3574,8 +3574,11 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                 ctx->err = "arena too small";
                 return FRS_E_NOSPACE;
             }
+            const size_t mc_lds = sizeof(uint32_t) * (size_t)(P.nch * kFrameWordsV3 + 16);  // <= 70 KB (8 channels)
+            FRS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mc_assemble),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)mc_lds));
             prof_begin(ctx, "assemble", &ev);
-            k_mc_assemble<<<(unsigned)nframes, 256, sizeof(uint32_t) * (size_t)(P.nch * kFrameWordsV3 + 16), st>>>(
+            k_mc_assemble<<<(unsigned)nframes, 256, mc_lds, st>>>(
                 P, dtiles, ctx->frame_tile.as<int32_t>(), dsub, dsbits, ctx->slots.as<uint32_t>(), dpbytes,
                 ctx->frame_off.as<int64_t>(), reinterpret_cast<uint8_t *>(arena_dev));
             prof_end(ctx, "assemble", ev);

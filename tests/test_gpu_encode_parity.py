@@ -189,7 +189,8 @@ def test_fast_path_stats_modes(dtype, lo, hi, tile, monkeypatch):
     (np.uint8, 3, (300, 500), 1),       # sample_rgb-like, partial last frame
     (np.int16, 4, (1024, 1024), 2),     # whole frames only
     (np.uint16, 5, (640, 701), 3),
-    (np.int16, 7, (256, 300), 4),       # the widest the multi-channel fast path takes
+    (np.int16, 7, (256, 300), 4),
+    (np.uint16, 8, (200, 333), 5),      # FLAC's channel limit: a 70 KB LDS frame image
 ])
 def test_multichannel_fast_path_matches_oracle(gpu_ctx, dtype, bands, shape, seed):
     """Plain convert of a >= 3-band raster (converter.py:185-216: one stream, channels interleaved): the fast kernels
