@@ -1762,6 +1762,28 @@ struct LaneReader {
     }
 };
 
+// Channel-planar int32 PCM of the multi-channel lane decoder -> the interleaved output (de-normalised when fused,
+// int32 PCM otherwise): one thread per output element, elements in output order (coalesced stores).
+__global__ void __launch_bounds__(256) k_interleave_dn(const int32_t *planar, const int64_t *poff, const int64_t *fbase,
+                                                      int ns, int nch, int blocksize, int32_t *pcm, DecOut dout) {
+    const int64_t total = (poff[ns] - poff[0]) * nch;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t g = poff[0] + e / nch;  // sample index
+        const int c = (int)(e - (g - poff[0]) * nch);
+        int lo = 0, hi = ns - 1;  // stream of sample g
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (poff[mid] <= g) lo = mid;
+            else hi = mid - 1;
+        }
+        const int64_t i = g - poff[lo];
+        const int64_t fi = fbase[lo] + i / blocksize;
+        const int32_t x = planar[(fi * nch + c) * (int64_t)blocksize + (i % blocksize)];
+        if (dout.out) dn_store(dout, g * nch + c, x, dout.dn[lo]);
+        else pcm[g * nch + c] = x;
+    }
+}
+
 // converter.py:88-110 value of one decoded sample as the bits of a <= 4-byte output element
 template <int OUT>
 __device__ inline uint32_t dn_bits_t(const DecOut &o, int32_t pcm, float2 p) {
@@ -1779,16 +1801,22 @@ __device__ inline uint32_t dn_bits_t(const DecOut &o, int32_t pcm, float2 p) {
     }
 }
 
-template <int OUT>
+// MC (multi-channel streams of >= 3 independent channels): the lane walks the frame's subframes in turn and writes
+// them channel-planar as int32 PCM to `planar` (frame fi, channel c at (fi * nch + c) * blocksize); k_interleave_dn
+// then interleaves and de-normalises.
+template <int OUT, bool MC = false>
 __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob, const int64_t *soff, int ns,
                                                            const int64_t *poff, const int64_t *cpos,
                                                            const int64_t *ends, const int64_t *fbase,
                                                            const int64_t *frame_cand, int64_t nframes,
                                                            int stream_bps, int32_t *pcm, int blocksize, int *nvalid,
-                                                           DecOut dout, int32_t *fb_list, int *fb_count) {
+                                                           DecOut dout, int32_t *fb_list, int *fb_count,
+                                                           int nch = 1, int32_t *planar = nullptr) {
+    static_assert(!MC || OUT == kOutPcm, "channel-planar int32 output");
     constexpr int es = OUT == kOutPcm ? 4 : OUT == kOutU8 ? 1 : 2;  // kOutAny: per-sample dn_store
     const int64_t fi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint8_t *obytes = OUT == kOutPcm ? reinterpret_cast<uint8_t *>(pcm) : static_cast<uint8_t *>(dout.out);
+    uint8_t *obytes = MC ? reinterpret_cast<uint8_t *>(planar)
+                         : OUT == kOutPcm ? reinterpret_cast<uint8_t *>(pcm) : static_cast<uint8_t *>(dout.out);
     bool ok = false;
     if (fi < nframes) {
         const int64_t ci = frame_cand[fi];
@@ -1800,13 +1828,15 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
             const int64_t nsamp = poff[s + 1] - poff[s];
             const int64_t kk = fi - fbase[s];
             const int64_t first = kk * blocksize;
-            const FrameHdr cd = parse_header(blob, fpos, send, 1, stream_bps);
-            if (cd.ok && cd.frame_no == kk && cd.bs <= blocksize && first + cd.bs <= nsamp) {
+            const FrameHdr cd = parse_header(blob, fpos, send, MC ? nch : 1, stream_bps);
+            bool take_all = !MC || cd.chass == nch - 1;  // independent channels only (no stereo decorrelation)
+            if (cd.ok && cd.frame_no == kk && cd.bs <= blocksize && first + cd.bs <= nsamp && take_all) {
                 const int bs = cd.bs;
-                const int64_t obase = poff[s] + first;
                 const float2 dnp = OUT != kOutPcm ? dout.dn[s] : make_float2(0.f, 0.f);
                 LaneReader br;
                 br.init(blob, fpos + cd.hdr_len, send);
+                for (int chn = 0; chn < (MC ? nch : 1) && take_all; chn++) {
+                const int64_t obase = MC ? (fi * nch + chn) * (int64_t)blocksize : poff[s] + first;
                 br.bits(1);
                 const int t = (int)br.bits(6);
                 int w = 0;
@@ -1930,9 +1960,11 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
                         }
                         if (br.bad) break;
                     }
-                    ok = take && !br.bad && ((br.pos() + 7) >> 3) + 2 == fend;
                 }
-                if (!take) fb_list[atomicAdd(fb_count, 1)] = (int32_t)fi;
+                take_all = take_all && take;
+                }  // channels
+                ok = take_all && !br.bad && ((br.pos() + 7) >> 3) + 2 == fend;
+                if (!take_all) fb_list[atomicAdd(fb_count, 1)] = (int32_t)fi;
             }
         }
     }
@@ -2019,13 +2051,20 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     // per CU at 62 KB of LDS each); FRS_DECODE_LANE=0/1 overrides for tests
     bool lane = pipe && frames >= kLaneMinFrames;
     if (ctx->decode_lane >= 0) lane = pipe && ctx->decode_lane == 1;
+    // multi-channel streams (>= 3 independent channels, 16-bit): the lane decoder walks each frame's subframes into a
+    // channel-planar int32 scratch, k_interleave_dn interleaves (and de-normalises); the wave decoder takes the rest
+    const bool mcl = channels >= 3 && channels <= 8 && bps <= 16 && blocksize <= kDecResMax && !ctx->force_generic &&
+                     frames >= 64 && ctx->decode_lane != 0;
+    const int64_t nsamp_all = pcm_off[nstreams] - pcm_off[0];
+    const int64_t planar_words = mcl ? frames * channels * (int64_t)blocksize : 0;
     if (fused && (!pipe || lane)) {  // the wave decoder de-normalises out of an int32 scratch
-        const int64_t nsamp = pcm_off[nstreams] - pcm_off[0];
         if (!pcm_dev) {
-            FRS_HIP(ctx->dec_pcm.ensure((size_t)nsamp * channels * 4 + 16));
+            FRS_HIP(ctx->dec_pcm.ensure((size_t)std::max(nsamp_all * channels, planar_words) * 4 + 16));
             pcm_dev = ctx->dec_pcm.as<int32_t>() - pcm_off[0] * channels;
         }
     }
+    if (mcl && !fused) FRS_HIP(ctx->dec_pcm.ensure((size_t)planar_words * 4 + 16));
+    // (the planar scratch is consumed by k_interleave_dn before the fallback decoder reuses dec_pcm)
     // Candidate capacity: every true frame plus false syncs (a sync pattern with a CRC-8-correct header inside
     // frame data, ~1e-7 per byte) with a wide margin; a crafted stream with more is rejected (nothing is written
     // past the cap).  Indices stay below 2^31.
@@ -2095,7 +2134,8 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     prof_begin(ctx, "decode_span", &ev);
     // launched before the host knows the candidate count (no mid-query sync): an upper-bound grid strides over
     // *ncand on the device; an overflowing selection makes every later kernel a no-op and is reported below
-    if (lane) {  // batched: one lane per candidate, over an upper-bound grid (no mid-call sync)
+    if (lane || !pipe) {  // batched (or long multi-channel / 32-bit frames, which the wave form would walk on one lane
+                          // past its LDS stage): one lane per candidate, over an upper-bound grid (no mid-call sync)
         k_span_crc_lane<<<(unsigned)((std::min<int64_t>(cand_cap, 2 * frames + 256) + 255) / 256), 256, 0, st>>>(
             blob_dev, dsoff, nstreams, cpos, ncand, (int)cand_cap, max_frame, ends, nexti);
     } else if (max_frame < (int64_t)4096 * 256) {  // x^(8m) table range of the wave CRC
@@ -2134,6 +2174,19 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         k_decode_frames_wave_list<<<(unsigned)std::min<int64_t>(frames, 4 * (int64_t)ctx->num_cus), 64, 0, st>>>(
             blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, dchain, channels, bps, pcm_dev, blocksize, nvalid,
             dout, fbl, fbc);
+    } else if (mcl) {
+        FRS_HIP(ctx->dec_fb.ensure(sizeof(int32_t) * (size_t)frames + 64));
+        int32_t *fbl = ctx->dec_fb.as<int32_t>();
+        int *fbc = ncand + 3;
+        int32_t *planar = ctx->dec_pcm.as<int32_t>();
+        k_decode_frames_lane<kOutPcm, true><<<(unsigned)((frames + 255) / 256), 256, 0, st>>>(
+            blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, dchain, frames, bps, pcm_dev, blocksize, nvalid, dout,
+            fbl, fbc, channels, planar);
+        k_interleave_dn<<<(unsigned)std::min<int64_t>((nsamp_all * channels + 255) / 256, 16 * (int64_t)ctx->num_cus),
+                          256, 0, st>>>(planar, dpoff, dfbase, nstreams, channels, blocksize, pcm_dev, dout);
+        k_decode_frames_wave_list<<<(unsigned)std::min<int64_t>(frames, 4 * (int64_t)ctx->num_cus), 64, 0, st>>>(
+            blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, dchain, channels, bps, pcm_dev, blocksize, nvalid,
+            dout, fbl, fbc);
     } else if (pipe)
         k_decode_frames_pipe<<<(unsigned)frames, 128, 0, st>>>(blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase,
                                                                dchain, frames, channels, bps, pcm_dev, blocksize, nvalid,
@@ -2148,7 +2201,7 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     FRS_HIP(hipMemcpyAsync(hv, ncand, sizeof(int) * 4, hipMemcpyDeviceToHost, st));
     FRS_HIP(hipStreamSynchronize(st));
     prof_collect(ctx);
-    if (ctx->prof && lane) {  // frames the lane decoder handed to the wave decoder (profile_avg_ms of this name)
+    if (ctx->prof && (lane || mcl)) {  // frames the lane decoder handed to the wave decoder (profile_avg_ms of this name)
         ProfEntry &e = ctx->prof_tab["lane_fallback_frames"];
         e.total_ms += hv[3];
         e.count += 1;
