@@ -2222,8 +2222,9 @@ constexpr uint64_t kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62, kValMask = (1u
 // the fixed candidate's partition sums fall out of the fixed-predictor totals pass.
 
 constexpr int kXpowHi = (kXpowBytes + 63) / 64;
+constexpr int kBufWordsV3 = kFrameWordsV3 + 64;  // + the overflow row of the code writer (lds_put_left)
 struct EncV3Shared {
-    uint32_t bits[4][kFrameWordsV3];
+    uint32_t bits[4][kBufWordsV3];
     int16_t lut[kLutCap];
     uint16_t crc8x[8][256];  // slice-by-8 tables (T_0..T_3 serve the slice-by-4 / byte steps)
     uint16_t xlo[64];       // x^(8m) mod P, m = 0..63
@@ -2252,6 +2253,15 @@ __device__ inline FbMap fb_map(uint32_t words) {  // words the frame may touch (
     const uint32_t c = max(1u, (words + 63) >> 6);
     return FbMap{c, ((1u << 20) + c - 1) / c, 64 * c - 1};
 }
+// The code writer (lds_put_left) ORs a straddling code's second word one row below its first (a ds offset),
+// which is word w + 1 except when w is the last word of its column: that part lands in the column's overflow
+// row C instead of row 0 of the next column.  fb_fold moves those words home (after the wave's writes landed).
+__device__ inline void fb_fold(uint32_t *buf, const FbMap &M, int lane) {
+    uint32_t *ovr = buf + (M.c << 6) + lane;
+    const uint32_t v = *ovr;
+    *ovr = 0;
+    if (lane < 63 && v) atomicOr(buf + lane + 1, v);
+}
 
 // bit writer without branches: the (up to 32-bit) code at [pos, pos + nbits) straddles at most 2 words
 __device__ inline void lds_put_bits2(uint32_t *buf, const FbMap &M, uint32_t pos, uint32_t val, int nbits) {
@@ -2275,14 +2285,17 @@ __device__ inline uint32_t sad_u32(uint32_t a, uint32_t b, uint32_t c) {
     return d;
 }
 
-// OR a left-aligned code (its first bit in bit 31) into the bit buffer at bit position pos
-__device__ inline void lds_put_left(uint32_t *buf, const FbMap &M, uint32_t pos, uint32_t codeL) {
+// OR a left-aligned code (its first bit in bit 31) into the bit buffer at bit position pos.  The second word goes
+// one row below the first (+256 B, the ds offset): word wi + 1, or the column's overflow row (fb_fold).
+// nk4 = -4 (64 C - 1): byte address = buf + 256 wi + nk4 col(wi), one 24-bit multiply-add.
+__device__ inline void lds_put_left(uint32_t *buf, const FbMap &M, int nk4, uint32_t pos, uint32_t codeL) {
     const uint32_t hi = __builtin_amdgcn_alignbit(0u, codeL, pos);  // codeL >> (pos & 31)
     const uint32_t lo = __builtin_amdgcn_alignbit(codeL, 0u, pos);  // codeL << (32 - (pos & 31)); 0 if aligned
-    // phys(wi + 1) = (wi << 6) - col(wi + 1) (64 C - 1) + 64; the + 64 folds into the ds offset
-    const uint32_t wi = pos >> 5, base = wi << 6;
-    atomicOr(buf + ((uint32_t)__mul24((int)M.col(wi), -(int)M.k) + base), hi);
-    atomicOr(buf + ((uint32_t)__mul24((int)M.col(wi + 1), -(int)M.k) + base) + 64, lo);
+    const uint32_t wi = pos >> 5;
+    uint32_t *p = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(buf) + (wi << 8) +
+                                               __mul24((int)M.col(wi), nk4));
+    atomicOr(p, hi);
+    atomicOr(p + 64, lo);
 }
 
 __device__ inline uint32_t zigzag(int32_t r) { return ((uint32_t)r << 1) ^ (uint32_t)(r >> 31); }
@@ -2438,7 +2451,7 @@ __device__ inline void resolve_and_store(const EncodeParams &P, PendingFrame &pf
     if (ok) {
         for (uint32_t i = 0; i < M.c; i++) fbuf[(i << 6) | (uint32_t)lane] = 0;
     } else {
-        for (uint32_t i = (uint32_t)lane; i < (uint32_t)kFrameWordsV3; i += 64) fbuf[i] = 0;
+        for (uint32_t i = (uint32_t)lane; i < (uint32_t)kBufWordsV3; i += 64) fbuf[i] = 0;
     }
     pf.f = -1;
 }
@@ -2814,14 +2827,14 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
             if (m % 4 == 0 && m) asm volatile("" : "+v"(lens));
             int32_t re, ro;
             residual_pair(E, C, shift, m, re, ro);
-            const uint32_t ue = zigzag(re), uo = zigzag(ro);
-            uint32_t le = 1u + (uint32_t)k + (ue >> k), lo = 1u + (uint32_t)k + (uo >> k);
+            uint32_t le = zigzag(re) >> k, lo = zigzag(ro) >> k;
             if (2 * m < kMaxLpc) {
                 if (l0 && 2 * m < o) le = 0;
                 if (l0 && 2 * m + 1 < o) lo = 0;
             }
             lens += le + lo;
         }
+        lens += (uint32_t)(64 - (l0 ? o : 0)) * (1u + (uint32_t)k);  // unary stop bit + k low bits per code
         reg_fence(E);
         const uint32_t incl = dpp_incl_scan_u32(lens);
         const uint64_t excl = incl - lens;
@@ -2912,11 +2925,12 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
                           (uint32_t)qi & ((1u << A.lpc_prec) - 1u), A.lpc_prec);
     }
     if (type >= 2 && ok && (lane & (lanes_per - 1)) == 0) lds_put_bits2(fbuf, M, run - 4u, (uint32_t)k, 4);
+    const int nk4 = -4 * (int)M.k;
     if (type == 1) {
         const uint32_t p0 = pos + (uint32_t)(64 * lane) * (uint32_t)sbps;
         const uint32_t shl = 32u - (uint32_t)sbps;
 #pragma unroll
-        for (int j = 0; j < 64; j++) lds_put_left(fbuf, M, p0 + (uint32_t)j * sbps, (uint32_t)X(j) << shl);
+        for (int j = 0; j < 64; j++) lds_put_left(fbuf, M, nk4, p0 + (uint32_t)j * sbps, (uint32_t)X(j) << shl);
     } else if (type >= 2 && ok) {
         // code = stop bit + k low bits, left-aligned: (u << (31 - k)) with the stop bit forced on
         const uint32_t sh = 31u - (uint32_t)k, oneL = 0x80000000u, lowL = (k ? (0xFFFFFFFFu >> (32 - k)) : 0u) << sh;
@@ -2935,13 +2949,18 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
                     codeL = 0;
                     adv = 0;
                 }
-                lds_put_left(fbuf, M, run + q, codeL);
+                lds_put_left(fbuf, M, nk4, run + q, codeL);
                 run += adv;
             }
         }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS atomics have landed
     __builtin_amdgcn_wave_barrier();
+    if (type == 1 || (type >= 2 && ok)) {  // (wave-uniform) codes were written: overflow rows home
+        fb_fold(fbuf, M, lane);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+    }
     uint32_t crc = 0;
     if (!SUB && ok) {
         // slice-by-4 over 32-bit words, one contiguous word range per lane, combined with x^(8m) factors
@@ -2987,7 +3006,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
             for (uint32_t wi = (uint32_t)lane; wi < nw; wi += 64) dst[wi] = fbuf[M(wi)];
             for (uint32_t i = 0; i < M.c; i++) fbuf[(i << 6) | (uint32_t)lane] = 0;
         } else {
-            for (uint32_t i = (uint32_t)lane; i < (uint32_t)kFrameWordsV3; i += 64) fbuf[i] = 0;
+            for (uint32_t i = (uint32_t)lane; i < (uint32_t)kBufWordsV3; i += 64) fbuf[i] = 0;
         }
         if (l0) sub_bits[sub] = ok ? (int32_t)end_bits : -1;
         (void)fbytes;
@@ -3017,7 +3036,7 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
     for (int i = threadIdx.x; i < 256; i += blockDim.x) S.crc8[i] = c_crc8[i];
     for (int i = threadIdx.x; i < 64; i += blockDim.x) S.xlo[i] = g_xpow_bytes[i];
     for (int i = threadIdx.x; i < kXpowHi; i += blockDim.x) S.xhi[i] = g_xpow_bytes[64 * i];
-    for (int i = threadIdx.x; i < 4 * kFrameWordsV3; i += blockDim.x) (&S.bits[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < 4 * kBufWordsV3; i += blockDim.x) (&S.bits[0][0])[i] = 0;
     if (threadIdx.x == 0) S.lut_tile = -1;
     PendingFrame prev;
     uint32_t *fbuf = S.bits[wave];
