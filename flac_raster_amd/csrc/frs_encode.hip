@@ -2298,6 +2298,24 @@ __device__ inline void lds_put_left(uint32_t *buf, const FbMap &M, int nk4, uint
     atomicOr(p + 64, lo);
 }
 
+// LUT normalisation of 64 packed 16-bit samples straight into packed pairs (no wasted bits): both halves' LDS
+// byte addresses by one packed 16-bit multiply-add (2 x + lutbase - 2 min, exact mod 2^16: the LUT lies below
+// 64 KB of LDS), two ds_read_u16 and one v_lshl_or per pair.  (d16 / d16_hi loads into one register would save the
+// v_lshl_or, but the second load of a pair must not issue before the first has landed.)
+__device__ inline void lut_gather_pairs(const uint32_t *w, const int16_t *lut, int32_t imin, uint32_t *out) {
+    const uint32_t lb = (uint32_t)reinterpret_cast<uintptr_t>(lut);  // low 32 bits of a flat LDS address
+    const uint32_t c16 = (lb - 2u * (uint32_t)imin) & 0xFFFFu, cc = c16 | (c16 << 16), two = 0x00020002u;
+    const char *lds0 = reinterpret_cast<const char *>(lut) - lb;  // LDS byte 0
+#pragma unroll
+    for (int m = 0; m < 32; m++) {
+        uint32_t a;
+        asm("v_pk_mad_u16 %0, %1, %2, %3" : "=v"(a) : "v"(w[m]), "v"(two), "v"(cc));
+        const uint32_t lo = *reinterpret_cast<const uint16_t *>(lds0 + (a & 0xFFFFu));
+        const uint32_t hi = *reinterpret_cast<const uint16_t *>(lds0 + (a >> 16));
+        out[m] = lo | (hi << 16);
+    }
+}
+
 __device__ inline uint32_t zigzag(int32_t r) { return ((uint32_t)r << 1) ^ (uint32_t)(r >> 31); }
 
 struct PendingFrame {  // a frame whose bytes sit in the wave's bit buffer, offset not yet resolved
@@ -2554,11 +2572,15 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         const uint32_t sl0 = (uint32_t)s0 + 64u * (uint32_t)lane;  // tile pixels < 2^31
         const uint32_t row = udiv_inv(sl0, (uint32_t)g.w, 1.0 / (double)g.w);
         ch.load(base, P.row_stride, g.w, row, (int)(sl0 - row * (uint32_t)g.w), (g.w % 64) == 0 ? P.vec_ok : 0, 64);
-        int32_t lo = 0;
-        norm_chunk<DT>(ch, tn, lut, [&](int j, int32_t x) {
-            if (j & 1) E[4 + (j >> 1)] = pack2(lo, x >> w);
-            else lo = x >> w;
-        });
+        if (sizeof(T) == 2 && tn.mode == kNormLut && w == 0) {  // (wave-uniform) the common case
+            lut_gather_pairs(ch.w, lut, (int32_t)tn.imin, E + 4);
+        } else {
+            int32_t lo = 0;
+            norm_chunk<DT>(ch, tn, lut, [&](int j, int32_t x) {
+                if (j & 1) E[4 + (j >> 1)] = pack2(lo, x >> w);
+                else lo = x >> w;
+            });
+        }
     }
 #pragma unroll
     for (int m = 0; m < 4; m++) E[m] = dpp_wave_shr1(E[32 + m]);
@@ -2932,8 +2954,9 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
 #pragma unroll
         for (int j = 0; j < 64; j++) lds_put_left(fbuf, M, nk4, p0 + (uint32_t)j * sbps, (uint32_t)X(j) << shl);
     } else if (type >= 2 && ok) {
-        // code = stop bit + k low bits, left-aligned: (u << (31 - k)) with the stop bit forced on
-        const uint32_t sh = 31u - (uint32_t)k, oneL = 0x80000000u, lowL = (k ? (0xFFFFFFFFu >> (32 - k)) : 0u) << sh;
+        // code = stop bit + k low bits, left-aligned: u << (31 - k) keeps u's low k bits below bit 31 (higher bits
+        // shift out, bit k lands on bit 31) and the stop bit is forced on
+        const uint32_t sh = 31u - (uint32_t)k, oneL = 0x80000000u;
 #pragma unroll
         for (int m = 0; m < 32; m++) {
             if (m % 4 == 0 && m) asm volatile("" : "+v"(run));
@@ -2943,7 +2966,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
             for (int h = 0; h < 2; h++) {
                 const int j = 2 * m + h;
                 const uint32_t u = zigzag(h ? ro : re);
-                uint32_t q = u >> k, codeL = ((u << sh) & lowL) | oneL, adv = q + 1 + (uint32_t)k;
+                uint32_t q = u >> k, codeL = (u << sh) | oneL, adv = q + 1 + (uint32_t)k;
                 if (j < kMaxLpc && l0 && j < o) {
                     q = 0;
                     codeL = 0;
