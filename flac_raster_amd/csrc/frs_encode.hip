@@ -797,6 +797,15 @@ constexpr int kEncThreads = 256;
 constexpr int kBitWords = 4096 + 64;  // one 32-bit subframe (4096 x 32 bits) + headers + carry
 
 __constant__ uint8_t c_crc8[256];
+// 2^18 / (n - order) for the first Rice partition of partition order po (n = 4096 >> po), order 0..8 (libFLAC's
+// parameter estimate; the other partitions divide by a power of two)
+__constant__ uint32_t c_rice_div[6][9] = {
+    {64, 64, 64, 64, 64, 64, 64, 64, 64},
+    {128, 128, 128, 128, 128, 128, 128, 128, 128},
+    {256, 256, 256, 256, 257, 257, 257, 257, 258},
+    {512, 513, 514, 515, 516, 517, 518, 519, 520},
+    {1024, 1028, 1032, 1036, 1040, 1044, 1048, 1052, 1057},
+    {2048, 2064, 2080, 2097, 2114, 2131, 2148, 2166, 2184}};
 
 struct RiceChoice {
     uint32_t bits;   // estimated residual bits (find_best_partition_order_)
@@ -2681,59 +2690,23 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
             }
         }
     };
-    // 32-bit form of the same search, exact when every lane sum is < 2^24 (group sums < 2^30): the division
-    // by a non-first partition's size is a shift, and k ? s >> (k-1) : s << 1 == (2s) >> k
-    auto rice32 = [&](uint32_t lane_sum, int order, uint32_t &best_bits, int &best_po, int &my_k) {
-        best_bits = 0;
-        best_po = 0;
-        my_k = 0;
-        uint32_t g = lane_sum;
-        g += bfly_partner<1>(g);
+    // 32-bit form of the same search, exact when every lane sum is < 2^24 (group sums < 2^30), for NC candidates
+    // at once.  Every lane computes the bits of ITS partition at every order (replicated over the partition's lanes);
+    // an order's total then needs only the butterfly stages at or above its partition width (2 + 3 + 4 + 5 stages for
+    // orders 5..1 instead of a full 6-stage wave sum per order), and the division by a non-first partition's size is
+    // a shift (the first partition's 2^18 / (n - order) comes from a table); k ? s >> (k-1) : s << 1 == (2s) >> k.
+    auto rice32m = [&](auto NCt, const uint32_t *sums, const int *ord, uint32_t *bb, int *bp, int *bk) {
+        constexpr int NC = decltype(NCt)::value;
+        uint32_t g[NC], V[NC][6], Kp[NC];
 #pragma unroll
-        for (int po = 5; po >= 0; po--) {
-            if (po == 4) g += bfly_partner<2>(g);
-            if (po == 3) g += bfly_partner<4>(g);
-            if (po == 2) g += bfly_partner<8>(g);
-            if (po == 1) g += bfly_partner<16>(g);
-            if (po == 0) g += bfly_partner<32>(g);
-            const int lanes_per = 64 >> po;
-            const uint32_t pbase = (uint32_t)(n >> po);
-            const bool first = lane < lanes_per;
-            const uint32_t ns = first ? pbase - (uint32_t)order : pbase;
-            const uint32_t div_first = uni(0x40000u / (pbase - (uint32_t)order));
-            const uint32_t pf = (uint32_t)(((uint64_t)(g - 1u) * div_first) >> 18);
-            const uint32_t pr = (g - 1u) >> (12 - po);
-            const uint32_t prod = first ? pf : pr;
-            uint32_t k = (g < 2 || prod == 0) ? 0u : 32u - (uint32_t)__builtin_clz(prod);
-            k = min(k, 14u);
-            const uint32_t pb = 4 + (1 + k) * ns + ((2 * g) >> k) - (ns >> 1);
-            const uint32_t contrib = ((lane & (lanes_per - 1)) == 0) ? pb : 0u;
-            const uint32_t bits = 6 + dpp_wave_sum_u32(contrib);
-            if (best_bits == 0 || bits < best_bits) {
-                best_bits = bits;
-                best_po = po;
-                my_k = (int)k;
-            }
+        for (int c = 0; c < NC; c++) {
+            g[c] = sums[c] + bfly_partner<1>(sums[c]);
+            Kp[c] = 0;
         }
-    };
-    auto rice = [&](uint32_t lane_sum, int order, uint32_t &best_bits, int &best_po, int &my_k) {
-        if (__ballot(lane_sum >= (1u << 24)) == 0) rice32(lane_sum, order, best_bits, best_po, my_k);
-        else rice64(lane_sum, order, best_bits, best_po, my_k);
-    };
-    // both candidates' searches in one loop (independent DPP chains overlap); exact 32-bit form when every
-    // lane sum is < 2^24, else the 64-bit form per candidate
-    auto rice32x2 = [&](uint32_t sa, int oa, uint32_t sb, int ob, uint32_t *bb, int *bp, int *bk) {
-        uint32_t g[2] = {sa, sb};
-        const int ord[2] = {oa, ob};
-        bb[0] = bb[1] = 0;
-        bp[0] = bp[1] = 0;
-        bk[0] = bk[1] = 0;
-#pragma unroll
-        for (int c = 0; c < 2; c++) g[c] += bfly_partner<1>(g[c]);
 #pragma unroll
         for (int po = 5; po >= 0; po--) {
 #pragma unroll
-            for (int c = 0; c < 2; c++) {
+            for (int c = 0; c < NC; c++) {
                 if (po == 4) g[c] += bfly_partner<2>(g[c]);
                 if (po == 3) g[c] += bfly_partner<4>(g[c]);
                 if (po == 2) g[c] += bfly_partner<8>(g[c]);
@@ -2743,31 +2716,65 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
             const int lanes_per = 64 >> po;
             const uint32_t pbase = (uint32_t)(n >> po);
             const bool first = lane < lanes_per;
-            uint32_t contrib[2], kk[2];
 #pragma unroll
-            for (int c = 0; c < 2; c++) {
+            for (int c = 0; c < NC; c++) {
                 const uint32_t ns = first ? pbase - (uint32_t)ord[c] : pbase;
-                const uint32_t div_first = uni(0x40000u / (pbase - (uint32_t)ord[c]));
+                const uint32_t div_first = c_rice_div[po][ord[c]];
                 const uint32_t pf = (uint32_t)(((uint64_t)(g[c] - 1u) * div_first) >> 18);
                 const uint32_t pr = (g[c] - 1u) >> (12 - po);
                 const uint32_t prod = first ? pf : pr;
                 uint32_t k = (g[c] < 2 || prod == 0) ? 0u : 32u - (uint32_t)__builtin_clz(prod);
                 k = min(k, 14u);
-                kk[c] = k;
-                const uint32_t pb = 4 + (1 + k) * ns + ((2 * g[c]) >> k) - (ns >> 1);
-                contrib[c] = ((lane & (lanes_per - 1)) == 0) ? pb : 0u;
+                Kp[c] |= k << (4 * (5 - po));
+                V[c][5 - po] = 4 + (1 + k) * ns + ((2 * g[c]) >> k) - (ns >> 1);
             }
-            uint32_t tot[2];
-            dpp_wave_sum_multi<2>(contrib, tot);
+        }
+        // V[c][i] (order 5 - i) is uniform over partitions of 2^(i + 1) lanes: butterflies from that width up
 #pragma unroll
-            for (int c = 0; c < 2; c++) {
-                const uint32_t bits = 6 + tot[c];
-                if (bb[c] == 0 || bits < bb[c]) {
-                    bb[c] = bits;
-                    bp[c] = po;
-                    bk[c] = (int)kk[c];
+        for (int c = 0; c < NC; c++) V[c][0] += bfly_partner<2>(V[c][0]);
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+#pragma unroll
+            for (int i = 0; i <= 1; i++) V[c][i] += bfly_partner<4>(V[c][i]);
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+#pragma unroll
+            for (int i = 0; i <= 2; i++) V[c][i] += bfly_partner<8>(V[c][i]);
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+#pragma unroll
+            for (int i = 0; i <= 3; i++) V[c][i] += bfly_partner<16>(V[c][i]);
+#pragma unroll
+        for (int c = 0; c < NC; c++)
+#pragma unroll
+            for (int i = 0; i <= 4; i++) V[c][i] += bfly_partner<32>(V[c][i]);
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+            uint32_t best_bits = 0;
+            int best_i = 0;
+#pragma unroll
+            for (int i = 0; i < 6; i++) {  // orders 5 .. 0, strict <
+                const uint32_t bits = 6 + uni(V[c][i]);
+                if (best_bits == 0 || bits < best_bits) {
+                    best_bits = bits;
+                    best_i = i;
                 }
             }
+            bb[c] = best_bits;
+            bp[c] = 5 - best_i;
+            bk[c] = (int)((Kp[c] >> (4 * best_i)) & 15u);
+        }
+    };
+    auto rice = [&](uint32_t lane_sum, int order, uint32_t &best_bits, int &best_po, int &my_k) {
+        if (__ballot(lane_sum >= (1u << 24)) == 0) {
+            const uint32_t sm[1] = {lane_sum};
+            const int od[1] = {order};
+            uint32_t b1[1];
+            int p1[1], k1[1];
+            rice32m(std::integral_constant<int, 1>{}, sm, od, b1, p1, k1);
+            best_bits = b1[0], best_po = p1[0], my_k = k1[0];
+        } else {
+            rice64(lane_sum, order, best_bits, best_po, my_k);
         }
     };
     uint32_t rb_f = 0, rb_l = 0;
@@ -2775,7 +2782,9 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     if (cand_fixed && cand_lpc && __ballot(sf >= (1u << 24) || sl >= (1u << 24)) == 0) {
         uint32_t bb[2];
         int bp[2], bk[2];
-        rice32x2(sf, of, sl, ol, bb, bp, bk);
+        const uint32_t sm[2] = {sf, sl};
+        const int od[2] = {of, ol};
+        rice32m(std::integral_constant<int, 2>{}, sm, od, bb, bp, bk);
         rb_f = bb[0], po_f = bp[0], k_f = bk[0];
         rb_l = bb[1], po_l = bp[1], k_l = bk[1];
     } else {
