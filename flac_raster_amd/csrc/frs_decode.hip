@@ -619,6 +619,42 @@ __global__ void __launch_bounds__(64) k_chain_lds(const int64_t *soff, int ns, c
     if (in_lds)
         for (int k = lane; k < c1 - c0; k += 64) nx[k] = nexti[c0 + k];
     __syncthreads();
+    if (!in_lds && c0 < c1 && cpos[c0] == soff[s] && nf > 0) {
+        // a long stream (one multi-channel file: tens of thousands of frames) would be walked one dependent global
+        // load per frame.  Optimistic parallel ranking instead: the verified candidates (link != -1) in position
+        // order ARE the chain when there are nf of them, each links to the next and the last to the stream end --
+        // checked below; anything else (a false sync with a verified span) falls back to the exact walk.
+        int64_t cnt = 0;
+        for (int i0 = c0; i0 < c1; i0 += 256) {
+            int32_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = i0 + 64 * u + lane;
+                v[u] = i < c1 ? nexti[i] : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = i0 + 64 * u + lane;
+                const uint64_t m = __ballot(v[u] != -1);
+                const int64_t r = cnt + __popcll(m & ((1ull << lane) - 1ull));
+                if (v[u] != -1 && r < nf) frame_cand[fb + r] = i;
+                cnt += __popcll(m);
+            }
+        }
+        bool good = cnt == nf;
+        if (good) {
+            __threadfence();
+            bool bad_link = false;
+            for (int64_t k = lane; k < nf; k += 64) {
+                const int64_t ci = frame_cand[fb + k];
+                const int32_t want = k + 1 < nf ? (int32_t)frame_cand[fb + k + 1] : -2;
+                bad_link |= nexti[ci] != want || (k == 0 && ci != c0);  // frame 0 is the stream's first byte
+            }
+            good = __ballot(bad_link) == 0;
+        }
+        if (good) return;
+        __threadfence();
+    }
     if (lane != 0) return;
     bool ok = c0 < c1 && cpos[c0] == soff[s];
     int64_t k = 0;

@@ -146,3 +146,30 @@ def test_multichannel_decode_matches_oracle(gpu_ctx, kind, bands, dtype, monkeyp
     assert np.array_equal(vals.reshape(-1), O.denormalize_i16(ref, mn, mx, dtype).reshape(-1))
     assert np.array_equal(vals.reshape(H, W, bands).transpose(2, 0, 1), data)  # lossless round trip
     dctx.close()
+
+
+@pytest.mark.parametrize("kind", ["lane", "pipe"])
+def test_long_stream_chain_matches_oracle(gpu_ctx, kind, monkeypatch):
+    """One stream of more frames than k_chain_lds's LDS table (4096; a plain convert of a large raster is one stream):
+    its frames are ranked in parallel (the verified sync candidates in position order, every link checked) instead of
+    a dependent walk; the decode equals the oracle's, and a frame broken in the middle still ends in FrsError."""
+    from flac_raster_amd import _native
+    rng = np.random.default_rng(11)
+    H, W = 2304, 8192
+    y, x = np.meshgrid(np.linspace(0, 20, H), np.linspace(0, 60, W), indexing="ij")
+    band = (1000 + 300 * np.sin(x * 0.8) * np.cos(y * 0.3) + 60 * rng.random((H, W))).astype(np.int16)
+    d = gpu_ctx.make_desc(H, W, band.dtype, tile_h=H, tile_w=W, sample_rate=44100, bits_per_sample=16)
+    arena, off, mn, mx, bps = gpu_ctx.encode_tiles_host(band, d)
+    n = H * W
+    assert n // 4096 > 4096
+    dctx = _decoder_ctx(kind, monkeypatch)
+    pcm = dctx.decode_frames_host(arena, off, [n], channels=1, bps=16)
+    assert np.array_equal(pcm, O.decode_frames(arena.tobytes(), 1, 16, n))
+    vals = dctx.decode_tiles_host(arena, off, [n], channels=1, bps=16, data_min=mn, data_max=mx, dtype=band.dtype)
+    assert np.array_equal(vals.reshape(H, W), band)
+    flipped = arena.copy()
+    mid = int(off[1]) * 7 // 10
+    flipped[mid:mid + 64] ^= 0x5A
+    with pytest.raises(_native.FrsError):
+        dctx.decode_frames_host(flipped, off, [n], channels=1, bps=16)
+    dctx.close()
