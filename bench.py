@@ -400,11 +400,12 @@ def end_to_end(ctx, raster, arena, off_dev, rows, W, T, args):
                 lossless &= bool(np.array_equal(arr[0], band[w["row_off"]:w["row_off"] + w["height"],
                                                              w["col_off"]:w["col_off"] + w["width"]]))
         ms = np.array(lat) * 1e3
-        res["extract_streaming"] = {"p50_ms": round(float(np.percentile(ms, 50)), 3),
-                                    "p90_ms": round(float(np.percentile(ms, 90)), 3), "queries": len(lat),
-                                    "index_load_ms": round(load_ms, 2), "lossless": lossless,
-                                    "path": "file: select + range read + tag parse + fused GPU decode -> host array"}
-        if not args.no_cpu:
+        if len(lat):  # (--queries 0: no extract leg)
+            res["extract_streaming"] = {"p50_ms": round(float(np.percentile(ms, 50)), 3),
+                                        "p90_ms": round(float(np.percentile(ms, 90)), 3), "queries": len(lat),
+                                        "index_load_ms": round(load_ms, 2), "lossless": lossless,
+                                        "path": "file: select + range read + tag parse + fused GPU decode -> host array"}
+        if not args.no_cpu and len(lat):
             res["cpu_baseline"] = e2e_cpu_baseline(band, out, index, n, T, qs)
     finally:
         if out.exists():

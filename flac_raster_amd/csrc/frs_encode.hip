@@ -1292,6 +1292,14 @@ constexpr int kFrameWordsV3 = 2176;  // 69632 bits >= worst exact frame (DESIGN.
 constexpr int kXpowBytes = kFrameWordsV3 * 4 + 64;  // multiple of 64 (LDS split tables)
 __constant__ uint16_t c_crc16x8[8][256];           // T_k[v] = CRC-16 of byte v followed by k zero bytes
 __device__ uint16_t g_xpow_bytes[kXpowBytes];      // x^(8m) mod P for m bytes
+__device__ uint16_t g_xpow_8k[32];                  // x^(8 * 8192 q) mod P
+// x^(8m) mod P for a byte count m: one table read below kXpowBytes, two reads and a multiply below 256 KiB (frames
+// of up to 8 channels), the square-and-multiply loop beyond
+__device__ inline uint32_t xpow_bytes(int64_t m) {
+    if (m < kXpowBytes) return g_xpow_bytes[m];
+    if (m < 32 * 8192) return gf_mulmod(g_xpow_bytes[m & 8191], g_xpow_8k[m >> 13]);
+    return xpow8((uint64_t)m);
+}
 
 // CRC-16 (init 0) of bytes [0, L) of a 4-byte aligned frame image, by one 256-thread work-group: thread t folds a
 // contiguous word range with slice-by-4 tables in LDS (T), shifts it to the end of the frame by x^(8m) (one
@@ -1314,7 +1322,7 @@ __device__ inline uint32_t wg_crc16(const uint8_t *src, int64_t L, const uint16_
         end = L;
     }
     const int64_t m = L - end;
-    if (c && m > 0) c = gf_mulmod(c, m < kXpowBytes ? (uint32_t)g_xpow_bytes[m] : xpow8((uint64_t)m));
+    if (c && m > 0) c = gf_mulmod(c, xpow_bytes(m));
     for (int o = 32; o > 0; o >>= 1) c ^= __shfl_xor(c, o);
     if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
     __syncthreads();
@@ -3166,7 +3174,10 @@ __global__ void k_mc_frame_bytes(const EncodeParams P, const TileGeom *tiles, co
     frame_bytes[f] = ((bits + 7) >> 3) + 2;
 }
 
-// one work-group per frame: the frame image in LDS (big-endian bit order words), then its bytes to the arena
+// Persistent work-groups (CRC tables loaded once), one frame at a time: the frame image in LDS (big-endian bit
+// order words), then its bytes to the arena.  Only the frame's own words are zeroed; a subframe's interior words are
+// plain stores (each is made of two of its source words), its first and last words -- shared with the header or the
+// neighbouring subframe -- are ORed in.
 __global__ void __launch_bounds__(256) k_mc_assemble(const EncodeParams P, const TileGeom *tiles, const int32_t *ftile,
                                                     const uint32_t *sub_slots, const int32_t *sub_bits,
                                                     const uint32_t *pslots, const int64_t *pbytes,
@@ -3174,35 +3185,54 @@ __global__ void __launch_bounds__(256) k_mc_assemble(const EncodeParams P, const
     extern __shared__ uint32_t W[];  // nch * kFrameWordsV3 + 16 words
     __shared__ uint16_t T[4][256];
     __shared__ uint32_t wc[4];
-    const int64_t f = blockIdx.x;
+    const int tid = threadIdx.x;
+    wg_load_crc_tables(T);
+    for (int64_t f = blockIdx.x; f < P.nframes; f += gridDim.x) {
+    __syncthreads();  // the previous frame's readers of W / wc are done
     const TileGeom g = tiles[ftile[f]];
     const int64_t fk = f - g.frame_base;
     uint8_t *dst = arena + frame_off[f];
-    const int tid = threadIdx.x;
     if (g.partial && fk == g.nframes - 1) {  // sealed by the generic kernels: copy
         const int64_t si = g.partial - 1, nb = pbytes[si];
         const uint8_t *src = reinterpret_cast<const uint8_t *>(pslots + (size_t)si * P.slot_words);
         for (int64_t i = tid; i < nb; i += 256) dst[i] = src[i];
-        return;
+        continue;
     }
-    const int nwmax = P.nch * kFrameWordsV3 + 16;
-    for (int i = tid; i < nwmax; i += 256) W[i] = 0;
-    wg_load_crc_tables(T);  // (syncs: W is zeroed)
     uint8_t h[16];
     const int hb = mc_frame_header(h, (uint32_t)fk, P.nch, P.sample_rate);
+    int64_t total = 8 * hb;
+    for (int c = 0; c < P.nch; c++) total += max(0, sub_bits[f * P.nch + c]);
+    const int nwz = (int)(((total + 7) >> 3) + 2 + 3) / 4 + 1;  // words of body + CRC-16, one spare
+    for (int i = tid; i < nwz; i += 256) W[i] = 0;
+    __syncthreads();
     if (tid == 0)
         for (int i = 0; i < hb; i++) W[i >> 2] |= (uint32_t)h[i] << (24 - 8 * (i & 3));
-    __syncthreads();
     int64_t o = 8 * hb;
     for (int c = 0; c < P.nch; c++) {
         const int32_t nbits = sub_bits[f * P.nch + c];
         const uint32_t *sw = sub_slots + (size_t)(f * P.nch + c) * kFrameWordsV3;
         const int nw = (nbits + 31) >> 5, sh = (int)(o & 31);
         const int64_t w0 = o >> 5;
-        for (int k = tid; k < nw; k += 256) {
-            const uint32_t v = sw[k];
-            atomicOr(&W[w0 + k], v >> sh);
-            if (sh) atomicOr(&W[w0 + k + 1], v << (32 - sh));
+        const int64_t wl = (o + nbits - 1) >> 5;  // last destination word holding a bit of this subframe
+        // destination word w0 + k (k = 0 .. wl - w0) = (sw[k] >> sh) | (sw[k - 1] << (32 - sh)); the loads of a
+        // thread's (up to) 8 words issue together (one memory latency per 2048 words, not one per word)
+        const int64_t span = nbits > 0 ? wl - w0 : -1;
+        for (int64_t kb = 0; kb <= span; kb += 256 * 8) {
+            uint32_t va[8], vb[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int64_t k = kb + 256 * u + tid;
+                va[u] = (k <= span && k < nw) ? sw[k] : 0u;
+                vb[u] = (k <= span && k > 0 && k - 1 < nw) ? sw[k - 1] : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int64_t k = kb + 256 * u + tid;
+                if (k > span) break;
+                const uint32_t v = (va[u] >> sh) | (sh ? vb[u] << (32 - sh) : 0u);
+                if (k == 0 || k == span) atomicOr(&W[w0 + k], v);
+                else W[w0 + k] = v;
+            }
         }
         o += nbits;
     }
@@ -3229,7 +3259,7 @@ __global__ void __launch_bounds__(256) k_mc_assemble(const EncodeParams P, const
             end = B;
         }
         const int64_t m = B - end;
-        if (c && m > 0) c = gf_mulmod(c, m < kXpowBytes ? (uint32_t)g_xpow_bytes[m] : xpow8((uint64_t)m));
+        if (c && m > 0) c = gf_mulmod(c, xpow_bytes(m));
         for (int d = 32; d > 0; d >>= 1) c ^= __shfl_xor(c, d);
         if ((tid & 63) == 0) wc[tid >> 6] = c;
         __syncthreads();
@@ -3255,6 +3285,7 @@ __global__ void __launch_bounds__(256) k_mc_assemble(const EncodeParams P, const
         dw[k] = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)sh);
     }
     for (int64_t i = hbytes + 4 * nbw + tid; i < S; i += 256) dst[i] = byte_at(i);
+    }
 }
 
 // results of the fast path packed for one D2H copy: tile offsets [ntiles + 1], (dmin, dmax) per tile, error flags
@@ -3323,6 +3354,15 @@ static int upload_tables(frs_ctx *ctx) {
     }
     FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_crc16x8), t4, sizeof(t4), 0, hipMemcpyHostToDevice, ctx->stream));
     FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xpow_bytes), xb, sizeof(xb), 0, hipMemcpyHostToDevice, ctx->stream));
+    static uint16_t x8k[32];
+    uint32_t x8192 = 1;  // x^(8 * 8192)
+    for (int m = 0; m < 8192; m++) x8192 = mulmod(x8192, 0x100);
+    uint32_t q = 1;
+    for (int j = 0; j < 32; j++) {
+        x8k[j] = (uint16_t)q;
+        q = mulmod(q, x8192);
+    }
+    FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_xpow_8k), x8k, sizeof(x8k), 0, hipMemcpyHostToDevice, ctx->stream));
     FRS_HIP(hipStreamSynchronize(ctx->stream));
     g_tables_ready[ctx->device] = true;
     return FRS_OK;
@@ -3629,7 +3669,8 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
             FRS_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mc_assemble),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)mc_lds));
             prof_begin(ctx, "assemble", &ev);
-            k_mc_assemble<<<(unsigned)nframes, 256, mc_lds, st>>>(
+            const int64_t mc_grid = nframes;  // one work-group per frame (the frame loop runs once)
+            k_mc_assemble<<<(unsigned)mc_grid, 256, mc_lds, st>>>(
                 P, dtiles, ctx->frame_tile.as<int32_t>(), dsub, dsbits, ctx->slots.as<uint32_t>(), dpbytes,
                 ctx->frame_off.as<int64_t>(), reinterpret_cast<uint8_t *>(arena_dev));
             prof_end(ctx, "assemble", ev);
