@@ -70,8 +70,9 @@ def main():
     from flac_raster_amd import _native, distributed
 
     rank, world, local_rank = distributed.env_rank_world()
-    ctx = _native.Context(local_rank)
-    comm = distributed.init_comm(ctx, "rccl") if world > 1 else None
+    # one rank per GPU; FRS_COMM_BACKEND=tcp (the host exchange) lets a rehearsal put several ranks on one GPU
+    ctx = _native.Context(local_rank % max(1, _native.device_count()))
+    comm = distributed.init_comm(ctx, os.environ.get("FRS_COMM_BACKEND", "rccl")) if world > 1 else None
 
     T, W, H, B = args.tile, args.width, args.height, args.bands
     tcols, trows = (W + T - 1) // T, (H + T - 1) // T
@@ -175,7 +176,7 @@ def main():
         result["sentinel2"] = sentinel2(ctx)
         result["convert_multiband"] = convert_multiband(ctx)
         result["end_to_end"] = end_to_end(ctx, raster, arena, off, rows, W, T, args)
-    if rank == 0 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu:  # (the CPU baseline is an N = 1 figure)
         result["cpu_baseline"] = cpu_baseline(ctx, raster, rows, W, T, off, arena, args)
     if rank == 0:
         print(json.dumps(result), flush=True)
