@@ -49,8 +49,8 @@ KERNEL_SYMBOL = {"encode": "frs::k_encode_v3<3>", "analyze": "frs::k_analyze_v3<
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--height", type=int, default=40000, help="raster rows (C4: 40000), split over the ranks")
     ap.add_argument("--width", type=int, default=40000)
     ap.add_argument("--bands", type=int, default=4)
