@@ -42,7 +42,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E peak 8.0 TB/s
 VALU_PEAK_GINST_S = 1024 * 2.4 * 0.5
 METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"] if (ROOT / "BASELINE.json").exists() else \
     "Mpixels/sec encode (create-streaming) + bbox-extract ms, 1/2/4/8 GPU; bit-exact vs ref"
-KERNEL_SYMBOL = {"encode": "frs::k_encode_v3<3>", "analyze": "frs::k_analyze_v3<3, false, true>",
+KERNEL_SYMBOL = {"encode": "frs::k_encode_v3<3, false>", "analyze": "frs::k_analyze_v3<3, false, true>",
                  "stats": "frs::k_tile_stats_vec<3>"}
 
 
