@@ -2572,6 +2572,10 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     // the WG's LDS LUT belongs to tile `want`; a frame of another tile takes the exact division instead
     if (t != want && tn.mode == kNormLut) tn.mode = kNormSlow;
     const int16_t *lut = S.lut;
+    // issue priority: phase A (up to the size publish) and the previous frame's look-back + store gate the successors'
+    // look-backs, phase B (packing, CRC) gates nobody until the next frame -- the SIMD's arbiter prefers the former
+    // (encode 3.81 -> 3.65 ms on C4)
+    __builtin_amdgcn_s_setprio(2);
     const int64_t fk = f - g.frame_base;
     const int64_t s0 = fk * kMaxBlock;
     constexpr int n = kMaxBlock;
@@ -2898,6 +2902,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     //      look-back rarely waits; store it and free the bit buffer
     if constexpr (!SUB)
         if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
+    __builtin_amdgcn_s_setprio(0);
     reg_fence(E);
     // ---- phase B: every bit of this frame into the (zeroed) buffer, then the CRC-16
     if (l0 && tab) {
