@@ -2251,6 +2251,9 @@ struct EncV3Shared {
     int want;
     int lut_tile;
 };
+// lut_gather_pairs forms LUT byte addresses mod 2^16: the LUT (the only LDS object of k_encode_v3 is this struct)
+// must end below 64 KiB
+static_assert(offsetof(EncV3Shared, lut) + sizeof(int16_t) * kLutCap <= 65536, "LUT beyond 64 KiB of LDS");
 
 // Bank-aware layout of a wave's frame buffer.  Word w of the frame lives at row (w mod C), column (w / C) of a
 // 64-column matrix, C = ceil(words / 64) <= 34 chosen per frame: phys(w) = (w mod C) * 64 + w / C, so the LDS
@@ -2704,8 +2707,8 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     };
     // 32-bit form of the same search, exact when every lane sum is < 2^24 (group sums < 2^30), for NC candidates
     // at once.  Every lane computes the bits of ITS partition at every order (replicated over the partition's lanes);
-    // an order's total then needs only the butterfly stages at or above its partition width (2 + 3 + 4 + 5 stages for
-    // orders 5..1 instead of a full 6-stage wave sum per order), and the division by a non-first partition's size is
+    // an order's total then needs only the butterfly stages at or above its partition width (5, 4, 3, 2, 1 and 0 stages
+    // for orders 5..0 instead of a full 6-stage wave sum per order), and the division by a non-first partition's size is
     // a shift (the first partition's 2^18 / (n - order) comes from a table); k ? s >> (k-1) : s << 1 == (2s) >> k.
     auto rice32m = [&](auto NCt, const uint32_t *sums, const int *ord, uint32_t *bb, int *bp, int *bk) {
         constexpr int NC = decltype(NCt)::value;
