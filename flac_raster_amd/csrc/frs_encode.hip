@@ -3546,8 +3546,8 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                     ((d->tile_w * es) % 16 == 0) && ((d->width * es) % 16 == 0);
     }
     // Tile stats on the fast path (16-bit samples, 16-B aligned rows, one wave per tile): fused into the analysis
-    // launch (k_analyze_v3<DT, false, true>: min/max, parameters and LUT per wave).  Otherwise (and with
-    // FRS_ABLATE 4096) the stats kernels run before the analysis.
+    // launch (k_analyze_v3<DT, false, true>: min/max, parameters and LUT per wave).  Otherwise the stats kernels
+    // run before the analysis.
     const bool fuse_stats = fast && stats_vec && sizeof(T) == 2 && one_wave_tiles;
     // 1. tile stats
     if (!fuse_stats) {
