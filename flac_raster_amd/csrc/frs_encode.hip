@@ -2419,9 +2419,11 @@ __device__ inline void resolve_and_store(const EncodeParams &P, PendingFrame &pf
                     break;
                 }
                 // back off: polling waves otherwise flood L2 with 64-lane status reads
+                __builtin_amdgcn_s_setprio(0);  // a polling wave yields the arbiter while it sleeps
                 if (spins < 4) __builtin_amdgcn_s_sleep(2);
                 else if (spins < 16) __builtin_amdgcn_s_sleep(8);
                 else __builtin_amdgcn_s_sleep(32);
+                __builtin_amdgcn_s_setprio(2);
                 continue;
             }
             accum += dpp_wave_sum_u64(mine);
