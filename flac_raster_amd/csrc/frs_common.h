@@ -71,6 +71,8 @@ struct EncodeParams {
     int32_t ntiles;
     int32_t norm_mode;    // 0 converter.py:56-86, 1 spatial_encoder.py:229-248
     int32_t vec_ok;       // alignment class of the row segments: 16, 8 or 4 bytes (vector loads), 0 = gather
+    int32_t nvch;         // coded signals per frame: nch, or 4 for a two-channel stream (L, R, mid, side:
+                          // libFLAC's exhaustive mid/side search, stream_encoder.c process_subframes_)
 };
 
 __host__ __device__ inline int ilog2_u32(uint32_t v) { return 31 - __builtin_clz(v); }

@@ -852,10 +852,12 @@ __device__ __attribute__((always_inline)) inline void decode_one_frame(const uin
     BitReader br;  // bits_base[k] = blob[k + bits_shift] (LDS stage or the blob itself)
     br.init(bits_base, fpos + cd.hdr_len - bits_shift, fend_known - bits_shift);
     const int nch = channels;
+    bool combined = false;  // mid/side already undone while the 33-bit side was decoded
     // decode subframes straight into the output (interleaved), then verify the CRC
     for (int c = 0; c < nch; c++) {
         int sbps = cd.bps;
-        if ((cd.chass == 8 && c == 1) || (cd.chass == 9 && c == 0) || (cd.chass == 10 && c == 1)) sbps++;
+        const bool side = (cd.chass == 8 && c == 1) || (cd.chass == 9 && c == 0) || (cd.chass == 10 && c == 1);
+        if (side) sbps++;
         br.bits(1);
         const int t = (int)br.bits(6);
         int w = 0;
@@ -864,6 +866,86 @@ __device__ __attribute__((always_inline)) inline void decode_one_frame(const uin
         if (br.err || sbps <= 0 || sbps > 33) return;
         int32_t *x = outb + c;
         const int bs = cd.bs;
+        if (side && cd.bps == 32) {
+            // The 33-bit side signal of a 32-bit stereo stream: an exact int64 walk (history ring of the last 32
+            // samples).  Left-/right-side keep its low 32 bits (the other channel is L - S / R + S mod 2^32);
+            // mid-side needs all 33, so L and R are formed here and the post-pass skips the frame.
+            int64_t hist[32];
+            auto rd = [&](int nb) -> int64_t {  // signed field of nb <= 33 bits
+                if (nb <= 32) return (int64_t)br.sbits(nb);
+                const uint64_t hi = br.bits(nb - 32), lo = br.bits(32);
+                const uint64_t v = (hi << 32) | lo;
+                return (int64_t)(v << (64 - nb)) >> (64 - nb);
+            };
+            auto put = [&](int i, int64_t v) {
+                hist[i & 31] = v;
+                const int64_t sd = (int64_t)((uint64_t)v << w);
+                int32_t *pr = outb + (int64_t)i * nch;
+                if (cd.chass == 10) {
+                    const int64_t mid = (int64_t)((uint64_t)(int64_t)pr[0] << 1) | (sd & 1);
+                    pr[0] = (int32_t)((mid + sd) >> 1);
+                    pr[1] = (int32_t)((mid - sd) >> 1);
+                } else {
+                    x[(int64_t)i * nch] = (int32_t)sd;
+                }
+            };
+            if (t == 0) {
+                const int64_t v = rd(sbps);
+                for (int i = 0; i < bs; i++) put(i, v);
+            } else if (t == 1) {
+                for (int i = 0; i < bs; i++) put(i, rd(sbps));
+            } else if ((t >= 8 && t <= 12) || t >= 32) {
+                const bool lpc = t >= 32;
+                const int o = lpc ? t - 31 : t - 8;
+                if (o > bs) return;
+                int32_t q[32];
+                int shift = 0;
+                for (int i = 0; i < o; i++) put(i, rd(sbps));
+                if (lpc) {
+                    const int prec = (int)br.bits(4) + 1;
+                    if (prec == 16) return;
+                    shift = br.sbits(5);
+                    if (shift < 0) return;
+                    for (int i = 0; i < o; i++) q[i] = br.sbits(prec);
+                }
+                const int method = (int)br.bits(2);
+                if (method > 1) return;
+                const int po = (int)br.bits(4);
+                const int pb = method == 0 ? 4 : 5, esc = (1 << pb) - 1;
+                if ((bs >> po) < o || (bs & ((1 << po) - 1))) return;
+                int i = o;
+                for (int p = 0; p < (1 << po); p++) {
+                    const int ns = (bs >> po) - (p == 0 ? o : 0);
+                    const int kp = (int)br.bits(pb);
+                    const int nb = kp == esc ? (int)br.bits(5) : 0;
+                    for (int j = 0; j < ns; j++, i++) {
+                        int64_t r;
+                        if (kp == esc) r = nb ? (int64_t)br.sbits(nb) : 0;
+                        else {
+                            const uint32_t qq = br.unary();
+                            const uint32_t u = (qq << kp) | br.bits(kp);
+                            r = (int32_t)((u >> 1) ^ (uint32_t)(-(int32_t)(u & 1)));
+                        }
+                        int64_t pred = 0;
+                        if (lpc) {
+                            for (int m = 0; m < o; m++) pred += (int64_t)q[m] * hist[(i - 1 - m) & 31];
+                            pred >>= shift;
+                        } else {
+                            const int64_t a = o > 0 ? hist[(i - 1) & 31] : 0, b = o > 1 ? hist[(i - 2) & 31] : 0,
+                                          d = o > 2 ? hist[(i - 3) & 31] : 0, e = o > 3 ? hist[(i - 4) & 31] : 0;
+                            pred = o == 1 ? a : o == 2 ? 2 * a - b : o == 3 ? 3 * a - 3 * b + d
+                                 : o == 4 ? 4 * a - 6 * b + 4 * d - e : 0;
+                        }
+                        put(i, r + pred);
+                        if (br.err) return;
+                    }
+                }
+            } else {
+                return;
+            }
+            if (cd.chass == 10) combined = true;
+            continue;
+        }
         if (t == 0) {
             const int32_t v = br.sbits(sbps);
             for (int i = 0; i < bs; i++) x[(int64_t)i * nch] = v;
@@ -1052,7 +1134,7 @@ __device__ __attribute__((always_inline)) inline void decode_one_frame(const uin
         if (w)
             for (int i = 0; i < bs; i++) x[(int64_t)i * nch] = (int32_t)((uint32_t)x[(int64_t)i * nch] << w);
     }
-    if (cd.chass >= 8) {
+    if (cd.chass >= 8 && !combined) {
         for (int i = 0; i < cd.bs; i++) {
             int32_t *pr = outb + (int64_t)i * nch;
             const int64_t a = pr[0], sd = pr[1];
@@ -1800,8 +1882,11 @@ struct LaneReader {
 
 // Channel-planar int32 PCM of the multi-channel lane decoder -> the interleaved output (de-normalised when fused,
 // int32 PCM otherwise): one thread per output element, elements in output order (coalesced stores).
+// Two-channel streams (fchass != nullptr): the frame's channel assignment (written by the lane decoder) undoes
+// libFLAC's stereo decorrelation here -- left-side R = L - S, right-side L = R + S, mid-side from (M << 1 | S & 1).
 __global__ void __launch_bounds__(256) k_interleave_dn(const int32_t *planar, const int64_t *poff, const int64_t *fbase,
-                                                      int ns, int nch, int blocksize, int32_t *pcm, DecOut dout) {
+                                                      int ns, int nch, int blocksize, int32_t *pcm, DecOut dout,
+                                                      const int8_t *fchass) {
     const int64_t total = (poff[ns] - poff[0]) * nch;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t g = poff[0] + e / nch;  // sample index
@@ -1814,7 +1899,20 @@ __global__ void __launch_bounds__(256) k_interleave_dn(const int32_t *planar, co
         }
         const int64_t i = g - poff[lo];
         const int64_t fi = fbase[lo] + i / blocksize;
-        const int32_t x = planar[(fi * nch + c) * (int64_t)blocksize + (i % blocksize)];
+        int32_t x = planar[(fi * nch + c) * (int64_t)blocksize + (i % blocksize)];
+        if (fchass) {
+            const int ca = fchass[fi];
+            if (ca >= 8) {
+                const int64_t a = planar[(fi * 2) * (int64_t)blocksize + (i % blocksize)];
+                const int64_t sd = planar[(fi * 2 + 1) * (int64_t)blocksize + (i % blocksize)];
+                if (ca == 8) x = c == 0 ? (int32_t)a : (int32_t)(a - sd);
+                else if (ca == 9) x = c == 0 ? (int32_t)(a + sd) : (int32_t)sd;
+                else {
+                    const int64_t mid = (a * 2) | (sd & 1);
+                    x = (int32_t)(c == 0 ? (mid + sd) >> 1 : (mid - sd) >> 1);
+                }
+            }
+        }
         if (dout.out) dn_store(dout, g * nch + c, x, dout.dn[lo]);
         else pcm[g * nch + c] = x;
     }
@@ -1837,9 +1935,10 @@ __device__ inline uint32_t dn_bits_t(const DecOut &o, int32_t pcm, float2 p) {
     }
 }
 
-// MC (multi-channel streams of >= 3 independent channels): the lane walks the frame's subframes in turn and writes
-// them channel-planar as int32 PCM to `planar` (frame fi, channel c at (fi * nch + c) * blocksize); k_interleave_dn
-// then interleaves and de-normalises.
+// MC (multi-channel streams of >= 3 independent channels, and two-channel streams in any of the four assignments):
+// the lane walks the frame's subframes in turn and writes them channel-planar as int32 PCM to `planar` (frame fi,
+// channel c at (fi * nch + c) * blocksize); k_interleave_dn then interleaves (undoing the stereo decorrelation
+// by fchass[fi]) and de-normalises.
 template <int OUT, bool MC = false>
 __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob, const int64_t *soff, int ns,
                                                            const int64_t *poff, const int64_t *cpos,
@@ -1847,7 +1946,8 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
                                                            const int64_t *frame_cand, int64_t nframes,
                                                            int stream_bps, int32_t *pcm, int blocksize, int *nvalid,
                                                            DecOut dout, int32_t *fb_list, int *fb_count,
-                                                           int nch = 1, int32_t *planar = nullptr) {
+                                                           int nch = 1, int32_t *planar = nullptr,
+                                                           int8_t *fchass = nullptr) {
     static_assert(!MC || OUT == kOutPcm, "channel-planar int32 output");
     constexpr int es = OUT == kOutPcm ? 4 : OUT == kOutU8 ? 1 : 2;  // kOutAny: per-sample dn_store
     const int64_t fi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1865,7 +1965,9 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
             const int64_t kk = fi - fbase[s];
             const int64_t first = kk * blocksize;
             const FrameHdr cd = parse_header(blob, fpos, send, MC ? nch : 1, stream_bps);
-            bool take_all = !MC || cd.chass == nch - 1;  // independent channels only (no stereo decorrelation)
+            // independent channels, or a two-channel frame in any assignment (k_interleave_dn undoes it)
+            bool take_all = !MC || cd.chass == nch - 1 || (nch == 2 && cd.chass >= 8 && cd.chass <= 10);
+            if (MC && fchass && cd.ok) fchass[fi] = (int8_t)cd.chass;
             if (cd.ok && cd.frame_no == kk && cd.bs <= blocksize && first + cd.bs <= nsamp && take_all) {
                 const int bs = cd.bs;
                 const float2 dnp = OUT != kOutPcm ? dout.dn[s] : make_float2(0.f, 0.f);
@@ -1877,9 +1979,12 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
                 const int t = (int)br.bits(6);
                 int w = 0;
                 if (br.bits(1)) w = (int)br.unary() + 1;
-                const int sbps = cd.bps - w;
-                int o = 0, shift = 0, prec = 3;
-                bool take = cd.bps <= 16 && sbps > 0 && sbps <= 16;
+                // the side signal of a two-channel frame carries one extra bit
+                const bool side = MC && nch == 2 &&
+                                  ((cd.chass == 8 && chn == 1) || (cd.chass == 9 && chn == 0) || (cd.chass == 10 && chn == 1));
+                const int sbps = cd.bps - w + (side ? 1 : 0);
+                int o = 0, shift = 0;
+                bool take = cd.bps <= 16 && sbps > 0 && sbps <= 17;
                 const bool raw = t == 1;  // VERBATIM: order 0, raw residuals
                 if (t >= 8 && t <= 12) o = t - 8;
                 else if (t >= 32 && t <= 39) o = t - 31;
@@ -1896,7 +2001,7 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
                 for (int m = 0; m < 8; m++)
                     if (take && m < o) R[m] = br.sbits(sbps);  // warm-up: ring slot m = sample m
                 if (take && t >= 32) {
-                    prec = (int)br.bits(4) + 1;
+                    const int prec = (int)br.bits(4) + 1;
                     shift = br.sbits(5);
                     if (prec == 16 || shift < 0) take = false;
 #pragma unroll
@@ -1908,9 +2013,11 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
                     cq[2] = o == 3 ? 1 : o == 4 ? 4 : 0;
                     cq[3] = o == 4 ? -1 : 0;
                 }
-                int lg = 0;
-                while ((1 << lg) < o) lg++;
-                if (!(prec + sbps + lg <= 31)) take = false;
+                // 32-bit prediction (__mul24 taps): |sum q.x| <= sum|q| 2^(sbps-1) must stay below 2^31
+                uint32_t sumq = 0;
+#pragma unroll
+                for (int m = 0; m < 8; m++) sumq += (uint32_t)abs(cq[m]);
+                if ((32 - __builtin_clz(sumq | 1u)) + sbps - 1 > 31) take = false;
                 int pb = 4, esc = 15, psz = bs, part_end = bs, k = 0;
                 if (take && t >= 8) {
                     const int method = (int)br.bits(2);
@@ -2089,7 +2196,7 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     if (ctx->decode_lane >= 0) lane = pipe && ctx->decode_lane == 1;
     // multi-channel streams (>= 3 independent channels, 16-bit): the lane decoder walks each frame's subframes into a
     // channel-planar int32 scratch, k_interleave_dn interleaves (and de-normalises); the wave decoder takes the rest
-    const bool mcl = channels >= 3 && channels <= 8 && bps <= 16 && blocksize <= kDecResMax && !ctx->force_generic &&
+    const bool mcl = channels >= 2 && channels <= 8 && bps <= 16 && blocksize <= kDecResMax && !ctx->force_generic &&
                      frames >= 64 && ctx->decode_lane != 0;
     const int64_t nsamp_all = pcm_off[nstreams] - pcm_off[0];
     const int64_t planar_words = mcl ? frames * channels * (int64_t)blocksize : 0;
@@ -2117,11 +2224,18 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         FRS_HIP(hipMemsetAsync(ctx->dec_count.ptr, 0, ctx->dec_count.bytes, st));
     }
     {
-        void *before = ctx->dec_status.ptr;
+        // a grown buffer may come back at the same address with stale words (possibly of the current epoch), and an
+        // epoch that wraps could match an old word: zero the status words in both cases
+        const size_t before = ctx->dec_status.bytes;
         FRS_HIP(ctx->dec_status.ensure(sizeof(uint64_t) * (size_t)std::min<int64_t>(nblocks, kSelOnePassBlocks)));
-        if (ctx->dec_status.ptr != before) FRS_HIP(hipMemsetAsync(ctx->dec_status.ptr, 0, ctx->dec_status.bytes, st));
+        bool wrap = false;
+        if (++ctx->dec_epoch >= (1u << 24)) {
+            ctx->dec_epoch = 1;
+            wrap = true;
+        }
+        if (ctx->dec_status.bytes != before || wrap)
+            FRS_HIP(hipMemsetAsync(ctx->dec_status.ptr, 0, ctx->dec_status.bytes, st));
     }
-    if (++ctx->dec_epoch >= (1u << 24)) ctx->dec_epoch = 1;
     // per-call tables through the context's pinned staging in one DMA copy: stream_off | fbase | pcm_off | the
     // fused decode's per-stream (float32(max - min), float32(min)) pairs; the result counters come back after them
     const size_t tab = sizeof(int64_t) * (size_t)(nstreams + 1);
@@ -2215,11 +2329,16 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         int32_t *fbl = ctx->dec_fb.as<int32_t>();
         int *fbc = ncand + 3;
         int32_t *planar = ctx->dec_pcm.as<int32_t>();
+        int8_t *fchass = nullptr;
+        if (channels == 2) {
+            FRS_HIP(ctx->dec_chass.ensure((size_t)frames + 64));
+            fchass = ctx->dec_chass.as<int8_t>();
+        }
         k_decode_frames_lane<kOutPcm, true><<<(unsigned)((frames + 255) / 256), 256, 0, st>>>(
             blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, dchain, frames, bps, pcm_dev, blocksize, nvalid, dout,
-            fbl, fbc, channels, planar);
+            fbl, fbc, channels, planar, fchass);
         k_interleave_dn<<<(unsigned)std::min<int64_t>((nsamp_all * channels + 255) / 256, 16 * (int64_t)ctx->num_cus),
-                          256, 0, st>>>(planar, dpoff, dfbase, nstreams, channels, blocksize, pcm_dev, dout);
+                          256, 0, st>>>(planar, dpoff, dfbase, nstreams, channels, blocksize, pcm_dev, dout, fchass);
         k_decode_frames_wave_list<<<(unsigned)std::min<int64_t>(frames, 4 * (int64_t)ctx->num_cus), 64, 0, st>>>(
             blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, dchain, channels, bps, pcm_dev, blocksize, nvalid,
             dout, fbl, fbc);

@@ -353,16 +353,17 @@ __device__ inline double expected_bits(double lpc_error, double error_scale) {
 // wasted bits, constant test, fixed-predictor guess (fixed.c, totals over samples 4..n-1), LPC order by expected
 // bits, Levinson coefficients and their quantisation (lpc.c).  acc = windowed autocorrelation lags 0..8, t = fixed
 // totals of orders 0..4, or_acc = OR of the samples, diff = OR of (x ^ x[0]).
+// extra = 1 for the side signal of a two-channel stream (subframe_bps_mid_side[1] = bps - wasted + 1).
 template <bool WIDE>
-__device__ inline SubAnalysis generic_decide(const double *acc, const uint64_t *tt, uint32_t or_acc, uint32_t diff,
-                                             int n, const EncodeParams &P) {
+__device__ inline SubAnalysis generic_decide(const double *acc, const uint64_t *tt, uint64_t or_acc, uint64_t diff,
+                                             int n, const EncodeParams &P, int extra = 0) {
     const uint64_t t0 = tt[0], t1 = tt[1], t2 = tt[2], t3 = tt[3], t4 = tt[4];
     SubAnalysis A;
     A.n = n;
     int w = 0;
-    if (or_acc) w = __builtin_ctz(or_acc);
+    if (or_acc) w = __builtin_ctzll(or_acc);
     if (w > P.bps) w = P.bps;
-    const int sbps = P.bps - w;
+    const int sbps = P.bps - w + extra;
     A.wasted = w;
     A.flags = 0;
     A.fixed_order = 0;
@@ -504,20 +505,40 @@ __device__ inline SubAnalysis generic_decide(const double *acc, const uint64_t *
     return A;
 }
 
-template <int DT, bool WIDE>
+// Coded signal v of a frame at sample pointer p (band0's pixel): channel v when the stream is coded independently;
+// for a two-channel stream's mid/side pass (ST) v = 0 left, 1 right, 2 mid = (L + R) >> 1, 3 side = L - R (one bit
+// wider; 33 bits for a 32-bit stream: integer_signal_33bit_side), as FLAC__stream_encoder_process_interleaved
+// forms them from the unshifted samples.
+template <int DT, bool ST, typename XT>
+__device__ inline XT coded_sample(const typename Elem<DT>::T *p, int64_t band_stride, const Normalizer<DT> &nz,
+                                  int v) {
+    if constexpr (!ST) {
+        return (XT)nz(p[(int64_t)v * band_stride]);
+    } else {
+        if (v < 2) return (XT)nz(p[(int64_t)v * band_stride]);
+        const int64_t a = nz(p[0]), b = nz(p[band_stride]);
+        return v == 2 ? (XT)((a + b) >> 1) : (XT)(a - b);
+    }
+}
+
+template <int DT, bool WIDE, bool ST = false>
 __global__ void __launch_bounds__(128) k_analyze(const typename Elem<DT>::T *raster, EncodeParams P,
                                                 const TileGeom *tiles, const TileNorm *norms,
                                                 const float *__restrict__ window, SubAnalysis *out,
                                                 const int64_t *__restrict__ flist, int64_t nlist) {
-    // flist: the frames to analyse (the fast path's partial last frames), nullptr = every frame of the job
+    // flist: the frames to analyse (the fast path's partial last frames), nullptr = every frame of the job.
+    // One lane per coded signal: (frame, channel), or (frame, L/R/M/S) for a two-channel stream (ST).
     using T = typename Elem<DT>::T;
+    // sample type: 32 bits except the 33-bit side signal of a 32-bit stereo stream
+    using XA = std::conditional_t<ST && WIDE, int64_t, int32_t>;
+    using UA = std::make_unsigned_t<XA>;
     const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t nsub = (flist ? nlist : P.nframes) * P.nch;
+    const int64_t nsub = (flist ? nlist : P.nframes) * P.nvch;
     const bool live = li < nsub;
-    const int64_t fi = live ? li / P.nch : 0;
-    const int ch = live ? (int)(li - fi * P.nch) : 0;
+    const int64_t fi = live ? li / P.nvch : 0;
+    const int ch = live ? (int)(li - fi * P.nvch) : 0;
     const int64_t f = flist ? flist[fi] : fi;
-    const int64_t sub = f * P.nch + ch;
+    const int64_t sub = f * P.nvch + ch;
     const int t = tile_of_frame(tiles, P.ntiles, f);
     const TileGeom g = tiles[t];
     const int64_t s0 = (f - g.frame_base) * P.blocksize;
@@ -527,10 +548,11 @@ __global__ void __launch_bounds__(128) k_analyze(const typename Elem<DT>::T *ras
 
     int64_t row = s0 / g.w;
     int col = (int)(s0 - row * g.w);
-    const T *rowp = raster + (int64_t)(P.band0 + ch) * P.band_stride + (g.r0 + row) * P.row_stride + g.c0;
+    const T *rowp = raster + (int64_t)(P.band0 + (ST ? 0 : ch)) * P.band_stride + (g.r0 + row) * P.row_stride + g.c0;
 
-    uint32_t or_acc = 0, diff = 0;
-    int32_t x0 = 0, x1 = 0, p1 = 0, p2 = 0, p3 = 0;
+    UA or_acc = 0, diff = 0;
+    XA x0 = 0;
+    int32_t x1 = 0, p1 = 0, p2 = 0, p3 = 0;
     uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
     double acc[kMaxLpc + 1];
 #pragma unroll
@@ -552,21 +574,34 @@ __global__ void __launch_bounds__(128) k_analyze(const typename Elem<DT>::T *ras
         }
         return v;
     };
-    auto block8 = [&](int i0, const T *raw) {
+    // coded sample i (< n) of a stereo lane at the row cursor, which then advances
+    auto fetch_st = [&](int i) -> XA {
+        XA v = 0;
+        if (i < n) {
+            v = coded_sample<DT, true, XA>(rowp + col, P.band_stride, nz, ch);
+            if (++col == g.w) {
+                col = 0;
+                rowp += P.row_stride;
+            }
+        }
+        return v;
+    };
+    auto block8 = [&](int i0, const XA *xin) {
 #pragma unroll
         for (int j = 0; j < 8; j++) {
             const int i = i0 + j;
-            int32_t x = 0;
+            XA x = 0;
             if (i < n) {
-                x = nz(raw[j]);
+                x = xin[j];
                 if (i == 0) x0 = x;
-                or_acc |= (uint32_t)x;
-                diff |= (uint32_t)(x ^ x0);
+                or_acc |= (UA)x;
+                diff |= (UA)(x ^ x0);
                 if constexpr (!WIDE) {
-                    // 16-bit streams: |e_k| < 2^20, totals over samples 4..n-1 (fixed.c, data+4)
-                    const int32_t e1 = x - x1, e2 = e1 - p1, e3 = e2 - p2, e4 = e3 - p3;
+                    // 16-bit streams: |e_k| < 2^21 (17-bit side), totals over samples 4..n-1 (fixed.c, data+4)
+                    const int32_t xs = (int32_t)x;
+                    const int32_t e1 = xs - x1, e2 = e1 - p1, e3 = e2 - p2, e4 = e3 - p3;
                     if (i >= 4) {
-                        t0 += (uint32_t)abs(x);
+                        t0 += (uint32_t)abs(xs);
                         t1 += (uint32_t)abs(e1);
                         t2 += (uint32_t)abs(e2);
                         t3 += (uint32_t)abs(e3);
@@ -575,7 +610,7 @@ __global__ void __launch_bounds__(128) k_analyze(const typename Elem<DT>::T *ras
                     p3 = e3;
                     p2 = e2;
                     p1 = e1;
-                    x1 = x;
+                    x1 = xs;
                 }
             }
             // inactive lanes have x == 0 -> contribute exact zeros; window index is wave-uniform
@@ -593,15 +628,23 @@ __global__ void __launch_bounds__(128) k_analyze(const typename Elem<DT>::T *ras
         for (int j = 0; j < 8; j++) prev[j] = cur[j];
     };
     for (int i0 = 0; i0 < nloop; i0 += 8) {
-        T raw[8];
+        XA xin[8];
+        if constexpr (ST) {
 #pragma unroll
-        for (int j = 0; j < 8; j++) raw[j] = fetch(i0 + j);
-        block8(i0, raw);
+            for (int j = 0; j < 8; j++) xin[j] = fetch_st(i0 + j);
+        } else {
+            T raw[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) raw[j] = fetch(i0 + j);
+#pragma unroll
+            for (int j = 0; j < 8; j++) xin[j] = (i0 + j < n) ? (XA)nz(raw[j]) : (XA)0;
+        }
+        block8(i0, xin);
     }
     if (!live) return;
 
     const uint64_t tt[5] = {t0, t1, t2, t3, t4};
-    out[sub] = generic_decide<WIDE>(acc, tt, or_acc, diff, n, P);
+    out[sub] = generic_decide<WIDE>(acc, tt, (uint64_t)or_acc, (uint64_t)diff, n, P, (ST && ch == 3) ? 1 : 0);
 }
 
 // The fast path's partial last frames (n < blocksize, at most one per tile, 16-bit mono streams): one work-group per
@@ -689,15 +732,17 @@ __global__ void __launch_bounds__(kPartThreads) k_analyze_partial(const typename
 
 // 32-bit streams (bits_per_sample 24 -> pyflac bps 32) use libFLAC's limit_residual fixed estimator;
 // it needs 64-bit errors and validity tracking, done in a separate exact pass per lane.
-template <int DT>
+template <int DT, bool ST = false>
 __global__ void __launch_bounds__(128) k_analyze_fixed_wide(const typename Elem<DT>::T *raster, EncodeParams P,
                                                            const TileGeom *tiles, const TileNorm *norms,
                                                            SubAnalysis *out) {
+    // ST: two-channel stream, lanes per (frame, L/R/M/S); the side signal has 33 bits
+    // (FLAC__fixed_compute_best_predictor_limit_residual_33bit: the same arithmetic on int64 samples)
     using T = typename Elem<DT>::T;
     const int64_t sub = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (sub >= P.nframes * P.nch) return;
-    const int64_t f = sub / P.nch;
-    const int ch = (int)(sub - f * P.nch);
+    if (sub >= P.nframes * P.nvch) return;
+    const int64_t f = sub / P.nvch;
+    const int ch = (int)(sub - f * P.nvch);
     const int t = tile_of_frame(tiles, P.ntiles, f);
     const TileGeom g = tiles[t];
     const int64_t s0 = (f - g.frame_base) * P.blocksize;
@@ -707,19 +752,24 @@ __global__ void __launch_bounds__(128) k_analyze_fixed_wide(const typename Elem<
     SubAnalysis A = out[sub];
     if (n <= 4) return;
     const int w = A.wasted;
-    const int sbps = P.bps - w;
+    const int sbps = P.bps - w + ((ST && ch == 3) ? 1 : 0);
     int64_t row = s0 / g.w;
     int col = (int)(s0 - row * g.w);
-    const T *rowp = raster + (int64_t)(P.band0 + ch) * P.band_stride + (g.r0 + row) * P.row_stride + g.c0;
-    int64_t h1 = 0, h2 = 0, h3 = 0, h4 = 0;
-    uint64_t tt[5] = {0, 0, 0, 0, 0};
-    bool valid[5] = {true, true, true, true, true};
-    for (int i = 0; i < n; i++) {
-        const int64_t x = (int64_t)(nz(rowp[col]) >> w);
+    const T *const tbase = raster + (int64_t)(P.band0 + (ST ? 0 : ch)) * P.band_stride;
+    const T *rowp = tbase + (g.r0 + row) * P.row_stride + g.c0;
+    auto next = [&]() -> int64_t {
+        const int64_t x = coded_sample<DT, ST, int64_t>(rowp + col, P.band_stride, nz, ST ? ch : 0);
         if (++col == g.w) {
             col = 0;
             rowp += P.row_stride;
         }
+        return x;
+    };
+    int64_t h1 = 0, h2 = 0, h3 = 0, h4 = 0;
+    uint64_t tt[5] = {0, 0, 0, 0, 0};
+    bool valid[5] = {true, true, true, true, true};
+    for (int i = 0; i < n; i++) {
+        const int64_t x = next() >> w;
         uint64_t e[5];
         e[0] = (uint64_t)(x < 0 ? -x : x);
         int64_t v;
@@ -762,15 +812,11 @@ __global__ void __launch_bounds__(128) k_analyze_fixed_wide(const typename Elem<
         // all samples equal?  (rare; re-walk)
         row = s0 / g.w;
         col = (int)(s0 - row * g.w);
-        rowp = raster + (int64_t)(P.band0 + ch) * P.band_stride + (g.r0 + row) * P.row_stride + g.c0;
-        int32_t first = 0;
+        rowp = tbase + (g.r0 + row) * P.row_stride + g.c0;
+        int64_t first = 0;
         constant = true;
         for (int i = 0; i < n; i++) {
-            int32_t x = nz(rowp[col]);
-            if (++col == g.w) {
-                col = 0;
-                rowp += P.row_stride;
-            }
+            const int64_t x = next();
             if (i == 0) first = x;
             else if (x != first) {
                 constant = false;
@@ -884,22 +930,42 @@ __device__ inline void put_bits(uint32_t *buf, uint64_t pos, uint32_t val, int n
 
 __device__ inline uint32_t mask_bits(int64_t v, int n) { return n >= 32 ? (uint32_t)v : (uint32_t)v & ((1u << n) - 1u); }
 
+// a signed sample of nbits <= 33 bits (the 33-bit side signal of a 32-bit stereo stream goes out as 1 + 32 bits)
+__device__ inline void put_sample(uint32_t *buf, uint64_t pos, int64_t v, int nbits) {
+    if (nbits > 32) {
+        put_bits(buf, pos, (uint32_t)(v >> 32) & ((1u << (nbits - 32)) - 1u), nbits - 32);
+        put_bits(buf, pos + (uint64_t)(nbits - 32), (uint32_t)v, 32);
+    } else {
+        put_bits(buf, pos, mask_bits(v, nbits), nbits);
+    }
+}
+
 // LDS index of sample i in EncShared::xs: one pad word per 16 samples, so the 256 threads' contiguous 16-sample
 // chunks start in distinct banks (unpadded, thread t's chunk starts at bank 16 t mod 32: 16-way conflicts)
 __device__ inline int xsi(int i) { return i + (i >> 4); }
 
-struct EncShared {
-    int32_t xs[kMaxBlock + kMaxBlock / 16];
-    uint32_t bits[kBitWords];
+// XT = int64_t only for the 33-bit side signal of a 32-bit stereo stream (a VERBATIM 33-bit subframe is 4224 words)
+template <typename XT> struct EncShared {
+    static constexpr int kWords = sizeof(XT) == 8 ? 4096 + 192 : kBitWords;
+    XT xs[kMaxBlock + kMaxBlock / 16];
+    uint32_t bits[kWords];
     uint64_t psum[2][32];
-    uint32_t scan[kEncThreads];
     RiceChoice rc[2];
     int lpc_bad;
-    int choice;        // subframe type: 0 const, 1 verbatim, 2 fixed, 3 lpc
-    uint32_t est[4];
+    int choice;          // subframe type: 0 const, 1 verbatim, 2 fixed, 3 lpc
+    uint32_t best;       // its estimated bits (process_subframe_'s best_bits)
+    // two-channel streams: the decisions of L, R, mid, side and the chosen channel assignment
+    int vtype[4];
+    uint32_t vbits[4];
+    RiceChoice vrc[4];
+    int assign;          // FLAC__ChannelAssignment: 0 independent, 1 left-side, 2 right-side, 3 mid-side
 };
 
-template <int DT>
+// workgroup = frame.  ST: a two-channel stream -- the four signals L, R, M, S are evaluated (process_subframe_ each),
+// the assignment with the fewest estimated bits wins (stream_encoder.c process_subframes_, do_mid_side_stereo &&
+// !loose: independent, left-side, right-side, mid-side; a later one only if strictly smaller) and its two subframes
+// are written.
+template <int DT, bool ST = false, typename XT = int32_t>
 __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename Elem<DT>::T *raster, EncodeParams P,
                                                              const TileGeom *tiles, const TileNorm *norms,
                                                              const SubAnalysis *ana, uint32_t *slots,
@@ -908,7 +974,9 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
     // flist: frames to code (the fast path's partial last frames; slot / frame_bytes indexed by list position),
     // nullptr = frame blockIdx.x
     using T = typename Elem<DT>::T;
-    __shared__ EncShared S;
+    using Sh = EncShared<XT>;
+    constexpr int kWords = Sh::kWords;
+    __shared__ Sh S;
     const int tid = threadIdx.x;
     const int64_t si = blockIdx.x;
     const int64_t f = flist ? flist[si] : si;
@@ -922,9 +990,142 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
     uint32_t *slot = slots + (size_t)si * P.slot_words;
     const int rice_limit = P.bps > 16 ? 31 : 15;
     const int max_po_block = min(kMaxPartOrder, __builtin_ctz((unsigned)n));
+    const int chunk = (n + kEncThreads - 1) / kEncThreads;
+    const int i_beg = tid * chunk, i_end = min(n, i_beg + chunk);
 
-    for (int i = tid; i < kBitWords; i += kEncThreads) S.bits[i] = 0;
+    for (int i = tid; i < kWords; i += kEncThreads) S.bits[i] = 0;
     __syncthreads();
+
+    // ---- coded signal v (wasted bits w shifted out) into LDS, strided over threads: coalesced row segments
+    auto load = [&](int v, int w) {
+        const T *base = raster + (int64_t)(P.band0 + (ST ? 0 : v)) * P.band_stride + g.r0 * P.row_stride + g.c0;
+        for (int i = tid; i < n; i += kEncThreads) {
+            const int64_t p = s0 + i;
+            const int64_t r = p / g.w;
+            const int cc = (int)(p - r * g.w);
+            S.xs[xsi(i)] = coded_sample<DT, ST, XT>(base + r * P.row_stride + cc, P.band_stride, nz, ST ? v : 0) >> w;
+        }
+        if (tid < 64) S.psum[tid >> 5][tid & 31] = 0;
+        if (tid == 0) S.lpc_bad = 0;
+        __syncthreads();
+    };
+    // residual i of the FIXED (fixed == true) or LPC predictor of order o
+    auto resid = [&](const SubAnalysis &A, bool fixed, int o, int i) -> int64_t {
+        int64_t r;
+        if (fixed) {
+            const int64_t x = S.xs[xsi(i)];
+            switch (o) {
+            case 0: r = x; break;
+            case 1: r = x - S.xs[xsi(i - 1)]; break;
+            case 2: r = x - 2 * (int64_t)S.xs[xsi(i - 1)] + S.xs[xsi(i - 2)]; break;
+            case 3: r = x - 3 * (int64_t)S.xs[xsi(i - 1)] + 3 * (int64_t)S.xs[xsi(i - 2)] - S.xs[xsi(i - 3)]; break;
+            default: r = x - 4 * (int64_t)S.xs[xsi(i - 1)] + 6 * (int64_t)S.xs[xsi(i - 2)] - 4 * (int64_t)S.xs[xsi(i - 3)] + S.xs[xsi(i - 4)]; break;
+            }
+        } else {
+            int64_t s = 0;
+            for (int j = 0; j < o; j++) s += (int64_t)A.q[j] * S.xs[xsi(i - 1 - j)];
+            r = (int64_t)S.xs[xsi(i)] - (s >> A.lpc_shift);
+        }
+        return r;
+    };
+    auto max_po_for = [&](int o) {
+        int m = max_po_block;
+        while (m > 0 && (n >> m) <= o) m--;
+        return m;
+    };
+    // ---- process_subframe_: candidate partition sums, Rice search, choice (VERBATIM, CONSTANT | FIXED, LPC; strict <)
+    //      -> S.choice, S.best, S.rc
+    auto decide = [&](const SubAnalysis &A, int extra) {
+        const int w = A.wasted;
+        const int sbps = P.bps - w + extra;
+        const bool cand_fixed = n > 4 && !(A.flags & kFlagConstant) && (A.flags & kFlagFixedOk);
+        const bool cand_lpc = n > 4 && !(A.flags & kFlagConstant) && (A.flags & kFlagLpcOk);
+        const int mpo[2] = {max_po_for(A.fixed_order), max_po_for(A.lpc_order)};
+        for (int cand = 0; cand < 2; cand++) {
+            if (cand == 0 && !cand_fixed) continue;
+            if (cand == 1 && !cand_lpc) continue;
+            const int o = cand == 0 ? A.fixed_order : A.lpc_order;
+            const int ps = n >> mpo[cand];
+            int cur_p = -1;
+            uint64_t acc = 0;
+            for (int i = max(i_beg, o); i < i_end; i++) {
+                int64_t r = resid(A, cand == 0, o, i);
+                if (cand == 0) r = (int32_t)r;  // libFLAC stores fixed residuals as int32
+                else if (r <= INT32_MIN || r > INT32_MAX) S.lpc_bad = 1;
+                const int p = i / ps;
+                if (p != cur_p) {
+                    if (cur_p >= 0) atomicAdd((unsigned long long *)&S.psum[cand][cur_p], (unsigned long long)acc);
+                    cur_p = p;
+                    acc = 0;
+                }
+                acc += (uint64_t)(r < 0 ? -r : r);
+            }
+            if (cur_p >= 0) atomicAdd((unsigned long long *)&S.psum[cand][cur_p], (unsigned long long)acc);
+        }
+        __syncthreads();
+        if (tid == 0 || tid == 64) {
+            const int cand = tid == 0 ? 0 : 1;
+            const bool on = cand == 0 ? cand_fixed : (cand_lpc && !S.lpc_bad);
+            if (on) rice_search(S.psum[cand], mpo[cand], n, cand == 0 ? A.fixed_order : A.lpc_order, rice_limit, &S.rc[cand]);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t best = (uint32_t)(1 + 6 + 1 + w + n * sbps);
+            int type = 1;
+            if (n > 4) {
+                if (A.flags & kFlagConstant) {
+                    const uint32_t cb = (uint32_t)(1 + 6 + 1 + w + sbps);
+                    if (cb < best) {
+                        best = cb;
+                        type = 0;
+                    }
+                } else {
+                    if (cand_fixed) {
+                        uint32_t est = (uint32_t)(1 + 6 + 1 + w + A.fixed_order * sbps);
+                        est = (S.rc[0].bits < 0xFFFFFFFFu - est) ? est + S.rc[0].bits : 0xFFFFFFFFu;
+                        if (est < best) {
+                            best = est;
+                            type = 2;
+                        }
+                    }
+                    if (cand_lpc && !S.lpc_bad) {
+                        uint32_t est = (uint32_t)(1 + 6 + 1 + w + 4 + 5 + sbps * A.lpc_order + A.lpc_prec * A.lpc_order);
+                        est = (S.rc[1].bits < 0xFFFFFFFFu - est) ? est + S.rc[1].bits : 0xFFFFFFFFu;
+                        if (est != 0 && est < best) {
+                            best = est;
+                            type = 3;
+                        }
+                    }
+                }
+            }
+            S.choice = type;
+            S.best = best;
+        }
+        __syncthreads();
+    };
+
+    if constexpr (ST) {
+        for (int v = 0; v < 4; v++) {
+            const SubAnalysis A = ana[f * 4 + v];
+            load(v, A.wasted);
+            decide(A, v == 3 ? 1 : 0);
+            if (tid == 0) {
+                S.vtype[v] = S.choice;
+                S.vbits[v] = S.best;
+                S.vrc[v] = S.rc[S.choice == 2 ? 0 : 1];
+            }
+            __syncthreads();
+        }
+        if (tid == 0) {
+            const uint32_t bits[4] = {S.vbits[0] + S.vbits[1], S.vbits[0] + S.vbits[3], S.vbits[1] + S.vbits[3],
+                                      S.vbits[2] + S.vbits[3]};
+            int ca = 0;
+            for (int k = 1; k < 4; k++)
+                if (bits[k] < bits[ca]) ca = k;
+            S.assign = ca;
+        }
+        __syncthreads();
+    }
 
     // ---- frame header (RFC 9639 9.1; libFLAC FLAC__frame_add_header), thread 0
     uint64_t fb = 0;  // frame bit cursor relative to S.bits word 0
@@ -971,10 +1172,12 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
                 else src = srx = 13;
             }
             int bpc = P.bps == 8 ? 1 : P.bps == 12 ? 2 : P.bps == 16 ? 4 : P.bps == 20 ? 5 : P.bps == 24 ? 6 : P.bps == 32 ? 7 : 0;
+            // channel assignment: nch - 1 (independent), 8 left-side, 9 right-side, 10 mid-side
+            const int cac = ST ? (S.assign == 0 ? 1 : 7 + S.assign) : P.nch - 1;
             h[hb++] = 0xFF;
             h[hb++] = 0xF8;
             h[hb++] = (uint8_t)((bsc << 4) | src);
-            h[hb++] = (uint8_t)(((P.nch - 1) << 4) | (bpc << 1));
+            h[hb++] = (uint8_t)((cac << 4) | (bpc << 1));
             const uint32_t v = (uint32_t)fk;
             if (v < 0x80) h[hb++] = (uint8_t)v;
             else if (v < 0x800) { h[hb++] = (uint8_t)(0xC0 | (v >> 6)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
@@ -998,118 +1201,26 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
     }
 
     for (int c = 0; c < P.nch; c++) {
-        const SubAnalysis A = ana[f * P.nch + c];
+        // the signal coded as channel c: channel c, or for stereo (L, R) / (L, S) / (S, R) / (M, S)
+        int v = c;
+        if constexpr (ST) {
+            const int ca = S.assign;
+            v = ca == 0 ? c : ca == 1 ? (c == 0 ? 0 : 3) : ca == 2 ? (c == 0 ? 3 : 1) : (c == 0 ? 2 : 3);
+        }
+        const SubAnalysis A = ana[f * P.nvch + v];
         const int w = A.wasted;
-        const int sbps = P.bps - w;
-        // ---- load + normalise the block into LDS (strided over threads: coalesced row segments)
-        {
-            const T *base = raster + (int64_t)(P.band0 + c) * P.band_stride + g.r0 * P.row_stride + g.c0;
-            for (int i = tid; i < n; i += kEncThreads) {
-                const int64_t p = s0 + i;
-                const int64_t r = p / g.w;
-                const int cc = (int)(p - r * g.w);
-                S.xs[xsi(i)] = nz(base[r * P.row_stride + cc]) >> w;
-            }
+        const int sbps = P.bps - w + ((ST && v == 3) ? 1 : 0);
+        load(v, w);
+        int type;
+        const RiceChoice *rcp;
+        if constexpr (ST) {
+            type = S.vtype[v];
+            rcp = &S.vrc[v];
+        } else {
+            decide(A, 0);
+            type = S.choice;
+            rcp = &S.rc[type == 2 ? 0 : 1];
         }
-        if (tid < 64) {
-            S.psum[tid >> 5][tid & 31] = 0;
-        }
-        if (tid == 0) S.lpc_bad = 0;
-        __syncthreads();
-
-        // ---- candidate residual partition sums (FIXED guess and LPC)
-        const bool cand_fixed = n > 4 && !(A.flags & kFlagConstant) && (A.flags & kFlagFixedOk);
-        const bool cand_lpc = n > 4 && !(A.flags & kFlagConstant) && (A.flags & kFlagLpcOk);
-        int mpo[2] = {0, 0};
-        {
-            int o = A.fixed_order;
-            int m = max_po_block;
-            while (m > 0 && (n >> m) <= o) m--;
-            mpo[0] = m;
-            o = A.lpc_order;
-            m = max_po_block;
-            while (m > 0 && (n >> m) <= o) m--;
-            mpo[1] = m;
-        }
-        const int chunk = (n + kEncThreads - 1) / kEncThreads;
-        const int i_beg = tid * chunk, i_end = min(n, i_beg + chunk);
-        for (int cand = 0; cand < 2; cand++) {
-            if (cand == 0 && !cand_fixed) continue;
-            if (cand == 1 && !cand_lpc) continue;
-            const int o = cand == 0 ? A.fixed_order : A.lpc_order;
-            const int ps = n >> mpo[cand];
-            int cur_p = -1;
-            uint64_t acc = 0;
-            for (int i = max(i_beg, o); i < i_end; i++) {
-                int64_t r;
-                if (cand == 0) {
-                    const int64_t x = S.xs[xsi(i)];
-                    switch (o) {
-                    case 0: r = x; break;
-                    case 1: r = x - S.xs[xsi(i - 1)]; break;
-                    case 2: r = x - 2 * (int64_t)S.xs[xsi(i - 1)] + S.xs[xsi(i - 2)]; break;
-                    case 3: r = x - 3 * (int64_t)S.xs[xsi(i - 1)] + 3 * (int64_t)S.xs[xsi(i - 2)] - S.xs[xsi(i - 3)]; break;
-                    default: r = x - 4 * (int64_t)S.xs[xsi(i - 1)] + 6 * (int64_t)S.xs[xsi(i - 2)] - 4 * (int64_t)S.xs[xsi(i - 3)] + S.xs[xsi(i - 4)]; break;
-                    }
-                    r = (int32_t)r;  // libFLAC stores fixed residuals as int32
-                } else {
-                    int64_t s = 0;
-                    for (int j = 0; j < o; j++) s += (int64_t)A.q[j] * S.xs[xsi(i - 1 - j)];
-                    r = (int64_t)S.xs[xsi(i)] - (s >> A.lpc_shift);
-                    if (r <= INT32_MIN || r > INT32_MAX) S.lpc_bad = 1;
-                }
-                const int p = i / ps;
-                if (p != cur_p) {
-                    if (cur_p >= 0) atomicAdd((unsigned long long *)&S.psum[cand][cur_p], (unsigned long long)acc);
-                    cur_p = p;
-                    acc = 0;
-                }
-                acc += (uint64_t)(r < 0 ? -r : r);
-            }
-            if (cur_p >= 0) atomicAdd((unsigned long long *)&S.psum[cand][cur_p], (unsigned long long)acc);
-        }
-        __syncthreads();
-
-        // ---- decisions (process_subframe_ evaluation order: VERBATIM, CONSTANT | FIXED, LPC; strict <)
-        if (tid == 0 || tid == 64) {
-            const int cand = tid == 0 ? 0 : 1;
-            const bool on = cand == 0 ? cand_fixed : (cand_lpc && !S.lpc_bad);
-            if (on) rice_search(S.psum[cand], mpo[cand], n, cand == 0 ? A.fixed_order : A.lpc_order, rice_limit, &S.rc[cand]);
-        }
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t best = (uint32_t)(1 + 6 + 1 + w + n * sbps);
-            int type = 1;
-            if (n > 4) {
-                if (A.flags & kFlagConstant) {
-                    const uint32_t cb = (uint32_t)(1 + 6 + 1 + w + sbps);
-                    if (cb < best) {
-                        best = cb;
-                        type = 0;
-                    }
-                } else {
-                    if (cand_fixed) {
-                        uint32_t est = (uint32_t)(1 + 6 + 1 + w + A.fixed_order * sbps);
-                        est = (S.rc[0].bits < 0xFFFFFFFFu - est) ? est + S.rc[0].bits : 0xFFFFFFFFu;
-                        if (est < best) {
-                            best = est;
-                            type = 2;
-                        }
-                    }
-                    if (cand_lpc && !S.lpc_bad) {
-                        uint32_t est = (uint32_t)(1 + 6 + 1 + w + 4 + 5 + sbps * A.lpc_order + A.lpc_prec * A.lpc_order);
-                        est = (S.rc[1].bits < 0xFFFFFFFFu - est) ? est + S.rc[1].bits : 0xFFFFFFFFu;
-                        if (est != 0 && est < best) {
-                            best = est;
-                            type = 3;
-                        }
-                    }
-                }
-            }
-            S.choice = type;
-        }
-        __syncthreads();
-        const int type = S.choice;
 
         // ---- emit the subframe bits at fb (relative to S.bits)
         const uint64_t sb = fb;
@@ -1125,16 +1236,15 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
         }
         uint64_t sub_end;
         if (type == 0) {
-            if (tid == 0) put_bits(S.bits, pos, mask_bits(S.xs[xsi(0)], sbps), sbps);
+            if (tid == 0) put_sample(S.bits, pos, S.xs[xsi(0)], sbps);
             sub_end = pos + (uint64_t)sbps;
         } else if (type == 1) {
-            for (int i = tid; i < n; i += kEncThreads)
-                put_bits(S.bits, pos + (uint64_t)i * sbps, mask_bits(S.xs[xsi(i)], sbps), sbps);
+            for (int i = tid; i < n; i += kEncThreads) put_sample(S.bits, pos + (uint64_t)i * sbps, S.xs[xsi(i)], sbps);
             sub_end = pos + (uint64_t)n * sbps;
         } else {
             const int o = type == 2 ? A.fixed_order : A.lpc_order;
-            const RiceChoice &rc = S.rc[type == 2 ? 0 : 1];
-            for (int i = tid; i < o; i++) put_bits(S.bits, pos + (uint64_t)i * sbps, mask_bits(S.xs[xsi(i)], sbps), sbps);
+            const RiceChoice &rc = *rcp;
+            for (int i = tid; i < o; i++) put_sample(S.bits, pos + (uint64_t)i * sbps, S.xs[xsi(i)], sbps);
             pos += (uint64_t)o * sbps;
             if (type == 3) {
                 if (tid == 0) {
@@ -1157,28 +1267,12 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
             // per-thread code lengths of its chunk, then block exclusive scan
             uint64_t my = 0;
             for (int i = max(i_beg, o); i < i_end; i++) {
-                int64_t r;
-                if (type == 2) {
-                    const int64_t x = S.xs[xsi(i)];
-                    switch (o) {
-                    case 0: r = x; break;
-                    case 1: r = x - S.xs[xsi(i - 1)]; break;
-                    case 2: r = x - 2 * (int64_t)S.xs[xsi(i - 1)] + S.xs[xsi(i - 2)]; break;
-                    case 3: r = x - 3 * (int64_t)S.xs[xsi(i - 1)] + 3 * (int64_t)S.xs[xsi(i - 2)] - S.xs[xsi(i - 3)]; break;
-                    default: r = x - 4 * (int64_t)S.xs[xsi(i - 1)] + 6 * (int64_t)S.xs[xsi(i - 2)] - 4 * (int64_t)S.xs[xsi(i - 3)] + S.xs[xsi(i - 4)]; break;
-                    }
-                } else {
-                    int64_t s = 0;
-                    for (int j = 0; j < o; j++) s += (int64_t)A.q[j] * S.xs[xsi(i - 1 - j)];
-                    r = (int64_t)S.xs[xsi(i)] - (s >> A.lpc_shift);
-                }
-                const int32_t r32 = (int32_t)r;
+                const int32_t r32 = (int32_t)resid(A, type == 2, o, i);
                 const uint32_t u = ((uint32_t)r32 << 1) ^ (uint32_t)(r32 >> 31);
                 const int k = rc.k[i / ps];
                 my += 1 + (uint64_t)k + (u >> k);
             }
-            // block scan of my (bit counts fit 32 bits per thread chunk for sane data; use 64-bit total)
-            // two-level: wave inclusive scan with shuffles, then wave totals in LDS.
+            // block scan of my: wave inclusive scan with shuffles, then wave totals in LDS
             uint64_t incl = my;
             const int lane = tid & 63, wv = tid >> 6;
 #pragma unroll
@@ -1195,7 +1289,7 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
             uint64_t total = 0;
             for (int k = 0; k < kEncThreads / 64; k++) total += wtot[k];
             sub_end = pos + (uint64_t)pbits * (1 << po) + total;
-            if (sub_end > (uint64_t)kBitWords * 32 - 64) {  // exact code longer than the LDS window
+            if (sub_end > (uint64_t)kWords * 32 - 64) {  // exact code longer than the LDS window
                 if (tid == 0) atomicOr(error_flag, 2);
                 return;  // uniform: every thread sees the same sub_end
             }
@@ -1204,22 +1298,7 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
             uint64_t run = excl;
             __shared__ uint64_t pstart[32];
             for (int i = max(i_beg, o); i < i_end; i++) {
-                int64_t r;
-                if (type == 2) {
-                    const int64_t x = S.xs[xsi(i)];
-                    switch (o) {
-                    case 0: r = x; break;
-                    case 1: r = x - S.xs[xsi(i - 1)]; break;
-                    case 2: r = x - 2 * (int64_t)S.xs[xsi(i - 1)] + S.xs[xsi(i - 2)]; break;
-                    case 3: r = x - 3 * (int64_t)S.xs[xsi(i - 1)] + 3 * (int64_t)S.xs[xsi(i - 2)] - S.xs[xsi(i - 3)]; break;
-                    default: r = x - 4 * (int64_t)S.xs[xsi(i - 1)] + 6 * (int64_t)S.xs[xsi(i - 2)] - 4 * (int64_t)S.xs[xsi(i - 3)] + S.xs[xsi(i - 4)]; break;
-                    }
-                } else {
-                    int64_t s = 0;
-                    for (int j = 0; j < o; j++) s += (int64_t)A.q[j] * S.xs[xsi(i - 1 - j)];
-                    r = (int64_t)S.xs[xsi(i)] - (s >> A.lpc_shift);
-                }
-                const int32_t r32 = (int32_t)r;
+                const int32_t r32 = (int32_t)resid(A, type == 2, o, i);
                 const uint32_t u = ((uint32_t)r32 << 1) ^ (uint32_t)(r32 >> 31);
                 const int p = i / ps;
                 const int k = rc.k[p];
@@ -1247,7 +1326,7 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
             __syncthreads();
             const uint32_t keep = S.bits[full];
             __syncthreads();
-            for (int i = tid; i < kBitWords; i += kEncThreads) S.bits[i] = 0;
+            for (int i = tid; i < kWords; i += kEncThreads) S.bits[i] = 0;
             __syncthreads();
             if (tid == 0) S.bits[0] = keep;
             __syncthreads();
@@ -3415,7 +3494,9 @@ static int qlp_precision_for(int bps, int blocksize) {
 static int64_t slot_words_for(const frs_encode_desc *d) {
     // verbatim bound of a frame + header + slack (the exact coder can exceed the estimate a little)
     const int64_t bps = stream_bps_of(d);
-    const int64_t bits = 16 * 8 + (int64_t)d->nbands * (16 + 32 + (int64_t)d->blocksize * bps) + 64;
+    // (+ one bit per sample for a two-channel stream's side signal)
+    const int64_t bits = 16 * 8 + (int64_t)d->nbands * (16 + 32 + (int64_t)d->blocksize * bps) +
+                         (d->nbands == 2 ? (int64_t)d->blocksize : 0) + 64;
     return (bits + 31) / 32 + (int64_t)d->blocksize / 8 + 64;
 }
 
@@ -3475,13 +3556,14 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     P.ntiles = ntiles;
     P.norm_mode = d->norm_mode;
     P.vec_ok = 0;
+    P.nvch = P.nch == 2 ? 4 : P.nch;  // two channels: L, R, mid, side (level 5: exhaustive mid/side stereo)
 
     int rc = upload_tables(ctx);
     if (rc) return rc;
     hipStream_t st = ctx->stream;
     FRS_HIP(ctx->tiles.ensure(sizeof(TileGeom) * ntiles));
     FRS_HIP(ctx->norms.ensure(sizeof(TileNorm) * ntiles));
-    FRS_HIP(ctx->analysis.ensure(sizeof(SubAnalysis) * nframes * P.nch));
+    FRS_HIP(ctx->analysis.ensure(sizeof(SubAnalysis) * nframes * P.nvch));
     FRS_HIP(ctx->frame_bytes.ensure(sizeof(int64_t) * (nframes + 1) + 64));
     FRS_HIP(ctx->frame_off.ensure(sizeof(int64_t) * (nframes + 1)));
     FRS_HIP(ctx->tile_sizes.ensure(sizeof(int64_t) * (ntiles + 1) + 64));
@@ -3798,23 +3880,43 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         return FRS_OK;
     }
     FRS_HIP(ctx->slots.ensure((size_t)nframes * P.slot_words * 4));
-    // 2. analysis
-    const int64_t nsub = nframes * P.nch;
+    // 2. analysis (lane = coded signal: channel, or L/R/M/S of a two-channel stream)
+    const int64_t nsub = nframes * P.nvch;
+    const bool stereo = P.nch == 2;
+    const unsigned agrid = (unsigned)((nsub + 127) / 128);
     prof_begin(ctx, "analyze", &ev);
     if (P.bps > 16) {
-        k_analyze<DT, true><<<(unsigned)((nsub + 127) / 128), 128, 0, st>>>(raster, P, dtiles, dnorms,
-                                                                             ctx->window.as<float>(), dana, nullptr, 0);
-        k_analyze_fixed_wide<DT><<<(unsigned)((nsub + 127) / 128), 128, 0, st>>>(raster, P, dtiles, dnorms, dana);
+        if (stereo) {
+            k_analyze<DT, true, true><<<agrid, 128, 0, st>>>(raster, P, dtiles, dnorms, ctx->window.as<float>(), dana,
+                                                                nullptr, 0);
+            k_analyze_fixed_wide<DT, true><<<agrid, 128, 0, st>>>(raster, P, dtiles, dnorms, dana);
+        } else {
+            k_analyze<DT, true><<<agrid, 128, 0, st>>>(raster, P, dtiles, dnorms, ctx->window.as<float>(), dana,
+                                                         nullptr, 0);
+            k_analyze_fixed_wide<DT><<<agrid, 128, 0, st>>>(raster, P, dtiles, dnorms, dana);
+        }
     } else {
-        k_analyze<DT, false><<<(unsigned)((nsub + 127) / 128), 128, 0, st>>>(raster, P, dtiles, dnorms,
-                                                                              ctx->window.as<float>(), dana, nullptr, 0);
+        if (stereo)
+            k_analyze<DT, false, true><<<agrid, 128, 0, st>>>(raster, P, dtiles, dnorms, ctx->window.as<float>(), dana,
+                                                                 nullptr, 0);
+        else
+            k_analyze<DT, false><<<agrid, 128, 0, st>>>(raster, P, dtiles, dnorms, ctx->window.as<float>(), dana,
+                                                          nullptr, 0);
     }
     prof_end(ctx, "analyze", ev);
     // 3. encode frames into slots
     prof_begin(ctx, "encode", &ev);
-    k_encode_frames<DT><<<(unsigned)nframes, kEncThreads, 0, st>>>(raster, P, dtiles, dnorms, dana,
-                                                                   ctx->slots.as<uint32_t>(),
-                                                                   ctx->frame_bytes.as<int64_t>(), err_flag, nullptr);
+    uint32_t *dslots = ctx->slots.as<uint32_t>();
+    int64_t *dfb = ctx->frame_bytes.as<int64_t>();
+    if (stereo && P.bps > 16)
+        k_encode_frames<DT, true, int64_t><<<(unsigned)nframes, kEncThreads, 0, st>>>(raster, P, dtiles, dnorms, dana,
+                                                                                     dslots, dfb, err_flag, nullptr);
+    else if (stereo)
+        k_encode_frames<DT, true><<<(unsigned)nframes, kEncThreads, 0, st>>>(raster, P, dtiles, dnorms, dana, dslots,
+                                                                             dfb, err_flag, nullptr);
+    else
+        k_encode_frames<DT><<<(unsigned)nframes, kEncThreads, 0, st>>>(raster, P, dtiles, dnorms, dana, dslots, dfb,
+                                                                       err_flag, nullptr);
     prof_end(ctx, "encode", ev);
     // 4. offsets (frame_off[nframes] = total)
     k_scan_sizes<<<1, kScanThreads, 0, st>>>(ctx->frame_bytes.as<int64_t>(), ctx->frame_off.as<int64_t>(), nframes);

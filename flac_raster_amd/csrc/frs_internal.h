@@ -76,7 +76,7 @@ struct frs_ctx {
     HostPin pin;                       // pinned staging of the fast encode path (tiles, wave table, results)
     DevBuf host_pack;                  // device side of the packed fast-path results
     // decode scratch
-    DevBuf dec_cand, dec_count, dec_pcm, dec_soff, dec_next, dec_status, dec_fb, dec_sel;
+    DevBuf dec_cand, dec_count, dec_pcm, dec_soff, dec_next, dec_status, dec_fb, dec_sel, dec_chass;
     int decode_lane = -1;    // FRS_DECODE_LANE=0/1 (tests): force the pipelined / lane-per-frame decoder
     uint32_t dec_epoch = 0;  // call counter tagging the candidate selection's look-back words (24 bits, never 0)
     // profiling

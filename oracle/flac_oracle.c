@@ -111,7 +111,7 @@ void orc_window_tukey(float *w, int L, float p) {
 /* libFLAC fixed.c FLAC__fixed_compute_best_predictor(_wide): data points at sample 4 of the block
  * (warm-up read through data[-1..-4]).  Totals in 64 bits (identical to the 32-bit variant when it
  * does not overflow, which libFLAC guarantees by choosing the variant by bps). */
-static int fixed_best(const int32_t *data, int n, float bits[5]) {
+static int fixed_best(const int64_t *data, int n, float bits[5]) {
     uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
     for (int i = 0; i < n; i++) {
         int64_t x0 = data[i], x1 = data[i - 1], x2 = data[i - 2], x3 = data[i - 3], x4 = data[i - 4];
@@ -141,11 +141,12 @@ static int fixed_best(const int32_t *data, int n, float bits[5]) {
 }
 
 /* libFLAC 1.4.3 FLAC__fixed_compute_best_predictor_limit_residual (used when subframe_bps >= 28,
- * i.e. our 32-bit streams).  Includes its CHECK_ORDER_IS_VALID estimate quirk: the estimate for a
+ * i.e. our 32-bit streams; the _33bit twin for the side channel of a 32-bit stereo stream runs the same
+ * arithmetic on int64 samples).  Includes its CHECK_ORDER_IS_VALID estimate quirk: the estimate for a
  * "best so far" order is computed from total_error_0, the others are set to 34.0f.  This quirk is
  * why an all-zero 32-bit block is coded FIXED order 0 instead of CONSTANT (pinned by
  * test_data/sample_dem.flac). */
-static int fixed_best_limit_residual(const int32_t *data, int n, float bits[5]) {
+static int fixed_best_limit_residual(const int64_t *data, int n, float bits[5]) {
     uint64_t t[5] = {0, 0, 0, 0, 0}, smallest = UINT64_MAX;
     int valid[5] = {1, 1, 1, 1, 1};
     int order = 0;
@@ -153,11 +154,10 @@ static int fixed_best_limit_residual(const int32_t *data, int n, float bits[5]) 
         int64_t x0 = data[i];
         uint64_t e[5];
         e[0] = (uint64_t)llabs(x0);
-        e[1] = (i > -4) ? (uint64_t)llabs(x0 - (int64_t)data[i - 1]) : 0;
-        e[2] = (i > -3) ? (uint64_t)llabs(x0 - 2 * (int64_t)data[i - 1] + data[i - 2]) : 0;
-        e[3] = (i > -2) ? (uint64_t)llabs(x0 - 3 * (int64_t)data[i - 1] + 3 * (int64_t)data[i - 2] - data[i - 3]) : 0;
-        e[4] = (i > -1) ? (uint64_t)llabs(x0 - 4 * (int64_t)data[i - 1] + 6 * (int64_t)data[i - 2] -
-                                          4 * (int64_t)data[i - 3] + data[i - 4]) : 0;
+        e[1] = (i > -4) ? (uint64_t)llabs(x0 - data[i - 1]) : 0;
+        e[2] = (i > -3) ? (uint64_t)llabs(x0 - 2 * data[i - 1] + data[i - 2]) : 0;
+        e[3] = (i > -2) ? (uint64_t)llabs(x0 - 3 * data[i - 1] + 3 * data[i - 2] - data[i - 3]) : 0;
+        e[4] = (i > -1) ? (uint64_t)llabs(x0 - 4 * data[i - 1] + 6 * data[i - 2] - 4 * data[i - 3] + data[i - 4]) : 0;
         for (int k = 0; k < 5; k++) {
             t[k] += e[k];
             if (e[k] > INT32_MAX) valid[k] = 0;
@@ -274,11 +274,11 @@ static int quantize_coefs(const float *lp, int order, int precision, int32_t *q,
 }
 
 /* residual; returns 0 if a residual does not fit (libFLAC *_limit_residual returns false) */
-static int lpc_residual(const int32_t *x, int n, const int32_t *q, int order, int shift, int32_t *res) {
+static int lpc_residual(const int64_t *x, int n, const int32_t *q, int order, int shift, int32_t *res) {
     for (int i = order; i < n; i++) {
         int64_t s = 0;
         for (int j = 0; j < order; j++) s += (int64_t)q[j] * x[i - 1 - j];
-        int64_t r = (int64_t)x[i] - (s >> shift);
+        int64_t r = x[i] - (s >> shift);
         if (r <= INT32_MIN || r > INT32_MAX) return 0;
         res[i - order] = (int32_t)r;
     }
@@ -367,18 +367,21 @@ typedef struct {
 } subframe_t;
 
 /* process_subframe_ of libFLAC 1.4.3 at level 5 (max_lpc_order 8, tukey(0.5), partition orders 0..5,
- * no exhaustive search, no escapes, no qlp precision search). x is modified in place by the wasted
- * bits shift (as get_wasted_bits_ does). */
-static void decide_subframe(int32_t *x, int n, int bps, int cfg_blocksize, const float *window,
+ * no exhaustive search, no escapes, no qlp precision search).  x is modified in place by the wasted
+ * bits shift (as get_wasted_bits_ does).  bps is the STREAM's bits per sample (it sets the RICE2 limit,
+ * the qlp precision and the wasted-bits cap); extra = 1 for the side channel of process_subframes_'s
+ * mid/side pass (subframe_bps_mid_side[1] = bps - w + 1), 0 otherwise.  Samples are int64 so the side
+ * channel of a 32-bit stream (33 bits, integer_signal_33bit_side) takes the same code. */
+static void decide_subframe(int64_t *x, int n, int bps, int extra, int cfg_blocksize, const float *window,
                             int32_t *scratch_res, float *scratch_d, subframe_t *sf) {
-    /* get_wasted_bits_ */
-    int32_t orv = 0;
+    /* get_wasted_bits_ / get_wasted_bits_wide_ */
+    int64_t orv = 0;
     for (int i = 0; i < n && !(orv & 1); i++) orv |= x[i];
     int w = 0;
     if (orv != 0) { while (!(orv & 1)) { orv >>= 1; w++; } }
-    if (w > bps) w = bps;
     if (w) for (int i = 0; i < n; i++) x[i] >>= w;
-    int sbps = bps - w;
+    if (w > bps) w = bps;
+    int sbps = bps - w + extra;
     sf->wasted = w;
     sf->sbps = sbps;
     const int rice_limit = bps > 16 ? 31 : 15;
@@ -417,7 +420,7 @@ static void decide_subframe(int32_t *x, int n, int bps, int cfg_blocksize, const
         for (int i = o; i < n; i++) {
             int64_t p = 0;
             for (int j = 0; j < o; j++) p += (int64_t)fixed_coefs[o][j] * x[i - 1 - j];
-            scratch_res[i - o] = (int32_t)((int64_t)x[i] - p);
+            scratch_res[i - o] = (int32_t)(x[i] - p);
         }
         rice_t rc;
         uint32_t rb = find_best_partition(scratch_res, o, n, sbps, rice_limit, max_po, &rc);
@@ -482,7 +485,7 @@ static void write_residual(bw_t *bw, const int32_t *res, int n, int pred_order, 
     }
 }
 
-static void write_subframe(bw_t *bw, const int32_t *x, int n, const subframe_t *sf, int32_t *scratch_res) {
+static void write_subframe(bw_t *bw, const int64_t *x, int n, const subframe_t *sf, int32_t *scratch_res) {
     int typebits;
     switch (sf->type) {
     case SF_CONSTANT: typebits = 0; break;
@@ -510,7 +513,7 @@ static void write_subframe(bw_t *bw, const int32_t *x, int n, const subframe_t *
         for (int i = o; i < n; i++) {
             int64_t p = 0;
             for (int j = 0; j < o; j++) p += (int64_t)fixed_coefs[o][j] * x[i - 1 - j];
-            scratch_res[i - o] = (int32_t)((int64_t)x[i] - p);
+            scratch_res[i - o] = (int32_t)(x[i] - p);
         }
         write_residual(bw, scratch_res, n, o, &sf->rice);
     } else {
@@ -577,7 +580,7 @@ static int bps_code(int bps) {
     }
 }
 
-static void write_frame_header(bw_t *bw, int bs, int sr, int ch, int bps, uint32_t frame_no) {
+static void write_frame_header(bw_t *bw, int bs, int sr, int ch_assign, int bps, uint32_t frame_no) {
     int64_t start = bw->bits >> 3;
     int bsh, srh;
     int bc = bs_code(bs, &bsh), sc = sr_code(sr, &srh);
@@ -586,7 +589,7 @@ static void write_frame_header(bw_t *bw, int bs, int sr, int ch, int bps, uint32
     bw_put(bw, 0, 1); /* fixed blocksize */
     bw_put(bw, (uint64_t)bc, 4);
     bw_put(bw, (uint64_t)sc, 4);
-    bw_put(bw, (uint64_t)(ch - 1), 4); /* independent */
+    bw_put(bw, (uint64_t)ch_assign, 4); /* ch - 1 (independent) or 8/9/10 (left/right/mid-side) */
     bw_put(bw, (uint64_t)bps_code(bps), 3);
     bw_put(bw, 0, 1);
     /* UTF-8 coded frame number */
@@ -611,29 +614,56 @@ static void write_frame_header(bw_t *bw, int bs, int sr, int ch, int bps, uint32
 /* Encode the FLAC frames (no stream header) of `nsamples` interleaved samples with `ch` channels,
  * exactly as libFLAC 1.4.3 level 5 does through FLAC__stream_encoder_process_interleaved + finish
  * (a final short block keeps the full-length window: resize_buffers_ only grows).
+ *
+ * Two channels: level 5 sets do_mid_side_stereo=true, loose_mid_side_stereo=false
+ * (docs/sonos-pyflac.txt:6931), so process_subframes_ codes left, right, mid = (L+R)>>1 (bps) and
+ * side = L-R (bps+1) and writes the assignment with the fewest estimated bits among independent,
+ * left-side, right-side, mid-side (that order; a later one must be strictly smaller), header codes
+ * 1/8/9/10 (docs/sonos-pyflac.txt:2571-2576), subframes (L,R), (L,S), (S,R), (M,S).
  * Returns bytes written, or -(bytes needed) on overflow (rough upper bound). */
 int64_t orc_encode_frames(const int32_t *interleaved, int64_t nsamples, int ch, int bps, int sample_rate,
                           int blocksize, uint8_t *out, int64_t cap) {
     crc_init();
     if (ch < 1 || ch > ORC_MAX_CH || blocksize < 16) return -1;
+    const int stereo = ch == 2;
+    const int nv = stereo ? 4 : ch; /* coded signals: channels, or L, R, M, S */
     float *window = (float *)malloc(sizeof(float) * (size_t)blocksize);
     float *dbuf = (float *)malloc(sizeof(float) * (size_t)blocksize);
-    int32_t *xbuf = (int32_t *)malloc(sizeof(int32_t) * (size_t)blocksize * (size_t)ch);
+    int64_t *xbuf = (int64_t *)malloc(sizeof(int64_t) * (size_t)blocksize * (size_t)nv);
     int32_t *res = (int32_t *)malloc(sizeof(int32_t) * (size_t)blocksize);
     orc_window_tukey(window, blocksize, 0.5f);
     bw_t bw = {out, cap, 0, 0};
     uint32_t frame_no = 0;
+    subframe_t sf[ORC_MAX_CH];
     for (int64_t s0 = 0; s0 < nsamples; s0 += blocksize, frame_no++) {
         int n = (int)((nsamples - s0) < blocksize ? (nsamples - s0) : blocksize);
         int64_t fstart = bw.bits >> 3;
-        write_frame_header(&bw, n, sample_rate, ch, bps, frame_no);
         for (int c = 0; c < ch; c++) {
-            int32_t *x = xbuf + (size_t)c * blocksize;
+            int64_t *x = xbuf + (size_t)c * blocksize;
             for (int i = 0; i < n; i++) x[i] = interleaved[(s0 + i) * ch + c];
-            subframe_t sf;
-            memset(&sf, 0, sizeof(sf));
-            decide_subframe(x, n, bps, blocksize, window, res, dbuf, &sf);
-            write_subframe(&bw, x, n, &sf, res);
+        }
+        if (stereo) {
+            int64_t *l = xbuf, *r = xbuf + blocksize, *m = xbuf + 2 * (size_t)blocksize, *sd = xbuf + 3 * (size_t)blocksize;
+            for (int i = 0; i < n; i++) { m[i] = (l[i] + r[i]) >> 1; sd[i] = l[i] - r[i]; }
+        }
+        for (int v = 0; v < nv; v++) {
+            memset(&sf[v], 0, sizeof(sf[v]));
+            decide_subframe(xbuf + (size_t)v * blocksize, n, bps, stereo && v == 3, blocksize, window, res, dbuf, &sf[v]);
+        }
+        int assign = ch - 1, pick[2] = {0, 1};
+        if (stereo) {
+            const uint32_t bits[4] = {sf[0].est_bits + sf[1].est_bits, sf[0].est_bits + sf[3].est_bits,
+                                      sf[1].est_bits + sf[3].est_bits, sf[2].est_bits + sf[3].est_bits};
+            static const int picks[4][2] = {{0, 1}, {0, 3}, {3, 1}, {2, 3}};
+            int ca = 0;
+            for (int k = 1; k < 4; k++) if (bits[k] < bits[ca]) ca = k;
+            assign = ca == 0 ? 1 : 7 + ca;
+            pick[0] = picks[ca][0]; pick[1] = picks[ca][1];
+        }
+        write_frame_header(&bw, n, sample_rate, assign, bps, frame_no);
+        for (int c = 0; c < ch; c++) {
+            int v = stereo ? pick[c] : c;
+            write_subframe(&bw, xbuf + (size_t)v * blocksize, n, &sf[v], res);
         }
         bw_align(&bw);
         int64_t fend = bw.bits >> 3;
@@ -824,11 +854,13 @@ static uint32_t br_unary(br_t *b) {
 
 /* Decode the frames that follow a stream header; returns samples per channel decoded, or <0 on error.
  * out: interleaved int32, capacity cap_samples per channel. */
-int64_t orc_decode_frames(const uint8_t *in, int64_t n, int ch, int bps, int32_t *out, int64_t cap_samples) {
+static int64_t decode_frames_impl(const uint8_t *in, int64_t n, int ch, int bps, int32_t *out, int64_t cap_samples,
+                                  int8_t *ca_out, int64_t ca_cap) {
     crc_init();
+    int64_t nfr = 0;
     br_t b = {in, n, 0, 0};
     int64_t total = 0;
-    int32_t *tmp = (int32_t *)malloc(sizeof(int32_t) * 65536 * 8);
+    int64_t *tmp = (int64_t *)malloc(sizeof(int64_t) * 65536 * 8); /* int64: a 32-bit stream's side channel has 33 bits */
     while ((b.bit >> 3) + 2 <= n) {
         int64_t fstart = b.bit >> 3;
         if (br_u(&b, 14) != 0x3FFE) { free(tmp); return -2; }
@@ -851,12 +883,14 @@ int64_t orc_decode_frames(const uint8_t *in, int64_t n, int ch, int bps, int32_t
         uint8_t c8 = (uint8_t)br_u(&b, 8);
         if (c8 != crc8(in + fstart, hend - fstart)) { free(tmp); return -4; }
         int fbps = ss == 1 ? 8 : ss == 2 ? 12 : ss == 4 ? 16 : ss == 5 ? 20 : ss == 6 ? 24 : ss == 7 ? 32 : bps;
+        if (ca_out && nfr < ca_cap) ca_out[nfr] = (int8_t)ca;
+        nfr++;
         int nch = ca < 8 ? ca + 1 : 2;
         if (nch != ch || total + bs > cap_samples || bs > 65536) { free(tmp); return -5; }
         for (int c = 0; c < nch; c++) {
             int sbps = fbps;
             if ((ca == 8 && c == 1) || (ca == 9 && c == 0) || (ca == 10 && c == 1)) sbps++;
-            int32_t *x = tmp + (size_t)c * 65536;
+            int64_t *x = tmp + (size_t)c * 65536;
             br_u(&b, 1);
             int t = (int)br_u(&b, 6);
             int w = 0;
@@ -864,14 +898,14 @@ int64_t orc_decode_frames(const uint8_t *in, int64_t n, int ch, int bps, int32_t
             sbps -= w;
             if (t == 0) {
                 int64_t v = br_s(&b, sbps);
-                for (int i = 0; i < bs; i++) x[i] = (int32_t)v;
+                for (int i = 0; i < bs; i++) x[i] = v;
             } else if (t == 1) {
-                for (int i = 0; i < bs; i++) x[i] = (int32_t)br_s(&b, sbps);
+                for (int i = 0; i < bs; i++) x[i] = br_s(&b, sbps);
             } else if ((t >= 8 && t <= 12) || t >= 32) {
                 int lpc = t >= 32, o = lpc ? t - 31 : t - 8;
                 int64_t q[32];
                 int shift = 0, prec;
-                for (int i = 0; i < o; i++) x[i] = (int32_t)br_s(&b, sbps);
+                for (int i = 0; i < o; i++) x[i] = br_s(&b, sbps);
                 if (lpc) {
                     prec = (int)br_u(&b, 4) + 1;
                     shift = (int)br_s(&b, 5);
@@ -885,7 +919,7 @@ int64_t orc_decode_frames(const uint8_t *in, int64_t n, int ch, int bps, int32_t
                     int k = (int)br_u(&b, pb);
                     if (k == esc) {
                         int nb = (int)br_u(&b, 5);
-                        for (int i = 0; i < ns; i++) x[idx + i] = nb ? (int32_t)br_s(&b, nb) : 0;
+                        for (int i = 0; i < ns; i++) x[idx + i] = nb ? br_s(&b, nb) : 0;
                     } else {
                         for (int i = 0; i < ns; i++) {
                             uint32_t qq = br_unary(&b);
@@ -904,25 +938,25 @@ int64_t orc_decode_frames(const uint8_t *in, int64_t n, int ch, int bps, int32_t
                     } else {
                         for (int j = 0; j < o; j++) pred += (int64_t)fixed_coefs[o][j] * x[i - 1 - j];
                     }
-                    x[i] = (int32_t)(x[i] + pred);
+                    x[i] = x[i] + pred;
                 }
             } else {
                 free(tmp);
                 return -6;
             }
-            if (w) for (int i = 0; i < bs; i++) x[i] = (int32_t)((uint32_t)x[i] << w);
+            if (w) for (int i = 0; i < bs; i++) x[i] = (int64_t)((uint64_t)x[i] << w);
         }
         /* undo stereo decorrelation */
         if (ca >= 8) {
-            int32_t *l = tmp, *r = tmp + 65536;
+            int64_t *l = tmp, *r = tmp + 65536;
             for (int i = 0; i < bs; i++) {
                 int64_t a = l[i], s = r[i];
-                if (ca == 8) { r[i] = (int32_t)(a - s); }
-                else if (ca == 9) { l[i] = (int32_t)(a + s); }
+                if (ca == 8) { r[i] = a - s; }
+                else if (ca == 9) { l[i] = a + s; }
                 else {
-                    int64_t mid = (a << 1) | (s & 1);
-                    l[i] = (int32_t)((mid + s) >> 1);
-                    r[i] = (int32_t)((mid - s) >> 1);
+                    int64_t mid = (int64_t)((uint64_t)a << 1) | (s & 1);
+                    l[i] = (mid + s) >> 1;
+                    r[i] = (mid - s) >> 1;
                 }
             }
         }
@@ -931,11 +965,21 @@ int64_t orc_decode_frames(const uint8_t *in, int64_t n, int ch, int bps, int32_t
         uint16_t c16 = (uint16_t)br_u(&b, 16);
         if (b.err || c16 != crc16(in + fstart, fend - fstart)) { free(tmp); return -7; }
         for (int i = 0; i < bs; i++)
-            for (int c = 0; c < nch; c++) out[(total + i) * nch + c] = tmp[(size_t)c * 65536 + i];
+            for (int c = 0; c < nch; c++) out[(total + i) * nch + c] = (int32_t)tmp[(size_t)c * 65536 + i];
         total += bs;
     }
     free(tmp);
     return total;
+}
+
+int64_t orc_decode_frames(const uint8_t *in, int64_t n, int ch, int bps, int32_t *out, int64_t cap_samples) {
+    return decode_frames_impl(in, n, ch, bps, out, cap_samples, NULL, 0);
+}
+
+/* as orc_decode_frames, and the channel assignment code of every frame into ca_out (test diagnostics) */
+int64_t orc_decode_frames_ca(const uint8_t *in, int64_t n, int ch, int bps, int32_t *out, int64_t cap_samples,
+                             int8_t *ca_out, int64_t ca_cap) {
+    return decode_frames_impl(in, n, ch, bps, out, cap_samples, ca_out, ca_cap);
 }
 
 /* ------------------------------------------------------------------ streaming tiler (cli.py:690-763) */

@@ -46,6 +46,8 @@ def lib():
         L.orc_denormalize_i16.argtypes = [vp, i64, i32, ctypes.c_double, ctypes.c_double, i32, vp]
         L.orc_decode_frames.restype = i64
         L.orc_decode_frames.argtypes = [vp, i64, i32, i32, vp, i64]
+        L.orc_decode_frames_ca.restype = i64
+        L.orc_decode_frames_ca.argtypes = [vp, i64, i32, i32, vp, i64, vp, i64]
         L.orc_encode_tiles.restype = i64
         L.orc_encode_tiles.argtypes = [vp, i32, i64, i64, i64, i32, i32, i32, vp, i64, vp, vp, vp, i32]
         L.orc_normalize_spatial.restype = i32
@@ -126,6 +128,17 @@ def decode_frames(data: bytes, channels: int, bps: int, max_samples: int) -> np.
     if r < 0:
         raise RuntimeError(f"oracle decode error {r}")
     return out[:r]
+
+
+def frame_assignments(data: bytes, channels: int, bps: int, max_samples: int) -> np.ndarray:
+    """Channel-assignment code of every frame (0..7 independent, 8 left-side, 9 right-side, 10 mid-side)."""
+    buf = np.frombuffer(data, dtype=np.uint8)
+    out = np.empty((max_samples, channels), dtype=np.int32)
+    ca = np.empty(max_samples // 16 + 16, dtype=np.int8)
+    r = lib().orc_decode_frames_ca(_ptr(buf), len(buf), channels, bps, _ptr(out), max_samples, _ptr(ca), len(ca))
+    if r < 0:
+        raise RuntimeError(f"oracle decode error {r}")
+    return ca[: -(-r // 4096) if r else 0].copy()
 
 
 def denormalize_i16(pcm: np.ndarray, dmin: float, dmax: float, dtype, pcm_bps: int = 16) -> np.ndarray:
