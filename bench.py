@@ -65,14 +65,43 @@ def parse():
     return ap.parse_args()
 
 
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` without a launcher environment: start N local ranks of this script (one per GPU, the
+    environment torchrun would set) BEFORE anything touches the GPU, and return the exit code of the group (the
+    first failing rank's; the others are stopped then).  Rank 0 prints the JSON line."""
+    from flac_raster_amd import launch
+    return launch.run_ranks(args.gpus, [str(Path(__file__).resolve())] + sys.argv[1:], module=None)
+
+
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     from flac_raster_amd import _native, distributed
 
     rank, world, local_rank = distributed.env_rank_world()
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    backend = os.environ.get("FRS_COMM_BACKEND", "rccl") if world > 1 else "none"
+    if os.environ.get("FRS_BENCH_SELFTEST") == "1":  # CPU tests of the launch path: ranks, world, exchange
+        comm = distributed.init_comm(None, "tcp") if world > 1 else None
+        ranks = comm.allgather_i64(np.array([rank])) if comm is not None else np.array([0])
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "n_gpus": world, "ranks": [int(r) for r in ranks],
+                              "config": {"parallelism": parallelism(world, backend)}}), flush=True)
+        if comm is not None:
+            comm.close()
+        return
     # one rank per GPU; FRS_COMM_BACKEND=tcp (the host exchange) lets a rehearsal put several ranks on one GPU
-    ctx = _native.Context(local_rank % max(1, _native.device_count()))
-    comm = distributed.init_comm(ctx, os.environ.get("FRS_COMM_BACKEND", "rccl")) if world > 1 else None
+    ndev = _native.device_count()
+    if world > 1 and backend == "rccl" and world > ndev:
+        print(f"bench.py: {world} ranks but {ndev} GPUs (one rank per GPU; FRS_COMM_BACKEND=tcp shares a GPU)",
+              file=sys.stderr)
+        sys.exit(2)
+    ctx = _native.Context(local_rank % max(1, ndev))
+    comm = distributed.init_comm(ctx, backend) if world > 1 else None
 
     T, W, H, B = args.tile, args.width, args.height, args.bands
     tcols, trows = (W + T - 1) // T, (H + T - 1) // T
@@ -153,7 +182,7 @@ def main():
                    "create-streaming encode (band 1, device-resident) + C5 bbox extract",
                    "raster": f"{H}x{W}x{B} int16", "tile_size": T, "tiles": trows * tcols,
                    "tiles_rank0": int(counts[0]), "blocksize": 4096, "compression_level": 5,
-                   "parallelism": f"tile rows sharded x{world} (RCCL all-gather of tile sizes)",
+                   "parallelism": parallelism(world, backend),
                    "compressed_bytes_rank0": comp_bytes},
         "kernels_ms": {k: round(v, 4) for k, v in kernels.items()},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -185,6 +214,13 @@ def main():
     if comm is not None:
         comm.close()
     ctx.close()
+
+
+def parallelism(world: int, backend: str) -> str:
+    if world == 1:
+        return "single GPU (no exchange)"
+    how = {"rccl": "RCCL all-gather over xGMI", "tcp": "host TCP all-gather"}.get(backend, backend)
+    return f"tile rows sharded x{world} ({how} of tile sizes)"
 
 
 def bbox_extract(ctx, comm, raster, arena, off, tmin, tmax, H, W, T, row0, counts, nq):

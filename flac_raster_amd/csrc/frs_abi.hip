@@ -193,16 +193,37 @@ int frs_encode_tiles(frs_ctx *ctx, const frs_encode_desc *desc, const void *rast
 
 }  // extern "C"
 
+// argument checks shared by every decode entry point, before anything is sized or copied: the geometry ranges and
+// non-decreasing stream / sample offsets (reversed offsets would make a negative byte count a huge size_t)
+static int check_decode_args(frs_ctx *ctx, const int64_t *stream_off, const int64_t *pcm_off, int32_t nstreams,
+                             int32_t channels, int32_t bps, int32_t blocksize) {
+    if (!stream_off || !pcm_off || nstreams < 0 || channels < 1 || channels > 8 || blocksize < 16 ||
+        blocksize > 65535 || bps < 4 || bps > 32) {
+        ctx->err = "bad decode arguments";
+        return FRS_E_ARG;
+    }
+    for (int s = 1; s <= nstreams; s++)
+        if (stream_off[s] < stream_off[s - 1] || pcm_off[s] < pcm_off[s - 1]) {
+            ctx->err = "stream and sample offsets must be non-decreasing";
+            return FRS_E_ARG;
+        }
+    if (nstreams > 0 && (stream_off[0] < 0 || pcm_off[0] < 0)) {
+        ctx->err = "negative stream or sample offset";
+        return FRS_E_ARG;
+    }
+    return FRS_OK;
+}
+
 // shared argument checks and stream rebasing of the decode entry points: only [stream_off[0],
 // stream_off[nstreams]) is scanned, so a tile query inside a large arena touches just its own bytes
 static int decode_entry(frs_ctx *ctx, const uint8_t *blob_dev, const int64_t *stream_off, int32_t nstreams,
                         int32_t channels, int32_t bps, int32_t blocksize, int32_t *pcm_dev, const int64_t *pcm_off,
                         const double *dmin, const double *dmax, int32_t out_dtype, void *out_dev) {
-    if (!blob_dev || !stream_off || !pcm_off || nstreams < 0 || channels < 1 || channels > 8 || blocksize < 16 ||
-        blocksize > 65535 || bps < 4 || bps > 32) {
+    if (!blob_dev) {
         ctx->err = "bad decode arguments";
         return FRS_E_ARG;
     }
+    if (int rc = check_decode_args(ctx, stream_off, pcm_off, nstreams, channels, bps, blocksize)) return rc;
     if (out_dev && (!dmin || !dmax || frs::dtype_size(out_dtype) == 0)) {
         ctx->err = "bad decode arguments (data_min/data_max/out dtype)";
         return FRS_E_ARG;
@@ -239,7 +260,8 @@ int frs_decode_frames_device(frs_ctx *ctx, const uint8_t *blob_dev, const int64_
 int frs_decode_frames(frs_ctx *ctx, const uint8_t *blob_host, const int64_t *stream_off, int32_t nstreams,
                       int32_t channels, int32_t bps, int32_t blocksize, int32_t *pcm_host, const int64_t *pcm_off) {
     if (!ctx) return FRS_E_ARG;
-    if (!blob_host || !stream_off || !pcm_host || !pcm_off || nstreams < 0) { ctx->err = "bad decode arguments"; return FRS_E_ARG; }
+    if (!blob_host || !pcm_host) { ctx->err = "bad decode arguments"; return FRS_E_ARG; }
+    if (int rc = check_decode_args(ctx, stream_off, pcm_off, nstreams, channels, bps, blocksize)) return rc;
     FRS_HIP(hipSetDevice(ctx->device));
     const int64_t nbytes = nstreams ? stream_off[nstreams] : 0;
     const int64_t nsamp = nstreams ? pcm_off[nstreams] : 0;
@@ -268,10 +290,11 @@ int frs_decode_tiles(frs_ctx *ctx, const uint8_t *blob_host, const int64_t *stre
                      const double *data_max, int32_t out_dtype, void *out_host) {
     if (!ctx) return FRS_E_ARG;
     const int es = frs::dtype_size(out_dtype);
-    if (!blob_host || !stream_off || !out_host || !pcm_off || nstreams < 0 || es == 0 || channels < 1) {
+    if (!blob_host || !out_host || es == 0) {
         ctx->err = "bad decode arguments";
         return FRS_E_ARG;
     }
+    if (int rc = check_decode_args(ctx, stream_off, pcm_off, nstreams, channels, bps, blocksize)) return rc;
     FRS_HIP(hipSetDevice(ctx->device));
     if (nstreams == 0) return FRS_OK;
     const int64_t nbytes = stream_off[nstreams] - stream_off[0];
@@ -280,12 +303,14 @@ int frs_decode_tiles(frs_ctx *ctx, const uint8_t *blob_host, const int64_t *stre
     FRS_HIP(ctx->arena_stage.ensure((size_t)nout * es + 16));
     FRS_HIP(hipMemcpyAsync(ctx->raster_stage.ptr, blob_host + stream_off[0], (size_t)nbytes, hipMemcpyHostToDevice,
                            ctx->stream));
-    std::vector<int64_t> rel(nstreams + 1);
-    for (int s = 0; s <= nstreams; s++) rel[s] = stream_off[s] - stream_off[0];
-    // the device output starts at sample pcm_off[0] of the host array
-    uint8_t *dout = ctx->arena_stage.as<uint8_t>() - pcm_off[0] * channels * es;
+    // stream and sample offsets relative to the first stream: the device output is the staging buffer itself
+    std::vector<int64_t> rel(nstreams + 1), prel(nstreams + 1);
+    for (int s = 0; s <= nstreams; s++) {
+        rel[s] = stream_off[s] - stream_off[0];
+        prel[s] = pcm_off[s] - pcm_off[0];
+    }
     int rc = decode_entry(ctx, ctx->raster_stage.as<uint8_t>(), rel.data(), nstreams, channels, bps, blocksize, nullptr,
-                          pcm_off, data_min, data_max, out_dtype, dout);
+                          prel.data(), data_min, data_max, out_dtype, ctx->arena_stage.ptr);
     if (rc) return rc;
     FRS_HIP(hipMemcpyAsync(static_cast<uint8_t *>(out_host) + pcm_off[0] * channels * es, ctx->arena_stage.ptr,
                            (size_t)nout * es, hipMemcpyDeviceToHost, ctx->stream));

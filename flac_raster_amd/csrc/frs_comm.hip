@@ -7,8 +7,10 @@
 #include <dlfcn.h>
 #include <string.h>
 
+#include <chrono>
 #include <mutex>
 #include <string>
+#include <thread>
 
 #include <rccl/rccl.h>
 
@@ -29,6 +31,8 @@ struct RcclApi {
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
     ncclResult_t (*all_gather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
     const char *(*error_string)(ncclResult_t) = nullptr;
+    ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;                      // optional
+    ncclResult_t (*get_async_error)(ncclComm_t, ncclResult_t *) = nullptr;  // optional
     std::string err;
 };
 RcclApi g_api;
@@ -48,6 +52,8 @@ bool load_rccl() {
         g_api.comm_destroy = (decltype(g_api.comm_destroy))dlsym(g_api.h, "ncclCommDestroy");
         g_api.all_gather = (decltype(g_api.all_gather))dlsym(g_api.h, "ncclAllGather");
         g_api.error_string = (decltype(g_api.error_string))dlsym(g_api.h, "ncclGetErrorString");
+        g_api.comm_abort = (decltype(g_api.comm_abort))dlsym(g_api.h, "ncclCommAbort");
+        g_api.get_async_error = (decltype(g_api.get_async_error))dlsym(g_api.h, "ncclCommGetAsyncError");
         if (!g_api.get_unique_id || !g_api.comm_init_rank || !g_api.comm_destroy || !g_api.all_gather)
             g_api.err = "librccl.so lacks the nccl* entry points";
     });
@@ -120,8 +126,44 @@ int frs_comm_allgather_i64(frs_comm *c, const int64_t *send_host, int64_t count,
         return FRS_E_HIP;
     }
     FRS_HIP(hipMemcpyAsync(recv_host, drecv, sb * (size_t)c->nranks, hipMemcpyDeviceToHost, ctx->stream));
-    FRS_HIP(hipStreamSynchronize(ctx->stream));
-    return FRS_OK;
+    // bounded wait: a dead or hung peer would leave the collective pending for good.  Poll an event, check the
+    // communicator's asynchronous error, and abort it after $FRS_COMM_TIMEOUT seconds (default 120).
+    hipEvent_t done;
+    FRS_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    FRS_HIP(hipEventRecord(done, ctx->stream));
+    double limit_s = 120.0;
+    if (const char *e = getenv("FRS_COMM_TIMEOUT")) limit_s = atof(e);
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = FRS_OK;
+    for (int spin = 0;; spin++) {
+        const hipError_t q = hipEventQuery(done);
+        if (q == hipSuccess) break;
+        if (q != hipErrorNotReady) {
+            ctx->err = std::string("all-gather: ") + hipGetErrorString(q);
+            rc = FRS_E_HIP;
+            break;
+        }
+        ncclResult_t ae = ncclSuccess;
+        if (g_api.get_async_error && g_api.get_async_error(c->comm, &ae) == ncclSuccess && ae != ncclSuccess &&
+            ae != ncclInProgress) {
+            ctx->err = "ncclAllGather: " + nccl_msg(ae);
+            rc = FRS_E_HIP;
+            break;
+        }
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (el > limit_s) {
+            ctx->err = "ncclAllGather did not complete within FRS_COMM_TIMEOUT (a peer rank died or hung)";
+            rc = FRS_E_HIP;
+            break;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(spin < 1000 ? 5 : 200));
+    }
+    hipEventDestroy(done);
+    if (rc != FRS_OK && g_api.comm_abort && c->comm) {
+        g_api.comm_abort(c->comm);  // frees the pending collective; the communicator is unusable afterwards
+        c->comm = nullptr;
+    }
+    return rc;
 }
 
 }  // extern "C"

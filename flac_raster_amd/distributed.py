@@ -62,7 +62,11 @@ class TcpComm:
     """All-gather of byte strings over a TCP star (rank 0 is the hub).  Bootstrap of RcclComm and the exchange of
     the CPU tests; each call is one round trip per rank."""
 
-    def __init__(self, rank: int, world: int, addr: str = "127.0.0.1", port: int = 29600, timeout: float = 300.0):
+    def __init__(self, rank: int, world: int, addr: str = "127.0.0.1", port: int = 29600,
+                 timeout: Optional[float] = None):
+        # a dead peer closes its socket (EOF -> ConnectionError at once); a hung one is cut off after `timeout`
+        # seconds of silence ($FRS_COMM_TIMEOUT, default 120 s)
+        timeout = float(os.environ.get("FRS_COMM_TIMEOUT", "120")) if timeout is None else timeout
         self.rank, self.world = rank, world
         self.peers: List[socket.socket] = []
         self.sock: Optional[socket.socket] = None
@@ -77,6 +81,7 @@ class TcpComm:
             peers = {}
             while len(peers) < world - 1:
                 c, _ = srv.accept()
+                c.settimeout(timeout)
                 c.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
                 r = struct.unpack("<i", _recv_exact(c, 4))[0]
                 peers[r] = c
@@ -92,6 +97,7 @@ class TcpComm:
                     if time.time() > t_end:
                         raise
                     time.sleep(0.05)
+            s.settimeout(timeout)
             s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
             s.sendall(struct.pack("<i", rank))
             self.sock = s
@@ -206,7 +212,12 @@ def create_streaming_sharded(band_rows: np.ndarray, row0: int, full_shape: Tuple
     counts = [(shard_tile_rows(trows, world, r)[1] - shard_tile_rows(trows, world, r)[0]) * tcols for r in range(world)]
     if band_rows.shape[0] and row0 % tile:
         raise ValueError("a rank's slab must start on a tile-row boundary")
-    enc = encode(band_rows, tile)
+    if band_rows.shape[0] == 0 or band_rows.shape[1] == 0:
+        # more ranks than tile rows: nothing to encode, but the rank still joins the all-gather and the barrier
+        z = np.zeros(0, dtype=np.float64)
+        enc = EncodedTiles([], np.zeros(0, dtype=np.uint8), np.zeros(1, dtype=np.int64), z, z, 16)
+    else:
+        enc = encode(band_rows, tile)
     t1 = time.perf_counter()
     all_windows = tile_grid(H, W, tile)
     first = sum(counts[:rank])
@@ -253,15 +264,20 @@ def create_streaming_distributed(input_file: Path, output_file: Path, tile_size:
     from ._native import Context, device_count
     backend = backend or os.environ.get("FRS_COMM_BACKEND", "rccl")
     rank, world, local_rank = env_rank_world()
-    r = geotiff.read(input_file)
-    transform = r.transform or geotiff.Affine(1.0, 0.0, 0.0, 0.0, 1.0, 0.0)
-    H, W = r.height, r.width
-    tr0, tr1 = shard_tile_rows((H + tile_size - 1) // tile_size, world, rank)
-    slab = np.ascontiguousarray(r.data[0, tr0 * tile_size:min(tr1 * tile_size, H)])
-    ctx = Context(local_rank % max(1, device_count()))
+    with geotiff.TiffFile(input_file) as tf:  # only this rank's band-1 rows are decoded (cli.py:698-699)
+        H, W = tf.height, tf.width
+        tr0, tr1 = shard_tile_rows((H + tile_size - 1) // tile_size, world, rank)
+        transform, epsg, _, _ = tf.georef()
+        slab = np.ascontiguousarray(tf.read_rows(tr0 * tile_size, min(tr1 * tile_size, H), [0])[0])
+    transform = transform or geotiff.Affine(1.0, 0.0, 0.0, 0.0, 1.0, 0.0)
+    crs = f"EPSG:{epsg}" if epsg else None
+    ndev = device_count()
+    if backend == "rccl" and world > ndev:
+        raise RuntimeError(f"{world} ranks but {ndev} GPUs: one rank per GPU (FRS_COMM_BACKEND=tcp shares GPUs)")
+    ctx = Context(local_rank % max(1, ndev))
     comm = init_comm(ctx, backend)
     try:
-        return create_streaming_sharded(slab, tr0 * tile_size, (H, W), transform, r.crs_string, tile_size,
+        return create_streaming_sharded(slab, tr0 * tile_size, (H, W), transform, crs, tile_size,
                                         Path(output_file), comm, gpu_encoder(ctx))
     finally:
         comm.close()

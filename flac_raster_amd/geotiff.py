@@ -151,164 +151,260 @@ def _packbits_decode(data: bytes) -> bytes:
     return bytes(out)
 
 
-def read(path) -> GeoRaster:
-    buf = Path(path).read_bytes()
-    bo = "<" if buf[:2] == b"II" else ">"
-    magic = struct.unpack(bo + "H", buf[2:4])[0]
-    if magic == 42:
-        off = struct.unpack(bo + "I", buf[4:8])[0]
-        big = False
-    elif magic == 43:
-        off = struct.unpack(bo + "Q", buf[8:16])[0]
-        big = True
-    else:
-        raise ValueError(f"{path}: not a TIFF")
-    if big:
-        n = struct.unpack(bo + "Q", buf[off:off + 8])[0]
-        ent, esz, base = 20, 8, off + 8
-    else:
-        n = struct.unpack(bo + "H", buf[off:off + 2])[0]
-        ent, esz, base = 12, 4, off + 2
-    tags = {}
-    for i in range(n):
-        e = buf[base + ent * i: base + ent * (i + 1)]
-        tag, typ = struct.unpack(bo + "HH", e[:4])
-        cnt = struct.unpack(bo + ("Q" if big else "I"), e[4:4 + esz])[0]
-        fmt, sz = _TYPES.get(typ, ("B", 1))
-        nbytes = sz * cnt
-        raw = e[4 + esz:4 + 2 * esz]
-        if nbytes > esz:
-            vo = struct.unpack(bo + ("Q" if big else "I"), raw)[0]
-            raw = buf[vo:vo + nbytes]
-        if typ == 2:
-            tags[tag] = raw[:cnt].split(b"\0")[0].decode("latin-1")
+class TiffFile:
+    """A GeoTIFF opened by memory map: tags parsed once, pixel rows decoded on demand.
+
+    ``read_rows(row0, row1, bands)`` decodes only the strips / tiles that intersect the rows (uncompressed chunks
+    are viewed in place), so a rank of the sharded create-streaming reads its band-1 slab without touching the
+    rest of the file -- the reference's per-tile ``src.read(1, window=...)`` (cli.py:698-699) at slab granularity.
+    """
+
+    def __init__(self, path):
+        import mmap
+        self.path = Path(path)
+        self._f = open(self.path, "rb")
+        size = self.path.stat().st_size
+        self._mm = mmap.mmap(self._f.fileno(), 0, access=mmap.ACCESS_READ) if size else b""
+        buf = self._mm
+        bo = "<" if buf[:2] == b"II" else ">"
+        magic = struct.unpack(bo + "H", buf[2:4])[0]
+        if magic == 42:
+            off = struct.unpack(bo + "I", buf[4:8])[0]
+            big = False
+        elif magic == 43:
+            off = struct.unpack(bo + "Q", buf[8:16])[0]
+            big = True
         else:
-            tags[tag] = struct.unpack(bo + fmt * cnt, raw[:nbytes])
-    W, H = tags[256][0], tags[257][0]
-    spp = tags.get(277, (1,))[0]
-    bits = tags.get(258, (8,))[0]
-    sfmt = tags.get(339, (1,))[0]
-    comp = tags.get(259, (1,))[0]
-    planar = tags.get(284, (1,))[0]
-    pred = tags.get(317, (1,))[0]
-    kind = {1: "u", 2: "i", 3: "f"}[sfmt]
-    dt = np.dtype(f"{bo}{kind}{bits // 8}")
+            raise ValueError(f"{path}: not a TIFF")
+        if big:
+            n = struct.unpack(bo + "Q", buf[off:off + 8])[0]
+            ent, esz, base = 20, 8, off + 8
+        else:
+            n = struct.unpack(bo + "H", buf[off:off + 2])[0]
+            ent, esz, base = 12, 4, off + 2
+        tags = {}
+        for i in range(n):
+            e = buf[base + ent * i: base + ent * (i + 1)]
+            tag, typ = struct.unpack(bo + "HH", e[:4])
+            cnt = struct.unpack(bo + ("Q" if big else "I"), e[4:4 + esz])[0]
+            fmt, sz = _TYPES.get(typ, ("B", 1))
+            nbytes = sz * cnt
+            raw = e[4 + esz:4 + 2 * esz]
+            if nbytes > esz:
+                vo = struct.unpack(bo + ("Q" if big else "I"), raw)[0]
+                raw = buf[vo:vo + nbytes]
+            if typ == 2:
+                tags[tag] = raw[:cnt].split(b"\0")[0].decode("latin-1")
+            else:
+                tags[tag] = struct.unpack(bo + fmt * cnt, raw[:nbytes])
+        self.tags = tags
+        self.width, self.height = tags[256][0], tags[257][0]
+        self.spp = tags.get(277, (1,))[0]
+        bits = tags.get(258, (8,))[0]
+        sfmt = tags.get(339, (1,))[0]
+        self.comp = tags.get(259, (1,))[0]
+        self.planar = tags.get(284, (1,))[0]
+        self.pred = tags.get(317, (1,))[0]
+        kind = {1: "u", 2: "i", 3: "f"}[sfmt]
+        self.file_dtype = np.dtype(f"{bo}{kind}{bits // 8}")
+        self.dtype = self.file_dtype.newbyteorder("=")
 
-    def decomp(b: bytes) -> bytes:
-        if comp == 1:
-            return b
-        if comp in (8, 32946):
-            return zlib.decompress(b)
-        if comp == 5:
-            return _lzw_decode(b)
-        if comp == 32773:
-            return _packbits_decode(b)
-        raise NotImplementedError(f"TIFF compression {comp}")
+    def close(self):
+        if self._mm:
+            self._mm.close()
+        self._f.close()
 
-    nplanes = spp if planar == 2 else 1
-    cs = 1 if planar == 2 else spp
-    out = np.zeros((nplanes, H, W, cs), dtype=dt)
-    if 322 in tags:  # tiled
-        tw, th = tags[322][0], tags[323][0]
-        offs, cnts = tags[324], tags[325]
-        tx = (W + tw - 1) // tw
-        ty = (H + th - 1) // th
-        for pl in range(nplanes):
-            for j in range(ty):
-                for i in range(tx):
-                    k = pl * tx * ty + j * tx + i
-                    a = np.frombuffer(decomp(buf[offs[k]:offs[k] + cnts[k]]), dtype=dt)[:th * tw * cs]
-                    a = a.reshape(th, tw, cs)
-                    if pred == 2:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def count(self) -> int:
+        return self.spp
+
+    def _decomp(self, k: int, offs, cnts, nelem: int) -> np.ndarray:
+        b = self._mm[offs[k]:offs[k] + cnts[k]] if self.comp != 1 else None
+        if self.comp == 1:
+            return np.frombuffer(self._mm, dtype=self.file_dtype, count=nelem, offset=offs[k])
+        if self.comp in (8, 32946):
+            raw = zlib.decompress(b)
+        elif self.comp == 5:
+            raw = _lzw_decode(b)
+        elif self.comp == 32773:
+            raw = _packbits_decode(b)
+        else:
+            raise NotImplementedError(f"TIFF compression {self.comp}")
+        return np.frombuffer(raw, dtype=self.file_dtype)[:nelem]
+
+    def read_rows(self, row0: int = 0, row1: Optional[int] = None, bands: Optional[List[int]] = None) -> np.ndarray:
+        """Pixels of rows [row0, row1) of the given 0-based bands (default: all) -> (len(bands), rows, width)."""
+        H, W, spp = self.height, self.width, self.spp
+        row1 = H if row1 is None else min(row1, H)
+        bands = list(range(spp)) if bands is None else list(bands)
+        nr = max(0, row1 - row0)
+        dt = self.file_dtype
+        out = np.empty((len(bands), nr, W), dtype=self.dtype)
+        if nr == 0:
+            return out
+        tags = self.tags
+        chunky = self.planar != 2
+        cs = spp if chunky else 1
+        planes = [0] if chunky else bands  # planes to decode
+
+        if 322 in tags:  # tiled
+            tw, th = tags[322][0], tags[323][0]
+            offs, cnts = tags[324], tags[325]
+            tx, ty = (W + tw - 1) // tw, (H + th - 1) // th
+            for pl in planes:
+                sel = [(j, b) for j, b in enumerate(bands)] if chunky else [(bands.index(pl), 0)]
+                for jt in range(row0 // th, (row1 - 1) // th + 1):
+                    for i in range(tx):
+                        k = pl * tx * ty + jt * tx + i
+                        a = self._decomp(k, offs, cnts, th * tw * cs).reshape(th, tw, cs)
+                        if self.pred == 2:
+                            a = np.cumsum(a, axis=1, dtype=dt)
+                        h, w = min(th, H - jt * th), min(tw, W - i * tw)
+                        lo, hi = max(jt * th, row0), min(jt * th + h, row1)
+                        for j, bsel in sel:
+                            out[j, lo - row0:hi - row0, i * tw:i * tw + w] = a[lo - jt * th:hi - jt * th, :w, bsel]
+        else:
+            rps = tags.get(278, (H,))[0]
+            offs, cnts = tags[273], tags[279]
+            nstrips = (H + rps - 1) // rps
+            for pl in planes:
+                sel = [(j, b) for j, b in enumerate(bands)] if chunky else [(bands.index(pl), 0)]
+                for sidx in range(row0 // rps, (row1 - 1) // rps + 1):
+                    k = pl * nstrips + sidx
+                    rows = min(rps, H - sidx * rps)
+                    a = self._decomp(k, offs, cnts, rows * W * cs).reshape(rows, W, cs)
+                    if self.pred == 2:
                         a = np.cumsum(a, axis=1, dtype=dt)
-                    h = min(th, H - j * th)
-                    w = min(tw, W - i * tw)
-                    out[pl, j * th:j * th + h, i * tw:i * tw + w] = a[:h, :w]
-    else:
-        rps = tags.get(278, (H,))[0]
-        offs, cnts = tags[273], tags[279]
-        nstrips = (H + rps - 1) // rps
-        for pl in range(nplanes):
-            for s in range(nstrips):
-                k = pl * nstrips + s
-                rows = min(rps, H - s * rps)
-                a = np.frombuffer(decomp(buf[offs[k]:offs[k] + cnts[k]]), dtype=dt)[:rows * W * cs]
-                a = a.reshape(rows, W, cs)
-                if pred == 2:
-                    a = np.cumsum(a, axis=1, dtype=dt)
-                out[pl, s * rps:s * rps + rows] = a
-    if planar == 2:
-        data = out[:, :, :, 0]
-    else:
-        data = out[0].transpose(2, 0, 1)
-    data = np.ascontiguousarray(data).astype(dt.newbyteorder("="), copy=False)
-    # georeferencing (GDAL GTiff semantics, PixelIsArea default)
-    transform = None
-    if 34264 in tags:
-        m = tags[34264]
-        transform = Affine(m[0], m[1], m[3], m[4], m[5], m[7])
-    elif 33550 in tags and 33922 in tags:
-        sx, sy = tags[33550][0], tags[33550][1]
-        tp = tags[33922]
-        transform = Affine(sx, 0.0, tp[3] - tp[0] * sx, 0.0, -sy, tp[4] + tp[1] * sy)
-    epsg = None
-    extra = {}
-    if 34735 in tags:
-        gk = tags[34735]
-        nkeys = gk[3]
-        raster_type = 1
-        for i in range(nkeys):
-            kid, loc, cnt, val = gk[4 + 4 * i: 8 + 4 * i]
-            if loc == 0:
-                extra[kid] = val
-                if kid in (3072, 2048) and val not in (0, 32767):
-                    epsg = int(val) if (kid == 3072 or epsg is None) else epsg
-                if kid == 1025:
-                    raster_type = val
-        if raster_type == 2 and transform is not None and 34264 not in tags:
-            # PixelIsPoint: GDAL shifts the origin by half a pixel (GTIFF_POINT_GEO_IGNORE=FALSE)
-            transform = Affine(transform.a, transform.b, transform.c - 0.5 * transform.a - 0.5 * transform.b,
-                               transform.d, transform.e, transform.f - 0.5 * transform.d - 0.5 * transform.e)
-    nodata = None
-    if 42113 in tags:
-        try:
-            nodata = float(tags[42113])
-        except ValueError:
-            nodata = None
-    return GeoRaster(data=data, transform=transform, epsg=epsg, nodata=nodata, extra_geokeys=extra)
+                    lo, hi = max(sidx * rps, row0), min(sidx * rps + rows, row1)
+                    for j, bsel in sel:
+                        out[j, lo - row0:hi - row0] = a[lo - sidx * rps:hi - sidx * rps, :, bsel]
+        return out
+
+    def georef(self):
+        """(transform, epsg, nodata, extra geokeys) with GDAL GTiff semantics (PixelIsArea default)."""
+        tags = self.tags
+        transform = None
+        if 34264 in tags:
+            m = tags[34264]
+            transform = Affine(m[0], m[1], m[3], m[4], m[5], m[7])
+        elif 33550 in tags and 33922 in tags:
+            sx, sy = tags[33550][0], tags[33550][1]
+            tp = tags[33922]
+            transform = Affine(sx, 0.0, tp[3] - tp[0] * sx, 0.0, -sy, tp[4] + tp[1] * sy)
+        epsg = None
+        extra = {}
+        if 34735 in tags:
+            gk = tags[34735]
+            nkeys = gk[3]
+            raster_type = 1
+            for i in range(nkeys):
+                kid, loc, cnt, val = gk[4 + 4 * i: 8 + 4 * i]
+                if loc == 0:
+                    extra[kid] = val
+                    if kid in (3072, 2048) and val not in (0, 32767):
+                        epsg = int(val) if (kid == 3072 or epsg is None) else epsg
+                    if kid == 1025:
+                        raster_type = val
+            if raster_type == 2 and transform is not None and 34264 not in tags:
+                # PixelIsPoint: GDAL shifts the origin by half a pixel (GTIFF_POINT_GEO_IGNORE=FALSE)
+                transform = Affine(transform.a, transform.b, transform.c - 0.5 * transform.a - 0.5 * transform.b,
+                                   transform.d, transform.e, transform.f - 0.5 * transform.d - 0.5 * transform.e)
+        nodata = None
+        if 42113 in tags:
+            try:
+                nodata = float(tags[42113])
+            except ValueError:
+                nodata = None
+        return transform, epsg, nodata, extra
+
+    def raster(self, row0: int = 0, row1: Optional[int] = None, bands: Optional[List[int]] = None) -> GeoRaster:
+        transform, epsg, nodata, extra = self.georef()
+        return GeoRaster(data=self.read_rows(row0, row1, bands), transform=transform, epsg=epsg, nodata=nodata,
+                         extra_geokeys=extra)
+
+
+def read(path) -> GeoRaster:
+    """The whole raster (rasterio ``src.read()``)."""
+    with TiffFile(path) as tf:
+        return tf.raster()
 
 
 def write(path, data: np.ndarray, transform: Optional[Affine] = None, epsg: Optional[int] = None,
-          nodata: Optional[float] = None) -> None:
-    """Write (count, height, width) uncompressed GTiff (GDAL-like layout)."""
+          nodata: Optional[float] = None, compress: Optional[str] = None, predictor: int = 1,
+          tile: Optional[int] = None, planar: int = 1) -> None:
+    """Write (count, height, width) GTiff (GDAL-like layout): ~8 KB strips by default, or `tile` x `tile` tiles;
+    chunky (planar 1) or band-sequential (planar 2) samples; uncompressed or ``compress="deflate"`` with optional
+    horizontal differencing (predictor 2)."""
     a = np.asarray(data)
     if a.ndim == 2:
         a = a[None]
     count, H, W = a.shape
     dt = a.dtype
     a = np.ascontiguousarray(a.astype(dt.newbyteorder("<"), copy=False))
-    pix = np.ascontiguousarray(a.transpose(1, 2, 0)) if count > 1 else a[0]
-    row_bytes = W * count * dt.itemsize
-    rps = max(1, min(H, 8192 // max(1, row_bytes)))
-    nstrips = (H + rps - 1) // rps
-    raw = pix.tobytes()
-    big = len(raw) > 0xF0000000
+    chunky = planar == 1 or count == 1
+    cs = count if chunky else 1
+    planes = [np.ascontiguousarray(a.transpose(1, 2, 0))] if chunky else [a[b][:, :, None] for b in range(count)]
+
+    def encode_chunk(x: np.ndarray) -> bytes:  # x: (rows, cols, cs)
+        if predictor == 2:
+            x = x.copy()
+            x[:, 1:] = np.diff(x, axis=1)
+        b = np.ascontiguousarray(x).tobytes()
+        return zlib.compress(b, 6) if compress == "deflate" else b
+
+    chunks: List[bytes] = []
+    if tile:
+        tw = th = int(tile)
+        tx, ty = (W + tw - 1) // tw, (H + th - 1) // th
+        for pl in planes:
+            for j in range(ty):
+                for i in range(tx):
+                    blk = np.zeros((th, tw, cs), dtype=a.dtype)
+                    src = pl[j * th:(j + 1) * th, i * tw:(i + 1) * tw]
+                    blk[:src.shape[0], :src.shape[1]] = src
+                    chunks.append(encode_chunk(blk))
+        rps = None
+    else:
+        row_bytes = W * cs * dt.itemsize
+        rps = max(1, min(H, 8192 // max(1, row_bytes)))
+        nstrips = (H + rps - 1) // rps
+        for pl in planes:
+            for st in range(nstrips):
+                chunks.append(encode_chunk(pl[st * rps:(st + 1) * rps]))
+    total = sum(len(c) for c in chunks)
+    big = total > 0xF0000000
     sfmt = 3 if dt.kind == "f" else (2 if dt.kind == "i" else 1)
     entries: List[Tuple[int, int, tuple]] = []
 
     def add(tag, typ, vals):
         entries.append((tag, typ, tuple(vals) if isinstance(vals, (list, tuple)) else (vals,)))
 
+    off_tag, cnt_tag = (324, 325) if tile else (273, 279)
     add(256, 3 if W < 65536 else 4, W)
     add(257, 3 if H < 65536 else 4, H)
     add(258, 3, [dt.itemsize * 8] * count)
-    add(259, 3, 1)
+    add(259, 3, 8 if compress == "deflate" else 1)
     add(262, 3, 2 if (count == 3 and dt == np.uint8) else 1)
-    add(273, 16 if big else 4, [0] * nstrips)  # patched below
+    if not tile:
+        add(273, 16 if big else 4, [0] * len(chunks))  # patched below
     add(277, 3, count)
-    add(278, 3 if rps < 65536 else 4, rps)
-    add(279, 16 if big else 4, [min(rps, H - s * rps) * row_bytes for s in range(nstrips)])
-    add(284, 3, 1)
+    if not tile:
+        add(278, 3 if rps < 65536 else 4, rps)
+        add(279, 16 if big else 4, [len(c) for c in chunks])
+    add(284, 3, 1 if chunky else 2)
+    if predictor == 2:
+        add(317, 3, 2)
+    if tile:
+        add(322, 3, int(tile))
+        add(323, 3, int(tile))
+        add(324, 16 if big else 4, [0] * len(chunks))  # patched below
+        add(325, 16 if big else 4, [len(c) for c in chunks])
     if count > 1 and not (count == 3 and dt == np.uint8):
         add(338, 3, [0] * (count - 1))
     add(339, 3, [sfmt] * count)
@@ -336,8 +432,9 @@ def write(path, data: np.ndarray, transform: Optional[Affine] = None, epsg: Opti
     ent = 20 if big else 12
     ifd_size = (8 + len(entries) * ent + 8) if big else (2 + len(entries) * ent + 4)
     esz = 8 if big else 4
-    ool = bytearray()
     ool_base = hdr + ifd_size
+    chunk_off = np.zeros(len(chunks) + 1, dtype=np.int64)
+    chunk_off[1:] = np.cumsum([len(c) for c in chunks])
 
     def pack_vals(typ, vals):
         if typ == 2:
@@ -345,14 +442,14 @@ def write(path, data: np.ndarray, transform: Optional[Affine] = None, epsg: Opti
         fmt, _ = _TYPES[typ]
         return struct.pack("<" + fmt * len(vals), *vals)
 
-    # pixel data offset depends on ool size: compute two passes
+    # pixel data offset depends on the out-of-line size: two passes
     def build(data_off):
         out_ool = bytearray()
         ifd = bytearray()
         ifd += struct.pack("<Q", len(entries)) if big else struct.pack("<H", len(entries))
         for tag, typ, vals in entries:
-            if tag == 273:
-                vals = tuple(data_off + s * rps * row_bytes for s in range(nstrips))
+            if tag == off_tag:
+                vals = tuple(int(data_off + o) for o in chunk_off[:-1])
             payload = pack_vals(typ, vals)
             cnt = len(payload) if typ == 2 else len(vals)
             ifd += struct.pack("<HH", tag, typ) + (struct.pack("<Q", cnt) if big else struct.pack("<I", cnt))
@@ -377,4 +474,5 @@ def write(path, data: np.ndarray, transform: Optional[Affine] = None, epsg: Opti
             fh.write(b"II" + struct.pack("<HI", 42, hdr))
         fh.write(ifd)
         fh.write(ool)
-        fh.write(raw)
+        for c in chunks:
+            fh.write(c)

@@ -134,8 +134,13 @@ class EncodedTiles:
 
 def encode_band_tiles(band: np.ndarray, tile_size: int, ctx: Optional[Context] = None) -> EncodedTiles:
     """All band-1 tiles in one GPU launch sequence (the reference's tile loop, cli.py:690-763)."""
-    ctx = ctx or default_context()
     H, W = band.shape
+    if H == 0 or W == 0:  # an empty shard (more ranks than tile rows): no tiles, nothing to launch
+        z = np.zeros(0, dtype=np.float64)
+        _, bps = audio_params(1, 1, band.dtype)
+        return EncodedTiles([], np.zeros(0, dtype=np.uint8), np.zeros(1, dtype=np.int64), z, z,
+                            16 if bps == 16 else 32)
+    ctx = ctx or default_context()
     _, bps = audio_params(1, min(tile_size, H), band.dtype)
     d = ctx.make_desc(H, W, band.dtype, nbands=1, tile_h=tile_size, tile_w=tile_size, sample_rate=44100,
                       bits_per_sample=bps)
@@ -248,7 +253,8 @@ def create_streaming_array(band: np.ndarray, transform: geotiff.Affine, crs: Opt
 def create_streaming(input_file: Path, output_file: Path, tile_size: int = 1024,
                      ctx: Optional[Context] = None) -> Dict:
     """cli.py:620-804 without the console output: writes the streaming file, returns the index."""
-    r = geotiff.read(input_file)
+    with geotiff.TiffFile(input_file) as tf:  # band 1 only (cli.py:698-699)
+        r = tf.raster(bands=[0])
     transform = r.transform or geotiff.Affine(1.0, 0.0, 0.0, 0.0, 1.0, 0.0)
     return create_streaming_array(np.ascontiguousarray(r.data[0]), transform, r.crs_string, output_file, tile_size,
                                   ctx)

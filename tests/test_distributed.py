@@ -128,3 +128,71 @@ def test_rccl_comm_world_one(gpu_ctx, tmp_path, monkeypatch):
     finally:
         comm.close()
     assert out.read_bytes() == _reference(band, 256)
+
+
+def test_more_ranks_than_tile_rows(tmp_path):
+    """World 3 on a band of one tile row: ranks 1 and 2 hold empty slabs, still join the exchange, and the file is
+    the single-process one."""
+    band = _band(200, 650, 3)
+    out = tmp_path / "tiny.flac"
+    _run_ranks(3, out, band, 256)
+    assert out.read_bytes() == _reference(band, 256)
+
+
+_HANG_SCRIPT = """
+import os, sys, time
+sys.path.insert(0, {root!r})
+from flac_raster_amd import distributed as D
+rank, world, _ = D.env_rank_world()
+if rank == 1:
+    sys.exit(3)             # a rank that dies before the exchange
+comm = D.init_comm(None, "tcp")
+comm.barrier()              # rank 0 would wait here for the dead peer
+time.sleep(600)
+"""
+
+
+def test_rank_failure_is_bounded(tmp_path):
+    """launch.run_ranks: one rank exits non-zero -> the group stops within seconds and returns that code."""
+    import time
+    from flac_raster_amd import launch
+    script = tmp_path / "hang.py"
+    script.write_text(_HANG_SCRIPT.format(root=str(ROOT)))
+    t0 = time.monotonic()
+    rc = launch.run_ranks(2, [str(script)], module=None, timeout=60)
+    assert rc == 3
+    assert time.monotonic() - t0 < 30
+
+
+def test_cli_create_streaming_gpus_failure_returns_1(tmp_path):
+    """create-streaming --gpus 2 whose ranks cannot run (no GPU here; one GPU on the test box) exits 1 promptly."""
+    import subprocess
+    import time
+    from flac_raster_amd import geotiff
+    src = tmp_path / "in.tif"
+    geotiff.write(src, _band(300, 300, 2), geotiff.Affine(*TRANSFORM), 32636)
+    t0 = time.monotonic()
+    env = dict(os.environ, FRS_COMM_TIMEOUT="20")
+    r = subprocess.run([sys.executable, "-m", "flac_raster_amd", "create-streaming", str(src), "-o",
+                        str(tmp_path / "o.flac"), "--tile-size", "128", "--gpus", "2"], cwd=str(ROOT), env=env,
+                       capture_output=True, timeout=120)
+    assert r.returncode == 1, r.stderr[-2000:]
+    assert time.monotonic() - t0 < 30
+
+
+def test_bench_gpus_n_launches_n_ranks():
+    """bench.py --gpus 2 without a launcher starts two ranks (the driver's command shape); the self-test mode
+    exchanges rank ids over the host all-gather and rank 0 reports n_gpus 2."""
+    import json
+    import subprocess
+    env = dict(os.environ, FRS_BENCH_SELFTEST="1", FRS_COMM_BACKEND="tcp")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2"], env=env, capture_output=True,
+                       timeout=120, text=True)
+    assert r.returncode == 0, r.stderr
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["ranks"] == [0, 1]
+    assert "host TCP" in line["config"]["parallelism"]
+    bad = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2"], env=dict(env, WORLD_SIZE="1"),
+                         capture_output=True, timeout=60, text=True)
+    assert bad.returncode != 0

@@ -173,3 +173,15 @@ def test_long_stream_chain_matches_oracle(gpu_ctx, kind, monkeypatch):
     with pytest.raises(_native.FrsError):
         dctx.decode_frames_host(flipped, off, [n], channels=1, bps=16)
     dctx.close()
+
+
+def test_decode_rejects_reversed_offsets(gpu_ctx):
+    """Reversed stream / sample offsets are an argument error (checked before any staging is sized)."""
+    from flac_raster_amd import _native
+    blob = np.zeros(64, dtype=np.uint8)
+    for call in (lambda: gpu_ctx.decode_tiles_host(blob, [40, 0], [4096], channels=1, bps=16, data_min=[0.0],
+                                                   data_max=[1.0], dtype=np.int16),
+                 lambda: gpu_ctx.decode_frames_host(blob, [40, 0], [4096], channels=1, bps=16)):
+        with pytest.raises(_native.FrsError) as e:
+            call()
+        assert e.value.code == -1 and "non-decreasing" in str(e.value)

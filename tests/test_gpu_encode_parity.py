@@ -161,28 +161,28 @@ def test_fast_path_scale_and_noise(gpu_ctx, kind, shape, tile):
     (np.uint16, 0, 40000, 256),      # fast-division tiles (the SLOW analysis launch)
     (np.int16, -30000, 30000, 128),  # wrapping range (exact division)
 ])
-def test_fast_path_stats_modes(dtype, lo, hi, tile, monkeypatch):
-    """The fast path's tile stats run fused into the analysis launch (one wave per tile; default) or as separate
-    kernels before it (FRS_ABLATE 4096): both must give the oracle's bytes, also on a second call."""
-    from flac_raster_amd import _native
+def test_fast_path_stats_modes(gpu_ctx, dtype, lo, hi, tile):
+    """The fast path's tile stats run fused into the analysis launch (16-bit samples, 16-byte aligned rows, tiles
+    of <= 64 frames) or as separate kernels before it (k_tile_stats(_vec) + k_tile_finalize + k_build_lut: tiles of
+    more than 64 frames, rows that are not 16-byte runs).  Each geometry below takes one route -- checked through
+    the per-kernel profile ("stats" is timed only when the separate kernels run) -- and both must give the
+    oracle's bytes, also on a second call."""
     rng = np.random.default_rng(99)
-    H, W = 768, 1280
-    y, x = np.meshgrid(np.linspace(0, 1, H), np.linspace(0, 1, W), indexing="ij")
-    band = np.clip(lo + (hi - lo) * (0.5 + 0.45 * np.sin(7 * x) * np.cos(3 * y))
-                   + rng.normal(0, (hi - lo) * 0.01 + 0.3, (H, W)), lo, hi).astype(dtype)
-    band[:tile, :tile] = band[0, 0]
-    o_arena, o_off, o_mn, o_mx = O.encode_tiles(band, tile, threads=8)
-    for ablate in ("0", "4096"):
-        monkeypatch.setenv("FRS_ABLATE", ablate)
-        ctx = _native.Context(0)
-        try:
-            for _ in range(2):  # second call reuses the side stream, events and scratch
-                arena, off, mn, mx, bps = _gpu_tiles(ctx, band, tile)
-                assert list(off) == list(o_off), ablate
-                assert arena.tobytes() == o_arena.tobytes(), ablate
-                assert list(mn) == list(o_mn) and list(mx) == list(o_mx), ablate
-        finally:
-            ctx.close()
+    for H, W, t, fused in ((768, 1280, tile, True), (1100, 1300, 1024, False), (700, 1283, tile, False)):
+        y, x = np.meshgrid(np.linspace(0, 1, H), np.linspace(0, 1, W), indexing="ij")
+        band = np.clip(lo + (hi - lo) * (0.5 + 0.45 * np.sin(7 * x) * np.cos(3 * y))
+                       + rng.normal(0, (hi - lo) * 0.01 + 0.3, (H, W)), lo, hi).astype(dtype)
+        band[:t, :t] = band[0, 0]
+        o_arena, o_off, o_mn, o_mx = O.encode_tiles(band, t, threads=8)
+        for _ in range(2):  # second call reuses the scratch
+            gpu_ctx.profile(True)
+            gpu_ctx.profile_reset()
+            arena, off, mn, mx, bps = _gpu_tiles(gpu_ctx, band, t)
+            gpu_ctx.profile(False)
+            assert (gpu_ctx.profile_avg_ms("stats") <= 0) == fused, (H, W, t)
+            assert list(off) == list(o_off), (H, W, t)
+            assert arena.tobytes() == o_arena.tobytes(), (H, W, t)
+            assert list(mn) == list(o_mn) and list(mx) == list(o_mx), (H, W, t)
 
 
 @pytest.mark.parametrize("dtype,bands,shape,seed", [

@@ -153,3 +153,30 @@ def test_streaming_writer_equals_assembled_bytes(tmp_path):
     os.pwrite(fd, head, 0)
     os.close(fd)
     assert out.read_bytes() == head + b"".join(streams)
+
+
+def test_tiff_windowed_rows_equal_full_read(tmp_path, golden):
+    """TiffFile.read_rows decodes only the chunks under the rows and equals the slice of the full read, for
+    strips / tiles, chunky / planar, uncompressed / deflate (+ horizontal predictor), and the fixtures."""
+    import numpy as np
+    from flac_raster_amd import geotiff
+    rng = np.random.default_rng(5)
+    data = rng.integers(-3000, 3000, size=(3, 77, 91)).astype(np.int16)
+    paths = [golden / f"{n}.tif" for n in ("sample_rgb", "sample_dem", "sample_multispectral")]
+    for i, kw in enumerate([{}, dict(compress="deflate"), dict(compress="deflate", predictor=2),
+                            dict(tile=32), dict(tile=16, compress="deflate", predictor=2), dict(planar=2),
+                            dict(planar=2, tile=32, compress="deflate")]):
+        p = tmp_path / f"w{i}.tif"
+        geotiff.write(p, data, geotiff.Affine(2.0, 0.0, 10.0, 0.0, -2.0, 50.0), 32636, **kw)
+        assert np.array_equal(geotiff.read(p).data, data), kw
+        paths.append(p)
+    for p in paths:
+        full = geotiff.read(p)
+        with geotiff.TiffFile(p) as tf:
+            H = tf.height
+            for r0, r1 in ((0, 1), (5, 40), (H - 3, H), (0, H), (17, 18)):
+                for bands in (None, [0], [tf.count - 1]):
+                    got = tf.read_rows(r0, r1, bands)
+                    sel = full.data if bands is None else full.data[bands]
+                    assert np.array_equal(got, sel[:, r0:r1]), (p.name, r0, r1, bands)
+            assert tf.georef()[0] == full.transform
