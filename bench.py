@@ -488,14 +488,24 @@ def e2e_cpu_baseline(band, out, index, n, T, qs):
     return {"create_streaming": create, "extract_streaming": extract}
 
 
+def loaded_lib_sha256() -> str:
+    """sha256 of the codec library this process loads (FRS_LIB_PATH or the in-tree build)."""
+    import hashlib
+    from flac_raster_amd import _native
+    p = Path(os.environ.get("FRS_LIB_PATH", str(_native.LIB_PATH)))
+    return hashlib.sha256(p.read_bytes()).hexdigest()
+
+
 def pmc_for(path, kernel, px, field):
     """Per-launch PMC figure `field` of `kernel` from a committed summary (tools/pmc_traffic.py) measured on this
-    same workload (C4 slab of `px` pixels); None when absent or taken on another workload."""
+    same workload (C4 slab of `px` pixels) AND this same library build (its sha256 stamp); None otherwise."""
     try:
         d = json.loads(Path(path).read_text())
     except (OSError, ValueError):
         return None
     if d.get("pixels_per_launch") not in (None, px):
+        return None
+    if d.get("lib_sha256") != loaded_lib_sha256():
         return None
     k = d.get("kernels", {}).get(KERNEL_SYMBOL.get(kernel, kernel))
     return None if k is None or field not in k else k[field]

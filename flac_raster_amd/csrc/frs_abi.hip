@@ -4,7 +4,9 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
+#include <thread>
 
 #include <vector>
 
@@ -118,9 +120,14 @@ void frs_ctx_destroy(frs_ctx *ctx) {
     frs::prof_collect(ctx);
     DevBuf *bufs[] = {&ctx->tiles, &ctx->norms, &ctx->analysis, &ctx->slots, &ctx->frame_bytes, &ctx->frame_off,
                       &ctx->window, &ctx->tile_sizes, &ctx->luts, &ctx->status, &ctx->frame_tile, &ctx->hdr_tab, &ctx->wave_tab, &ctx->plist, &ctx->sub_slots, &ctx->sub_bits, &ctx->mc_bytes, &ctx->raster_stage, &ctx->arena_stage, &ctx->host_pack,
-                      &ctx->dec_cand, &ctx->dec_count, &ctx->dec_pcm, &ctx->dec_soff, &ctx->dec_next, &ctx->dec_status, &ctx->dec_fb, &ctx->dec_sel};
+                      &ctx->dec_cand, &ctx->dec_count, &ctx->dec_pcm, &ctx->dec_soff, &ctx->dec_next, &ctx->dec_status, &ctx->dec_fb, &ctx->dec_sel,
+                      &ctx->dec_chass};
     for (DevBuf *b : bufs) b->release();
     ctx->pin.release();
+    ctx->ring[0].release();
+    ctx->ring[1].release();
+    if (ctx->h2d_stream) hipStreamDestroy(ctx->h2d_stream);
+    if (ctx->d2h_stream) hipStreamDestroy(ctx->d2h_stream);
     hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -162,6 +169,121 @@ int frs_encode_tiles_device(frs_ctx *ctx, const frs_encode_desc *desc, const voi
     return frs::encode_job(ctx, desc, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max, stream_bps);
 }
 
+}  // extern "C"
+
+// memcpy by up to `nt` threads over contiguous ranges (host staging into pinned memory runs at a fraction of the
+// memory bandwidth on one thread)
+static void par_memcpy(void *dst, const void *src, size_t n, int nt) {
+    if (n < ((size_t)8 << 20) || nt <= 1) {
+        memcpy(dst, src, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t c = ((n + nt - 1) / nt + 4095) & ~(size_t)4095;
+    for (int i = 0; i < nt; i++) {
+        const size_t a = std::min(n, (size_t)i * c), b = std::min(n, a + c);
+        if (b > a)
+            th.emplace_back([=] { memcpy(static_cast<char *>(dst) + a, static_cast<const char *>(src) + a, b - a); });
+    }
+    for (auto &t : th) t.join();
+}
+
+static int host_threads() {
+    if (const char *e = getenv("FRS_HOST_THREADS")) return std::max(1, atoi(e));
+    if (const char *e = getenv("OMP_NUM_THREADS")) return std::max(1, std::min(16, atoi(e)));
+    return (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+}
+
+// Host-pointer encode of a single-band job (create-streaming band 1) in tile-row batches, so the PCIe transfers hide
+// behind each other and behind the kernels: batch b + 1 is copied into a pinned ring slot by `nt` host threads and
+// DMA'd on its own stream while batch b encodes on the context's stream, and batch b's frames go back on a third
+// stream while batch b + 1 encodes.  Frames land in arena_host exactly as one whole-job encode would put them.
+static int encode_tiles_batched(frs_ctx *ctx, const frs_encode_desc *desc, const uint8_t *src, size_t es,
+                                uint8_t *arena_host, int64_t arena_cap, int64_t *tile_off, double *tile_min,
+                                double *tile_max, int32_t *stream_bps, int64_t batch_rows) {
+    const int64_t tcols = (desc->width + desc->tile_w - 1) / desc->tile_w;
+    const int64_t t_lo = desc->tile_begin, t_hi = desc->tile_end;
+    const int64_t row_bytes = desc->row_stride * (int64_t)es;
+    const uint8_t *band = src + (size_t)desc->band0 * desc->band_stride * es;
+    // device copy of the band rows the job touches, and one arena for the whole job
+    const int64_t r_lo = (t_lo / tcols) * desc->tile_h;
+    const int64_t r_hi = std::min<int64_t>(desc->height, ((t_hi - 1) / tcols + 1) * desc->tile_h);
+    FRS_HIP(ctx->raster_stage.ensure((size_t)((r_hi - r_lo) * row_bytes)));
+    const int64_t bound = frs::arena_bound(desc);
+    FRS_HIP(ctx->arena_stage.ensure((size_t)bound));
+    if (!ctx->h2d_stream) FRS_HIP(hipStreamCreateWithFlags(&ctx->h2d_stream, hipStreamNonBlocking));
+    if (!ctx->d2h_stream) FRS_HIP(hipStreamCreateWithFlags(&ctx->d2h_stream, hipStreamNonBlocking));
+    const size_t slot = (size_t)(batch_rows * desc->tile_h * row_bytes);
+    FRS_HIP(ctx->ring[0].ensure(slot));
+    FRS_HIP(ctx->ring[1].ensure(slot));
+    // batches of whole tile rows (the first and last may be partial rows of the tile range)
+    struct Batch { int64_t t0, t1, r0, r1; };
+    std::vector<Batch> B;
+    for (int64_t t = t_lo; t < t_hi;) {
+        const int64_t tr = t / tcols;
+        const int64_t t1 = std::min(t_hi, (tr + batch_rows) * tcols);
+        const int64_t r0 = tr * desc->tile_h;
+        const int64_t r1 = std::min<int64_t>(desc->height, ((t1 - 1) / tcols + 1) * desc->tile_h);
+        B.push_back({t, t1, r0, r1});
+        t = t1;
+    }
+    const int nt = host_threads();
+    hipEvent_t up[2] = {nullptr, nullptr}, down = nullptr;
+    for (auto &e : up) FRS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    FRS_HIP(hipEventCreateWithFlags(&down, hipEventDisableTiming));
+    bool used[2] = {false, false};
+    int rc = FRS_OK;
+    auto stage = [&](size_t b) -> int {  // host copy into ring slot b % 2, then its DMA
+        const int k = (int)(b & 1);
+        if (used[k]) FRS_HIP(hipEventSynchronize(up[k]));  // the slot's previous DMA has drained
+        const size_t n = (size_t)((B[b].r1 - B[b].r0) * row_bytes);
+        par_memcpy(ctx->ring[k].ptr, band + (size_t)B[b].r0 * row_bytes, n, nt);
+        FRS_HIP(hipMemcpyAsync(ctx->raster_stage.as<uint8_t>() + (size_t)(B[b].r0 - r_lo) * row_bytes, ctx->ring[k].ptr,
+                               n, hipMemcpyHostToDevice, ctx->h2d_stream));
+        FRS_HIP(hipEventRecord(up[k], ctx->h2d_stream));
+        used[k] = true;
+        return FRS_OK;
+    };
+    int64_t aoff = 0;
+    if (B.size()) rc = stage(0);
+    // the device raster view starts at row r_lo: tiles address rows relative to the descriptor's origin
+    const uint8_t *dev_raster = ctx->raster_stage.as<uint8_t>() - (size_t)r_lo * row_bytes -
+                                (size_t)desc->band0 * desc->band_stride * es;
+    for (size_t b = 0; b < B.size() && rc == FRS_OK; b++) {
+        // the next batch's host copy overlaps this batch's DMA (and the previous batch's D2H)
+        if (b + 1 < B.size() && (rc = stage(b + 1)) != FRS_OK) break;
+        FRS_HIP(hipStreamWaitEvent(ctx->stream, up[b & 1], 0));  // batch b's rows are on the device
+        frs_encode_desc db = *desc;
+        db.tile_begin = B[b].t0;
+        db.tile_end = B[b].t1;
+        const int64_t nbt = B[b].t1 - B[b].t0, i0 = B[b].t0 - t_lo;
+        std::vector<int64_t> off(nbt + 1);
+        rc = frs::encode_job(ctx, &db, dev_raster, ctx->arena_stage.as<uint8_t>() + aoff, bound - aoff, off.data(),
+                             tile_min + i0, tile_max + i0, stream_bps);
+        if (rc) break;
+        const int64_t nbytes = off[nbt];
+        if (aoff + nbytes > arena_cap) {
+            tile_off[nbt + i0] = aoff + nbytes;
+            ctx->err = "arena too small";
+            rc = FRS_E_NOSPACE;
+            break;
+        }
+        for (int64_t i = 0; i <= nbt; i++) tile_off[i0 + i] = aoff + off[i];
+        FRS_HIP(hipEventRecord(down, ctx->stream));
+        FRS_HIP(hipStreamWaitEvent(ctx->d2h_stream, down, 0));
+        FRS_HIP(hipMemcpyAsync(arena_host + aoff, ctx->arena_stage.as<uint8_t>() + aoff, (size_t)nbytes,
+                               hipMemcpyDeviceToHost, ctx->d2h_stream));
+        aoff += nbytes;
+    }
+    hipStreamSynchronize(ctx->h2d_stream);
+    hipStreamSynchronize(ctx->d2h_stream);
+    for (auto &e : up) hipEventDestroy(e);
+    hipEventDestroy(down);
+    return rc;
+}
+
+extern "C" {
+
 int frs_encode_tiles(frs_ctx *ctx, const frs_encode_desc *desc, const void *raster_host, uint8_t *arena_host,
                      int64_t arena_cap, int64_t *tile_off, double *tile_min, double *tile_max, int32_t *stream_bps) {
     if (!ctx) return FRS_E_ARG;
@@ -173,6 +295,15 @@ int frs_encode_tiles(frs_ctx *ctx, const frs_encode_desc *desc, const void *rast
     const int64_t nb = desc->nbands > 1 ? desc->band0 + desc->nbands : desc->band0 + 1;
     const int64_t elems = (nb - 1) * desc->band_stride + (desc->height - 1) * desc->row_stride + desc->width;
     const size_t rbytes = (size_t)elems * es;
+    // large single-band jobs of several tile rows: batched, overlapped transfers (create-streaming band 1)
+    const int64_t tcols = (desc->width + desc->tile_w - 1) / desc->tile_w;
+    const int64_t trows = (desc->tile_end - 1) / tcols - desc->tile_begin / tcols + 1;
+    const int64_t trow_bytes = (int64_t)desc->tile_h * desc->row_stride * es;
+    if (desc->nbands == 1 && trows >= 4 && rbytes >= ((size_t)64 << 20)) {
+        const int64_t batch_rows = std::max<int64_t>(1, std::min<int64_t>(trows / 4, ((int64_t)256 << 20) / trow_bytes));
+        return encode_tiles_batched(ctx, desc, static_cast<const uint8_t *>(raster_host), (size_t)es, arena_host,
+                                    arena_cap, tile_off, tile_min, tile_max, stream_bps, batch_rows);
+    }
     FRS_HIP(ctx->raster_stage.ensure(rbytes));
     FRS_HIP(hipMemcpyAsync(ctx->raster_stage.ptr, raster_host, rbytes, hipMemcpyHostToDevice, ctx->stream));
     const int64_t bound = frs::arena_bound(desc);

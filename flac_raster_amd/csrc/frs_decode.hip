@@ -96,13 +96,13 @@ __device__ FrameHdr parse_header(const uint8_t *blob, int64_t p, int64_t end, in
 }
 
 // ---------------------------------------------------------------------------------- candidate selection
-// One pass over the blob: a block takes 64 KB (256 contiguous bytes per thread, 16-byte loads), flags the bytes that
+// One pass over the blob: a block takes 64 KB (16 KB per wave, coalesced 16-byte loads: sel_masks_co), flags the bytes that
 // start a sync code with a parseable CRC-8-correct header, and writes their positions, in order, at its
 // exclusive prefix -- found by decoupled look-back over the blocks' published counts, 64 predecessors per step
 // (one wave).  Blocks take their ordinal from a ticket (the block that draws the last ticket re-arms the counter
 // for the next call), so a predecessor is always resident or done.  Status word: [63:40] call epoch, [39:38]
 // flag, [37:0] count; words of another epoch read as "not published", so the buffer is never cleared.
-constexpr int kSelThreads = 256, kSelPerThread = 64, kSelChunks = 4, kSelBytes = kSelThreads * kSelPerThread * kSelChunks;
+constexpr int kSelThreads = 256, kSelBytes = 64 * 1024;  // 4 waves x 16 KB per block
 constexpr uint64_t kSelAgg = 1ull << 38, kSelIncl = 2ull << 38, kSelVal = (1ull << 38) - 1;
 
 __device__ inline int64_t wave_sum_i64(int64_t v) {
@@ -111,50 +111,89 @@ __device__ inline int64_t wave_sum_i64(int64_t v) {
     return v;
 }
 
-// Candidate flags of the kSelChunks * 64 bytes at aligned offset qt (byte q of the 16-byte aligned view is
-// blob[q - lead]; a 16-byte line holding a blob byte is mapped): bit j of masks[ch] marks the sync code with a
-// parseable, CRC-8-correct header at qt + 64 ch + j.  Returns the number of candidates.
-__device__ inline int sel_masks(const uint8_t *blob, int64_t nbytes, const int64_t *soff, int ns, int channels,
-                                int stream_bps, int64_t qt, uint64_t *masks) {
+// Coalesced candidate flags: wave w of a 64 KB block takes the contiguous 16 KB at qw = block base + 16 KB w; step k
+// of it is the 1 KB at qw + 1024 k, lane L its 16 bytes at + 16 L (one fully coalesced 16-byte load per lane and
+// step), and the byte after them comes from lane L + 1 (lane 63: the next step's lane 0, or one guarded byte after
+// the last step).  Bit j of m[k] marks a sync code with a parseable, CRC-8-correct header at qw + 1024 k + 16 L + j,
+// so candidates are ordered by (k, lane, j).  Returns the lane's candidate count.
+constexpr int kSelSteps = kSelBytes / (kSelThreads / 64) / 1024;  // 16 steps of 1 KB per wave
+static_assert(kSelSteps == 16, "64 KB blocks of 4 waves");
+__device__ inline int sel_masks_co(const uint8_t *blob, int64_t nbytes, const int64_t *soff, int ns, int channels,
+                                   int stream_bps, int64_t qw, int lane, uint32_t *m) {
     const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
     const uint8_t *base = blob - lead;
     const int64_t qend = nbytes + lead;
+    uint4 v[kSelSteps];
+#pragma unroll
+    for (int k = 0; k < kSelSteps; k++) {
+        const int64_t q = qw + 1024 * k + 16 * lane;
+        v[k] = q < qend ? *reinterpret_cast<const uint4 *>(base + q) : make_uint4(0, 0, 0, 0);
+    }
+    const int64_t qlast = qw + 1024 * kSelSteps;  // the byte after the wave's 16 KB
+    const uint32_t after = (lane == 63 && qlast < qend) ? base[qlast] : 0u;
     int cnt = 0;
 #pragma unroll
-    for (int ch = 0; ch < kSelChunks; ch++) {
-        const int64_t q0 = qt + kSelPerThread * ch;
-        uint32_t w[kSelPerThread / 4 + 1];
+    for (int k = 0; k < kSelSteps; k++) {
+        // first byte of the next 16 bytes: lane L + 1's word 0 (lane 63: next step's lane 0)
+        uint32_t nx = (uint32_t)__shfl_down((int)v[k].x, 1);
+        const uint32_t n0 = k + 1 < kSelSteps ? (uint32_t)__builtin_amdgcn_readlane((int)v[k + 1 < kSelSteps ? k + 1 : k].x, 0)
+                                              : after;
+        if (lane == 63) nx = n0;
+        const uint32_t w[5] = {v[k].x, v[k].y, v[k].z, v[k].w, nx & 0xFFu};
+        uint32_t mask = 0;
+        const int64_t q0 = qw + 1024 * k + 16 * lane;
 #pragma unroll
-        for (int v = 0; v < kSelPerThread / 16; v++) {
-            uint4 x = make_uint4(0, 0, 0, 0);
-            if (q0 + 16 * v < qend) x = *reinterpret_cast<const uint4 *>(base + q0 + 16 * v);
-            w[4 * v] = x.x;
-            w[4 * v + 1] = x.y;
-            w[4 * v + 2] = x.z;
-            w[4 * v + 3] = x.w;
-        }
-        w[kSelPerThread / 4] = (q0 + kSelPerThread < qend) ? base[q0 + kSelPerThread] : 0u;  // the byte after
-        uint64_t mask = 0;
-#pragma unroll
-        for (int k = 0; k < kSelPerThread / 4; k++) {
-            const uint32_t x = w[k];
+        for (int i = 0; i < 4; i++) {
+            const uint32_t x = w[i];
             if (((~x) - 0x01010101u) & x & 0x80808080u) {  // some byte is 0xFF
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const uint32_t b0 = (x >> (8 * j)) & 0xFF;
-                    const uint32_t b1 = j < 3 ? (x >> (8 * j + 8)) & 0xFF : w[k + 1] & 0xFF;
-                    const int64_t p = q0 + 4 * k + j - lead;
+                    const uint32_t b1 = j < 3 ? (x >> (8 * j + 8)) & 0xFF : w[i + 1] & 0xFF;
+                    const int64_t p = q0 + 4 * i + j - lead;
                     if (b0 == 0xFF && (b1 & 0xFE) == 0xF8 && p >= 0 && p + 1 < nbytes) {
-                        const int s = stream_of(soff, ns, p);
-                        if (parse_header(blob, p, soff[s + 1], channels, stream_bps).ok) mask |= 1ull << (4 * k + j);
+                        const int st = stream_of(soff, ns, p);
+                        if (parse_header(blob, p, soff[st + 1], channels, stream_bps).ok) mask |= 1u << (4 * i + j);
                     }
                 }
             }
         }
-        masks[ch] = mask;
-        cnt += __builtin_popcountll(mask);
+        m[k] = mask;
+        cnt += __builtin_popcount(mask);
     }
     return cnt;
+}
+
+__device__ inline int wave_excl_scan_i32(int v, int lane, int &total) {
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    total = __builtin_amdgcn_readlane(x, 63);
+    return x - v;
+}
+
+// candidate positions of one wave in (k, lane, j) order from output index `base`; past the cap only counted
+__device__ inline void sel_emit_co(const uint32_t *m, int64_t qw, int lane, int lead, int64_t base, int64_t *cpos,
+                                   int64_t cap) {
+#pragma unroll
+    for (int k = 0; k < kSelSteps; k++) {
+        int tot;
+        const int ex = wave_excl_scan_i32(__builtin_popcount(m[k]), lane, tot);
+        if (tot) {
+            int64_t idx = base + ex;
+            uint32_t mask = m[k];
+            while (mask) {
+                const int j = __builtin_ctz(mask);
+                mask &= mask - 1;
+                if (idx < cap) cpos[idx] = qw + 1024 * k + 16 * lane + j - lead;
+                idx++;
+            }
+        }
+        base += tot;
+    }
 }
 
 __global__ void __launch_bounds__(kSelThreads) k_sync_select(const uint8_t *blob, int64_t nbytes, const int64_t *soff,
@@ -172,17 +211,12 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_select(const uint8_t *blob
     __syncthreads();
     const int64_t ord = s_ord;
     const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
-    // thread t owns the contiguous kSelChunks * 64 bytes at ord * kSelBytes + 256 t (its candidates stay in order)
-    const int64_t qt = ord * kSelBytes + (int64_t)(kSelPerThread * kSelChunks) * t;
-    uint64_t masks[kSelChunks];
-    const int cnt = sel_masks(blob, nbytes, soff, ns, channels, stream_bps, qt, masks);
-    int x = cnt;
+    const int64_t qw = ord * kSelBytes + (int64_t)(kSelBytes / 4) * wv;
+    uint32_t m[kSelSteps];
+    int cnt = sel_masks_co(blob, nbytes, soff, ns, channels, stream_bps, qw, lane, m);
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) s_wsum[wv] = x;
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+    if (lane == 0) s_wsum[wv] = cnt;
     __syncthreads();
     int wbase = 0, tot = 0;
 #pragma unroll
@@ -231,17 +265,7 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_select(const uint8_t *blob
         }
     }
     __syncthreads();
-    int64_t idx = s_base + wbase + x - cnt;
-#pragma unroll
-    for (int ch = 0; ch < kSelChunks; ch++) {
-        uint64_t mask = masks[ch];
-        while (mask) {  // positions in increasing order; past the cap only counted
-            const int j = __builtin_ctzll(mask);
-            mask &= mask - 1;
-            if (idx < cap) cpos[idx] = qt + kSelPerThread * ch + j - lead;
-            idx++;
-        }
-    }
+    sel_emit_co(m, qw, lane, lead, s_base + wbase, cpos, cap);
 }
 
 // Large ranges (a whole arena): the single pass above serialises on its look-back (the inclusive prefix advances one
@@ -252,9 +276,9 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_count(const uint8_t *blob,
                                                           int ns, int channels, int stream_bps, int32_t *bcount) {
     __shared__ int s_wsum[kSelThreads / 64];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    uint64_t masks[kSelChunks];
-    int c = sel_masks(blob, nbytes, soff, ns, channels, stream_bps,
-                      (int64_t)blockIdx.x * kSelBytes + (int64_t)(kSelPerThread * kSelChunks) * t, masks);
+    uint32_t m[kSelSteps];
+    int c = sel_masks_co(blob, nbytes, soff, ns, channels, stream_bps,
+                         (int64_t)blockIdx.x * kSelBytes + (int64_t)(kSelBytes / 4) * wv, lane, m);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
     if (lane == 0) s_wsum[wv] = c;
@@ -302,31 +326,17 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_scatter(const uint8_t *blo
     __shared__ int s_wsum[kSelThreads / 64];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
-    const int64_t qt = (int64_t)blockIdx.x * kSelBytes + (int64_t)(kSelPerThread * kSelChunks) * t;
-    uint64_t masks[kSelChunks];
-    const int cnt = sel_masks(blob, nbytes, soff, ns, channels, stream_bps, qt, masks);
-    int x = cnt;
+    const int64_t qw = (int64_t)blockIdx.x * kSelBytes + (int64_t)(kSelBytes / 4) * wv;
+    uint32_t m[kSelSteps];
+    int c = sel_masks_co(blob, nbytes, soff, ns, channels, stream_bps, qw, lane, m);
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) s_wsum[wv] = x;
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if (lane == 0) s_wsum[wv] = c;
     __syncthreads();
     int wbase = 0;
 #pragma unroll
     for (int k = 0; k < kSelThreads / 64; k++) wbase += k < wv ? s_wsum[k] : 0;
-    int64_t idx = bbase[blockIdx.x] + wbase + x - cnt;
-#pragma unroll
-    for (int ch = 0; ch < kSelChunks; ch++) {
-        uint64_t mask = masks[ch];
-        while (mask) {
-            const int j = __builtin_ctzll(mask);
-            mask &= mask - 1;
-            if (idx < cap) cpos[idx] = qt + kSelPerThread * ch + j - lead;
-            idx++;
-        }
-    }
+    sel_emit_co(m, qw, lane, lead, bbase[blockIdx.x] + wbase, cpos, cap);
 }
 
 // Fused de-normalisation of decoded samples (converter.py:88-110 after pyflac + soundfile's PCM_16 WAV round

@@ -74,6 +74,8 @@ struct frs_ctx {
     // host staging (pinned)
     DevBuf raster_stage, arena_stage;  // device copies for the host-pointer entry points
     HostPin pin;                       // pinned staging of the fast encode path (tiles, wave table, results)
+    HostPin ring[2];                   // pinned upload ring of the batched host-pointer encode (frs_encode_tiles)
+    hipStream_t h2d_stream = nullptr, d2h_stream = nullptr;  // its copy engines' streams (created on first use)
     DevBuf host_pack;                  // device side of the packed fast-path results
     // decode scratch
     DevBuf dec_cand, dec_count, dec_pcm, dec_soff, dec_next, dec_status, dec_fb, dec_sel, dec_chass;

@@ -217,3 +217,23 @@ def test_multichannel_fast_path_matches_oracle(gpu_ctx, dtype, bands, shape, see
     assert bps == o_bps == 16
     assert arena[:off[-1]].tobytes() == ref
     assert (mn[0], mx[0]) == (o_mn, o_mx)
+
+
+def test_host_encode_batched_tile_ranges(gpu_ctx):
+    """frs_encode_tiles on a large single band goes through the batched, overlapped upload path (tile-row batches,
+    pinned ring, separate copy streams); a tile range that starts and ends mid-row must give the same bytes,
+    offsets and min/max as the whole job's corresponding tiles, and the whole job must equal the oracle."""
+    rng = np.random.default_rng(21)
+    H, W, T = 6000, 6000, 512
+    y, x = np.meshgrid(np.linspace(0, 20, H, dtype=np.float32), np.linspace(0, 20, W, dtype=np.float32),
+                       indexing="ij")
+    band = (1000 + 300 * np.sin(x * 0.8) * np.cos(y * 0.3) + 50 * rng.random((H, W), dtype=np.float32)).astype(np.int16)
+    arena, off, mn, mx, _ = _gpu_tiles(gpu_ctx, band, T)
+    o_arena, o_off, o_mn, o_mx = O.encode_tiles(band, T, threads=8)
+    assert np.array_equal(off, o_off) and arena.tobytes() == o_arena.tobytes()
+    d = gpu_ctx.make_desc(H, W, band.dtype, tile_h=T, tile_w=T, sample_rate=44100, bits_per_sample=16,
+                          tile_begin=5, tile_end=131)
+    a2, off2, mn2, mx2, _ = gpu_ctx.encode_tiles_host(band, d)
+    assert np.array_equal(off2, off[5:132] - off[5])
+    assert a2.tobytes() == arena[off[5]:off[131]].tobytes()
+    assert np.array_equal(mn2, mn[5:131]) and np.array_equal(mx2, mx[5:131])

@@ -12,6 +12,6 @@ timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch -
 timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write -o run -- $B > $O/write.log 2>&1 || exit 1
 timeout -s KILL 400 rocprofv3 --pmc SQ_INSTS_VALU --output-format csv -d $O/valu -o run -- $B > $O/valu.log 2>&1 || exit 1
 python3 tools/rocprof_summary.py $(find $O/kt -name "*kernel_stats.csv" | head -1) > $O/kernel_stats.md
-python3 tools/pmc_traffic.py $O/fetch $O/write $O/pmc_traffic.json --label r2 --pixels 1600000000 --valu $O/valu > $O/pmc.txt
+python3 tools/pmc_traffic.py $O/fetch $O/write $O/pmc_traffic.json --label r2 --pixels 1600000000 --valu $O/valu --lib flac_raster_amd/libflac_raster_amd.so > $O/pmc.txt
 tail -3 $O/kt.log
 cat $O/kernel_stats.md $O/pmc.txt

@@ -2,13 +2,17 @@
 """HBM traffic per kernel launch from rocprofv3 --pmc passes (run_counter_collection.csv).
 
 Usage: pmc_traffic.py FETCH_DIR WRITE_DIR OUT.json [--label TEXT] [--pixels PIXELS_PER_LAUNCH] [--valu DIR]
+                      [--lib PATH]
 
 FETCH_SIZE and WRITE_SIZE are in KB per dispatch (summed over TCC instances here).  On gfx950 FETCH_SIZE
 counts half the bytes of wide streaming reads, so it is doubled (MI355X_MICROARCH.md, "HBM [CDNA4]");
 WRITE_SIZE is taken as is.  The JSON maps kernel short names to mean bytes per launch, and bench.py copies
 the dominant kernel's figure into roofline.traffic.  --valu DIR (a `--pmc SQ_INSTS_VALU` pass) adds the mean
 wave-level VALU instructions per launch, which bench.py turns into roofline.issue (VALU issue rate vs peak).
+--lib PATH stamps the summary with the sha256 of the profiled library: bench.py uses the counters only when the
+library it loaded has the same hash (counters of another build are never reported as this build's).
 """
+import hashlib
 import csv
 import json
 import sys
@@ -46,8 +50,11 @@ def main():
     if "--valu" in sys.argv:
         for k, v in per_dispatch(sys.argv[sys.argv.index("--valu") + 1], "SQ_INSTS_VALU").items():
             kernels.setdefault(k, {})["valu_insts"] = v
-    json.dump({"label": label, "pixels_per_launch": pixels, "fetch_correction": 2.0, "kernels": kernels},
-              open(dst, "w"), indent=1)
+    lib_sha = None
+    if "--lib" in sys.argv:
+        lib_sha = hashlib.sha256(Path(sys.argv[sys.argv.index("--lib") + 1]).read_bytes()).hexdigest()
+    json.dump({"label": label, "pixels_per_launch": pixels, "fetch_correction": 2.0, "lib_sha256": lib_sha,
+               "kernels": kernels}, open(dst, "w"), indent=1)
     for k, v in kernels.items():
         print(f"{k}: read {v.get('read_bytes', 0) / 1e9:.3f} GB write {v.get('write_bytes', 0) / 1e9:.3f} GB "
               f"valu {v.get('valu_insts', 0):.4g}")
