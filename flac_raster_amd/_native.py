@@ -31,7 +31,7 @@ EXPORTS = (
     "frs_encode_arena_bound", "frs_encode_tiles_device", "frs_encode_tiles",
     "frs_decode_frames_device", "frs_decode_frames", "frs_decode_tiles_device", "frs_decode_tiles",
     "frs_denormalize_device", "frs_denormalize",
-    "frs_dev_malloc", "frs_dev_free", "frs_memcpy_h2d", "frs_memcpy_d2h", "frs_ctx_sync",
+    "frs_dev_malloc", "frs_dev_free", "frs_host_malloc", "frs_host_free", "frs_memcpy_h2d", "frs_memcpy_d2h", "frs_ctx_sync",
     "frs_synth_raster_device", "frs_ctx_stream", "frs_profile_enable", "frs_profile_avg_ms",
     "frs_profile_reset", "frs_comm_unique_id", "frs_comm_init", "frs_comm_destroy", "frs_comm_allgather_i64",
 )
@@ -117,6 +117,10 @@ def load_library(path: Optional[os.PathLike] = None):
         L.frs_dev_malloc.argtypes = [ctxp, i64]
         L.frs_dev_free.restype = None
         L.frs_dev_free.argtypes = [ctxp, vp]
+        L.frs_host_malloc.restype = vp
+        L.frs_host_malloc.argtypes = [ctxp, i64]
+        L.frs_host_free.restype = None
+        L.frs_host_free.argtypes = [ctxp, vp]
         L.frs_memcpy_h2d.restype = i32
         L.frs_memcpy_h2d.argtypes = [ctxp, vp, vp, i64]
         L.frs_memcpy_d2h.restype = i32
@@ -203,9 +207,11 @@ class Context:
             raise NativeUnavailable(f"frs_ctx_create({device}) failed: {STATUS.get(rc, rc)}")
         self.handle = h
         self.device = device
+        self._pin_ptr, self._pin_bytes = None, 0
 
     def close(self):
         if getattr(self, "handle", None):
+            self.release_pinned()
             self.lib.frs_ctx_destroy(self.handle)
             self.handle = None
 
@@ -236,6 +242,25 @@ class Context:
     def sync(self):
         self._check(self.lib.frs_ctx_sync(self.handle))
 
+    def pinned(self, nbytes: int) -> np.ndarray:
+        """uint8[nbytes] view of this context's page-locked host buffer (frs_host_malloc), grown on demand and reused
+        by the next call: the arena of a large host encode lands in it at DMA rate.  Valid until the next call or
+        release_pinned()."""
+        if nbytes > self._pin_bytes:
+            self.release_pinned()
+            size = max(int(nbytes), 2 * self._pin_bytes if self._pin_bytes else 0)
+            p = self.lib.frs_host_malloc(self.handle, size)
+            if not p:
+                raise FrsError(-2, self.last_error())  # FRS_E_HIP
+            self._pin_ptr, self._pin_bytes = p, size
+        buf = (ctypes.c_uint8 * self._pin_bytes).from_address(self._pin_ptr)
+        return np.frombuffer(buf, dtype=np.uint8, count=int(nbytes))
+
+    def release_pinned(self):
+        if self._pin_ptr:
+            self.lib.frs_host_free(self.handle, self._pin_ptr)
+            self._pin_ptr, self._pin_bytes = None, 0
+
     # ---- encode
     @staticmethod
     def make_desc(height, width, dtype, *, row_stride=None, band_stride=None, band0=0, nbands=1,
@@ -259,8 +284,10 @@ class Context:
     def arena_bound(self, desc: EncodeDesc) -> int:
         return int(self.lib.frs_encode_arena_bound(ctypes.byref(desc)))
 
-    def encode_tiles_host(self, raster: np.ndarray, desc: EncodeDesc) -> Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray, int]:
-        """Host-pointer encode.  Returns (arena uint8, tile_off int64[n+1], tile_min, tile_max, stream_bps)."""
+    def encode_tiles_host(self, raster: np.ndarray, desc: EncodeDesc, pinned: bool = False
+                          ) -> Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray, int]:
+        """Host-pointer encode.  Returns (arena uint8, tile_off int64[n+1], tile_min, tile_max, stream_bps).
+        pinned=True: the arena is a view of the context's page-locked buffer (see pinned())."""
         r = np.ascontiguousarray(raster)
         n = desc.tile_end - desc.tile_begin
         off = np.zeros(n + 1, dtype=np.int64)
@@ -268,7 +295,7 @@ class Context:
         mx = np.zeros(max(n, 1), dtype=np.float64)
         bps = ctypes.c_int32()
         cap = self.arena_bound(desc)
-        arena = np.empty(cap, dtype=np.uint8)
+        arena = self.pinned(cap) if pinned else np.empty(cap, dtype=np.uint8)
         self._check(self.lib.frs_encode_tiles(
             self.handle, ctypes.byref(desc), _p(r), _p(arena), cap, off.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
             mn.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), mx.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),

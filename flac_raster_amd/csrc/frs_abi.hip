@@ -493,6 +493,25 @@ void frs_dev_free(frs_ctx *ctx, void *ptr) {
     hipFree(ptr);
 }
 
+void *frs_host_malloc(frs_ctx *ctx, int64_t bytes) {
+    if (!ctx || bytes <= 0) return nullptr;
+    if (hipSetDevice(ctx->device) != hipSuccess) return nullptr;
+    void *p = nullptr;
+    hipError_t e = hipHostMalloc(&p, (size_t)bytes, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        ctx->err = std::string("hipHostMalloc: ") + hipGetErrorString(e);
+        return nullptr;
+    }
+    return p;
+}
+
+void frs_host_free(frs_ctx *ctx, void *ptr) {
+    if (!ctx || !ptr) return;
+    hipSetDevice(ctx->device);
+    hipDeviceSynchronize();  // (copies on the context's side streams may still read or write it)
+    hipHostFree(ptr);
+}
+
 int frs_memcpy_h2d(frs_ctx *ctx, void *dst_dev, const void *src_host, int64_t bytes) {
     if (!ctx) return FRS_E_ARG;
     if (bytes <= 0) return FRS_OK;

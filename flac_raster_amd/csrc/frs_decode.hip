@@ -13,6 +13,7 @@
 // are never used); the frame decoders decode the true frames and check that the subframes end exactly at
 // the CRC footer.  Positions are 64-bit throughout (a C4 arena is 3.1 GB); candidate indices are int32
 // and the candidate buffer is capped below 2^31.
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -118,17 +119,98 @@ __device__ inline int64_t wave_sum_i64(int64_t v) {
 // so candidates are ordered by (k, lane, j).  Returns the lane's candidate count.
 constexpr int kSelSteps = kSelBytes / (kSelThreads / 64) / 1024;  // 16 steps of 1 KB per wave
 static_assert(kSelSteps == 16, "64 KB blocks of 4 waves");
+
+// CRC-8 (poly 0x07) of one byte folded into c, bitwise (no table: the header check runs from registers)
+__device__ inline uint32_t crc8_byte(uint32_t c, uint32_t b) {
+    c ^= b;
+#pragma unroll
+    for (int k = 0; k < 8; k++) c = (c & 0x80u) ? ((c << 1) ^ 0x07u) & 0xFFu : (c << 1) & 0xFFu;
+    return c;
+}
+
+// parse_header on the 16 bytes h (little-endian dwords) that start at a sync code, `avail` bytes of the blob from
+// there: the same acceptance test (RFC 9639 9.1: reserved codes, UTF-8 frame number, CRC-8, channel count).
+__device__ inline bool header_ok_regs(const uint32_t *h, int64_t avail, int channels) {
+    auto B = [&](int t) -> uint32_t { return (h[t >> 2] >> (8 * (t & 3))) & 0xFFu; };
+    if (avail < 6) return false;
+    const uint32_t b2 = B(2), b3 = B(3);
+    const uint32_t bsc = b2 >> 4, src = b2 & 15, chass = b3 >> 4, ssc = (b3 >> 1) & 7;
+    if (bsc == 0 || src == 15 || chass > 10 || ssc == 3 || (b3 & 1)) return false;
+    const uint32_t v = B(4);
+    int extra = 0;
+    if (v & 0x80) {
+        if ((v & 0xE0) == 0xC0) extra = 1;
+        else if ((v & 0xF0) == 0xE0) extra = 2;
+        else if ((v & 0xF8) == 0xF0) extra = 3;
+        else if ((v & 0xFC) == 0xF8) extra = 4;
+        else if ((v & 0xFE) == 0xFC) extra = 5;
+        else return false;
+    }
+    int q = 5;
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+        if (i < extra) {
+            if (q >= avail || (B(5 + i) & 0xC0) != 0x80) return false;
+            q++;
+        }
+    }
+    if (bsc == 6) {
+        if (q >= avail) return false;
+        q += 1;
+    } else if (bsc == 7) {
+        if (q + 1 >= avail) return false;
+        q += 2;
+    }
+    if (src == 12) q += 1;
+    else if (src == 13 || src == 14) q += 2;
+    if (q >= avail) return false;  // q <= 14: the CRC-8 byte is h's byte q
+    uint32_t c = 0;
+#pragma unroll
+    for (int t = 0; t < 15; t++)
+        if (t < q) c = crc8_byte(c, B(t));
+    if (c != B(q)) return false;
+    const int nch = chass < 8 ? (int)chass + 1 : 2;
+    return nch == channels;
+}
+
+// dword idx (0..7) of the 32-byte window w0 | w1, idx dynamic (a select chain, no register indexing)
+__device__ inline uint32_t win_dword(const uint4 &w0, const uint4 &w1, int idx) {
+    uint32_t r = w0.x;
+    r = idx == 1 ? w0.y : r;
+    r = idx == 2 ? w0.z : r;
+    r = idx == 3 ? w0.w : r;
+    r = idx == 4 ? w1.x : r;
+    r = idx == 5 ? w1.y : r;
+    r = idx == 6 ? w1.z : r;
+    r = idx == 7 ? w1.w : r;
+    return r;
+}
+
+// Coalesced candidate flags: wave w of a 64 KB block takes the contiguous 16 KB at qw = block base + 16 KB w; step k
+// of it is the 1 KB at qw + 1024 k, lane L its 16 bytes at + 16 L (one fully coalesced 16-byte load per lane and
+// step).  Bit j of m[k] marks a sync code with a parseable, CRC-8-correct header at qw + 1024 k + 16 L + j, so
+// candidates are ordered by (k, lane, j).  The header check runs on registers: a step with a sync pattern fetches
+// each lane's successor 16 bytes (lane L + 1; lane 63: the next step's lane 0) by shuffles, so a header (<= 16 bytes)
+// lies in the lane's 32-byte window -- no dependent global loads, which had made the pass latency-bound (~1 TB/s).
+// Only a header starting in the wave's last 16 bytes takes the global parse.  Headers are bounded by the blob end
+// (not the stream end: a header straddling a stream boundary becomes a candidate whose CRC span never verifies).
+// Returns the lane's candidate count.
 __device__ inline int sel_masks_co(const uint8_t *blob, int64_t nbytes, const int64_t *soff, int ns, int channels,
                                    int stream_bps, int64_t qw, int lane, uint32_t *m) {
     const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
     const uint8_t *base = blob - lead;
     const int64_t qend = nbytes + lead;
+    // all 16 loads in flight at once: unconditional (a chunk past the end re-reads chunk 0 and is zeroed after) --
+    // a guarded load per step compiled to 16 load/wait round trips
     uint4 v[kSelSteps];
 #pragma unroll
     for (int k = 0; k < kSelSteps; k++) {
         const int64_t q = qw + 1024 * k + 16 * lane;
-        v[k] = q < qend ? *reinterpret_cast<const uint4 *>(base + q) : make_uint4(0, 0, 0, 0);
+        v[k] = *reinterpret_cast<const uint4 *>(base + (q < qend ? q : 0));
     }
+#pragma unroll
+    for (int k = 0; k < kSelSteps; k++)
+        if (qw + 1024 * k + 16 * lane >= qend) v[k] = make_uint4(0, 0, 0, 0);
     const int64_t qlast = qw + 1024 * kSelSteps;  // the byte after the wave's 16 KB
     const uint32_t after = (lane == 63 && qlast < qend) ? base[qlast] : 0u;
     int cnt = 0;
@@ -140,8 +222,8 @@ __device__ inline int sel_masks_co(const uint8_t *blob, int64_t nbytes, const in
                                               : after;
         if (lane == 63) nx = n0;
         const uint32_t w[5] = {v[k].x, v[k].y, v[k].z, v[k].w, nx & 0xFFu};
-        uint32_t mask = 0;
-        const int64_t q0 = qw + 1024 * k + 16 * lane;
+        // sync patterns (0xFF then 0xF8 / 0xF9) of this lane's 16 bytes
+        uint32_t raw = 0;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
             const uint32_t x = w[i];
@@ -150,12 +232,44 @@ __device__ inline int sel_masks_co(const uint8_t *blob, int64_t nbytes, const in
                 for (int j = 0; j < 4; j++) {
                     const uint32_t b0 = (x >> (8 * j)) & 0xFF;
                     const uint32_t b1 = j < 3 ? (x >> (8 * j + 8)) & 0xFF : w[i + 1] & 0xFF;
-                    const int64_t p = q0 + 4 * i + j - lead;
-                    if (b0 == 0xFF && (b1 & 0xFE) == 0xF8 && p >= 0 && p + 1 < nbytes) {
-                        const int st = stream_of(soff, ns, p);
-                        if (parse_header(blob, p, soff[st + 1], channels, stream_bps).ok) mask |= 1u << (4 * i + j);
-                    }
+                    if (b0 == 0xFF && (b1 & 0xFE) == 0xF8) raw |= 1u << (4 * i + j);
                 }
+            }
+        }
+        uint32_t mask = 0;
+        if (__ballot(raw != 0)) {  // (wave-uniform, ~3 % of steps) the successor 16 bytes of every lane
+            // lane L reads lane L + 1's chunk; lane 63 lane 0's chunk of the next step (all lanes shuffle: no
+            // cross-lane read inside a divergent branch)
+            const uint4 &vn = v[k + 1 < kSelSteps ? k + 1 : k];
+            const uint4 src = lane == 0 ? vn : v[k];
+            const int from = (lane + 1) & 63;
+            uint4 nv;
+            nv.x = (uint32_t)__shfl((int)src.x, from);
+            nv.y = (uint32_t)__shfl((int)src.y, from);
+            nv.z = (uint32_t)__shfl((int)src.z, from);
+            nv.w = (uint32_t)__shfl((int)src.w, from);
+            const int64_t q0 = qw + 1024 * k + 16 * lane;
+            const bool regs_ok = k + 1 < kSelSteps || lane < 63;  // the window holds the next 16 bytes
+            while (raw) {
+                const int j = __builtin_ctz(raw);
+                raw &= raw - 1;
+                const int64_t p = q0 + j - lead;
+                if (p < 0 || p + 1 >= nbytes) continue;
+                bool ok;
+                if (regs_ok) {
+                    uint32_t h[4];
+                    const int wi = j >> 2, sh = j & 3;
+#pragma unroll
+                    for (int d = 0; d < 4; d++) {
+                        const uint32_t lo = win_dword(v[k], nv, wi + d), hi = win_dword(v[k], nv, min(wi + d + 1, 7));
+                        h[d] = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)sh);
+                    }
+                    ok = header_ok_regs(h, min<int64_t>(nbytes - p, 16), channels);
+                } else {
+                    const int st = stream_of(soff, ns, p);
+                    ok = parse_header(blob, p, soff[st + 1], channels, stream_bps).ok;
+                }
+                if (ok) mask |= 1u << j;
             }
         }
         m[k] = mask;
@@ -566,6 +680,28 @@ __global__ void __launch_bounds__(256) k_span_crc_lane(const uint8_t *blob, cons
             };
             for (; b < stop && ((b + lead) & 3); b++) crc = ((crc << 8) & 0xFFFFu) ^ t4[0][((crc >> 8) ^ blob[b]) & 0xFF];
             for (; b + 4 <= stop && ((b + lead) & 15); b += 4) fold4(*reinterpret_cast<const uint32_t *>(abase + b + lead));
+            // whole 128-byte lines, all eight 16-byte loads issued together: a lane streams its own span, and with
+            // one 16-byte load per step the ~1500 concurrent streams of a CU evicted each line from L2 between its
+            // eight visits (PMC: 7x the span bytes fetched)
+            for (; b + 128 <= stop && ((b + lead) & 127); b += 16) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(abase + b + lead);
+                fold4(v.x);
+                fold4(v.y);
+                fold4(v.z);
+                fold4(v.w);
+            }
+            for (; b + 128 <= stop; b += 128) {
+                uint4 v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) v[u] = *reinterpret_cast<const uint4 *>(abase + b + lead + 16 * u);
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    fold4(v[u].x);
+                    fold4(v[u].y);
+                    fold4(v[u].z);
+                    fold4(v[u].w);
+                }
+            }
             for (; b + 16 <= stop; b += 16) {  // one 16-byte load per four dwords
                 const uint4 v = *reinterpret_cast<const uint4 *>(abase + b + lead);
                 fold4(v.x);
@@ -1775,26 +1911,35 @@ struct LaneReader {
     int n;                 // valid bits in c
     uint64_t qa, qb, qc;   // queued big-endian dwords, left-aligned (qa's high half first)
     int qw;                // dwords queued (<= 6)
-    uint64_t pa, pb;       // the chunk loaded a step ahead
+    uint4 praw;            // the chunk loaded a step ahead (raw little-endian; converted when it joins the queue)
+    int pval;              // its bytes before the stream end (16 unless the chunk crosses it)
     bool bad;
+    // The chunk at q as big-endian dword pairs, bytes at or past `end` zeroed.  Branch-free and unconditional: a guarded
+    // load compiled to a branch whose join waited for the load (vmcnt(0) at every chunk: no prefetch at all).  A chunk
+    // past the end re-reads the 16-byte-aligned chunk holding the last byte (never across a page) and is zeroed.
+    __device__ inline uint4 fetch(int64_t q, int &val) const {
+        const int64_t lastq = (end - 1 + lead) & ~(int64_t)15;
+        val = (int)max<int64_t>(0, min<int64_t>(16, end - (q - lead)));
+        return *reinterpret_cast<const uint4 *>(abase + (q <= lastq ? q : lastq));
+    }
+    __device__ static inline void convert(const uint4 &x, int val, uint64_t &a, uint64_t &b) {
+        auto keep = [&](uint32_t w, int d) -> uint32_t {  // dword d: bytes 4d..4d+3 (little-endian), zero past val
+            const int nb = val - 4 * d;
+            return nb >= 4 ? w : nb <= 0 ? 0u : (w & ((1u << (8 * nb)) - 1u));
+        };
+        a = ((uint64_t)__builtin_bswap32(keep(x.x, 0)) << 32) | __builtin_bswap32(keep(x.y, 1));
+        b = ((uint64_t)__builtin_bswap32(keep(x.z, 2)) << 32) | __builtin_bswap32(keep(x.w, 3));
+    }
     __device__ inline void load_chunk(int64_t q, uint64_t &a, uint64_t &b) const {
-        uint4 x;
-        if (q - lead + 16 <= end) {
-            x = *reinterpret_cast<const uint4 *>(abase + q);
-        } else {  // the stream's (and maybe the allocation's) last bytes: byte loads below `end` only
-            uint32_t v[4] = {0, 0, 0, 0};
-            for (int k = 0; k < 16; k++) {
-                const int64_t bpos = q - lead + k;
-                if (bpos >= 0 && bpos < end) v[k >> 2] |= (uint32_t)abase[q + k] << (8 * (k & 3));
-            }
-            x = make_uint4(v[0], v[1], v[2], v[3]);
-        }
-        a = ((uint64_t)__builtin_bswap32(x.x) << 32) | __builtin_bswap32(x.y);
-        b = ((uint64_t)__builtin_bswap32(x.z) << 32) | __builtin_bswap32(x.w);
+        int val;
+        const uint4 x = fetch(q, val);
+        convert(x, val, a, b);
     }
     // queue <- queue ++ prefetched chunk when at most two dwords are left (branch-free merge), next chunk in flight
     __device__ inline void top_up() {
         if (qw <= 2) {
+            uint64_t pa, pb;
+            convert(praw, pval, pa, pb);
             const uint64_t a1 = (qa & 0xFFFFFFFF00000000ull) | (pa >> 32);
             const uint64_t na = qw == 2 ? qa : qw == 1 ? a1 : pa;
             const uint64_t nb = qw == 2 ? pa : qw == 1 ? ((pa << 32) | (pb >> 32)) : pb;
@@ -1803,7 +1948,7 @@ struct LaneReader {
             qb = nb;
             qc = nc;
             qw += 4;
-            load_chunk(next, pa, pb);
+            praw = fetch(next, pval);
             next += 16;
             if (next - lead > end + 64) bad = true;  // runaway walk (corrupt data)
         }
@@ -1830,7 +1975,7 @@ struct LaneReader {
         load_chunk(q, qa, qb);
         qc = 0;
         qw = 4;
-        load_chunk(q + 16, pa, pb);
+        praw = fetch(q + 16, pval);
         next = q + 32;
         bad = false;
         const int r = (int)((pos + lead) & 15);
@@ -2319,9 +2464,11 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         int32_t *fbl = ctx->dec_fb.as<int32_t>();
         int *fbc = ncand + 3;
         const unsigned lg = (unsigned)((frames + 255) / 256);
+        // (experiment) FRS_DEC_LANE_LDS: dynamic LDS per work-group, i.e. a cap on the lane decoder's occupancy
+        static const size_t lane_lds = getenv("FRS_DEC_LANE_LDS") ? (size_t)atol(getenv("FRS_DEC_LANE_LDS")) : 0;
         const int okind = !fused ? kOutPcm : out_dtype == FRS_DT_I16 ? kOutI16 : out_dtype == FRS_DT_U16 ? kOutU16
                                    : out_dtype == FRS_DT_U8 ? kOutU8 : kOutAny;
-#define FRS_LANE(K) k_decode_frames_lane<K><<<lg, 256, 0, st>>>(blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, \
+#define FRS_LANE(K) k_decode_frames_lane<K><<<lg, 256, lane_lds, st>>>(blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, \
                                                               dchain, frames, bps, pcm_dev, blocksize, nvalid, dout, fbl, fbc)
         switch (okind) {
         case kOutPcm: FRS_LANE(kOutPcm); break;

@@ -286,6 +286,31 @@ class TiffFile:
                         out[j, lo - row0:hi - row0] = a[lo - sidx * rps:hi - sidx * rps, :, bsel]
         return out
 
+    def band_view(self, band: int = 0) -> Optional[np.ndarray]:
+        """Zero-copy (height, width) view of one band on the memory map, or None when the layout does not allow it
+        (compressed, predictor, tiled, pixel-interleaved multi-band, non-native byte order, or strips that are not
+        back to back in the file)."""
+        tags = self.tags
+        if self.comp != 1 or self.pred != 1 or 322 in tags or not self.file_dtype.isnative:
+            return None
+        if self.spp > 1 and self.planar != 2:
+            return None
+        H, W, isz = self.height, self.width, self.file_dtype.itemsize
+        rps = tags.get(278, (H,))[0]
+        offs, cnts = tags[273], tags[279]
+        nstrips = (H + rps - 1) // rps
+        k0 = band * nstrips
+        if len(offs) < k0 + nstrips:
+            return None
+        for i in range(nstrips):
+            rows = min(rps, H - i * rps)
+            k = k0 + i
+            if cnts[k] != rows * W * isz or (i and offs[k] != offs[k - 1] + cnts[k - 1]):
+                return None
+        if offs[k0] + H * W * isz > len(self._mm):
+            return None
+        return np.frombuffer(self._mm, dtype=self.file_dtype, count=H * W, offset=offs[k0]).reshape(H, W)
+
     def georef(self):
         """(transform, epsg, nodata, extra geokeys) with GDAL GTiff semantics (PixelIsArea default)."""
         tags = self.tags
@@ -337,10 +362,11 @@ def read(path) -> GeoRaster:
 
 def write(path, data: np.ndarray, transform: Optional[Affine] = None, epsg: Optional[int] = None,
           nodata: Optional[float] = None, compress: Optional[str] = None, predictor: int = 1,
-          tile: Optional[int] = None, planar: int = 1) -> None:
-    """Write (count, height, width) GTiff (GDAL-like layout): ~8 KB strips by default, or `tile` x `tile` tiles;
-    chunky (planar 1) or band-sequential (planar 2) samples; uncompressed or ``compress="deflate"`` with optional
-    horizontal differencing (predictor 2)."""
+          tile: Optional[int] = None, planar: int = 1, rows_per_strip: Optional[int] = None) -> None:
+    """Write (count, height, width) GTiff (GDAL-like layout): ~8 KB strips by default (or `rows_per_strip` rows), or
+    `tile` x `tile` tiles; chunky (planar 1) or band-sequential (planar 2) samples; uncompressed or
+    ``compress="deflate"`` with optional horizontal differencing (predictor 2).  Uncompressed strips are written
+    straight from the array (no staging copy: a multi-GB raster streams to the file)."""
     a = np.asarray(data)
     if a.ndim == 2:
         a = a[None]
@@ -359,6 +385,8 @@ def write(path, data: np.ndarray, transform: Optional[Affine] = None, epsg: Opti
         return zlib.compress(b, 6) if compress == "deflate" else b
 
     chunks: List[bytes] = []
+    direct = not tile and compress is None and predictor != 2  # strips written from array views
+    strips: List[np.ndarray] = []
     if tile:
         tw = th = int(tile)
         tx, ty = (W + tw - 1) // tw, (H + th - 1) // th
@@ -372,12 +400,17 @@ def write(path, data: np.ndarray, transform: Optional[Affine] = None, epsg: Opti
         rps = None
     else:
         row_bytes = W * cs * dt.itemsize
-        rps = max(1, min(H, 8192 // max(1, row_bytes)))
+        rps = int(rows_per_strip) if rows_per_strip else max(1, min(H, 8192 // max(1, row_bytes)))
+        rps = max(1, min(H, rps))
         nstrips = (H + rps - 1) // rps
         for pl in planes:
             for st in range(nstrips):
-                chunks.append(encode_chunk(pl[st * rps:(st + 1) * rps]))
-    total = sum(len(c) for c in chunks)
+                if direct:
+                    strips.append(pl[st * rps:(st + 1) * rps])
+                else:
+                    chunks.append(encode_chunk(pl[st * rps:(st + 1) * rps]))
+    sizes = [x.size * dt.itemsize for x in strips] if direct else [len(c) for c in chunks]
+    total = sum(sizes)
     big = total > 0xF0000000
     sfmt = 3 if dt.kind == "f" else (2 if dt.kind == "i" else 1)
     entries: List[Tuple[int, int, tuple]] = []
@@ -392,11 +425,11 @@ def write(path, data: np.ndarray, transform: Optional[Affine] = None, epsg: Opti
     add(259, 3, 8 if compress == "deflate" else 1)
     add(262, 3, 2 if (count == 3 and dt == np.uint8) else 1)
     if not tile:
-        add(273, 16 if big else 4, [0] * len(chunks))  # patched below
+        add(273, 16 if big else 4, [0] * len(sizes))  # patched below
     add(277, 3, count)
     if not tile:
         add(278, 3 if rps < 65536 else 4, rps)
-        add(279, 16 if big else 4, [len(c) for c in chunks])
+        add(279, 16 if big else 4, sizes)
     add(284, 3, 1 if chunky else 2)
     if predictor == 2:
         add(317, 3, 2)
@@ -433,8 +466,8 @@ def write(path, data: np.ndarray, transform: Optional[Affine] = None, epsg: Opti
     ifd_size = (8 + len(entries) * ent + 8) if big else (2 + len(entries) * ent + 4)
     esz = 8 if big else 4
     ool_base = hdr + ifd_size
-    chunk_off = np.zeros(len(chunks) + 1, dtype=np.int64)
-    chunk_off[1:] = np.cumsum([len(c) for c in chunks])
+    chunk_off = np.zeros(len(sizes) + 1, dtype=np.int64)
+    chunk_off[1:] = np.cumsum(sizes)
 
     def pack_vals(typ, vals):
         if typ == 2:
@@ -476,3 +509,5 @@ def write(path, data: np.ndarray, transform: Optional[Affine] = None, epsg: Opti
         fh.write(ool)
         for c in chunks:
             fh.write(c)
+        for x in strips:
+            fh.write(memoryview(np.ascontiguousarray(x)).cast("B"))

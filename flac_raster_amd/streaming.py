@@ -132,8 +132,11 @@ class EncodedTiles:
     stream_bps: int
 
 
-def encode_band_tiles(band: np.ndarray, tile_size: int, ctx: Optional[Context] = None) -> EncodedTiles:
-    """All band-1 tiles in one GPU launch sequence (the reference's tile loop, cli.py:690-763)."""
+def encode_band_tiles(band: np.ndarray, tile_size: int, ctx: Optional[Context] = None,
+                      pinned: bool = False) -> EncodedTiles:
+    """All band-1 tiles in one GPU launch sequence (the reference's tile loop, cli.py:690-763).  pinned=True: the
+    frames land in the context's page-locked buffer (reused by its next pinned call; create-streaming writes them
+    out at once)."""
     H, W = band.shape
     if H == 0 or W == 0:  # an empty shard (more ranks than tile rows): no tiles, nothing to launch
         z = np.zeros(0, dtype=np.float64)
@@ -144,7 +147,7 @@ def encode_band_tiles(band: np.ndarray, tile_size: int, ctx: Optional[Context] =
     _, bps = audio_params(1, min(tile_size, H), band.dtype)
     d = ctx.make_desc(H, W, band.dtype, nbands=1, tile_h=tile_size, tile_w=tile_size, sample_rate=44100,
                       bits_per_sample=bps)
-    arena, off, mn, mx, sbps = ctx.encode_tiles_host(np.ascontiguousarray(band), d)
+    arena, off, mn, mx, sbps = ctx.encode_tiles_host(np.ascontiguousarray(band), d, pinned=pinned)
     return EncodedTiles(tile_grid(H, W, tile_size), arena, off, mn, mx, sbps)
 
 
@@ -231,7 +234,8 @@ def create_streaming_array(band: np.ndarray, transform: geotiff.Affine, crs: Opt
     tm = timings if timings is not None else {}
     t0 = time.perf_counter()
     H, W = band.shape
-    enc = encode_band_tiles(band, tile_size, ctx)
+    # large jobs: frames back into page-locked memory (DMA rate, no page faults) and written from there
+    enc = encode_band_tiles(band, tile_size, ctx, pinned=band.nbytes >= (64 << 20))
     t1 = time.perf_counter()
     headers, frames, body = streaming_headers(enc, transform, crs, W, H, tile_size, band.dtype)
     index = {"crs": str(crs), "transform": list(transform), "width": W, "height": H, "tile_size": tile_size,
@@ -251,13 +255,25 @@ def create_streaming_array(band: np.ndarray, transform: geotiff.Affine, crs: Opt
 
 
 def create_streaming(input_file: Path, output_file: Path, tile_size: int = 1024,
-                     ctx: Optional[Context] = None) -> Dict:
-    """cli.py:620-804 without the console output: writes the streaming file, returns the index."""
-    with geotiff.TiffFile(input_file) as tf:  # band 1 only (cli.py:698-699)
-        r = tf.raster(bands=[0])
-    transform = r.transform or geotiff.Affine(1.0, 0.0, 0.0, 0.0, 1.0, 0.0)
-    return create_streaming_array(np.ascontiguousarray(r.data[0]), transform, r.crs_string, output_file, tile_size,
-                                  ctx)
+                     ctx: Optional[Context] = None, timings: Optional[Dict[str, float]] = None) -> Dict:
+    """cli.py:620-804 without the console output: writes the streaming file, returns the index.  Band 1 only
+    (cli.py:698-699): an uncompressed band-sequential (or single-band) file is encoded straight from its memory map
+    (no host copy of the band); otherwise its strips / tiles are decoded.  `timings` gets read_s + the stages of
+    create_streaming_array."""
+    tm = timings if timings is not None else {}
+    t0 = time.perf_counter()
+    with geotiff.TiffFile(input_file) as tf:
+        transform, epsg, _, _ = tf.georef()
+        crs = f"EPSG:{epsg}" if epsg else None
+        band = tf.band_view(0)
+        if band is None:
+            band = tf.read_rows(bands=[0])[0]
+        tm["read_s"] = time.perf_counter() - t0
+        transform = transform or geotiff.Affine(1.0, 0.0, 0.0, 0.0, 1.0, 0.0)
+        index = create_streaming_array(band, transform, crs, output_file, tile_size, ctx, tm)
+        del band
+    tm["total_s"] = time.perf_counter() - t0
+    return index
 
 
 # ----------------------------------------------------------------------------- read / select

@@ -170,6 +170,11 @@ int frs_comm_allgather_i64(frs_comm *comm, const int64_t *send_host, int64_t cou
 /* Device memory helpers so hosts need no other GPU runtime binding (no PyTorch in the codec path). */
 void *frs_dev_malloc(frs_ctx *ctx, int64_t bytes);
 void frs_dev_free(frs_ctx *ctx, void *ptr);
+/* Page-locked host memory: an arena_host given to frs_encode_tiles in such memory takes the frames back at DMA rate
+ * (a fresh pageable buffer is page-faulted and pinned page by page during the copy).  create-streaming writes the
+ * file straight from it (streaming.create_streaming_array). */
+void *frs_host_malloc(frs_ctx *ctx, int64_t bytes);
+void frs_host_free(frs_ctx *ctx, void *ptr);
 int frs_memcpy_h2d(frs_ctx *ctx, void *dst_dev, const void *src_host, int64_t bytes);
 int frs_memcpy_d2h(frs_ctx *ctx, void *dst_host, const void *src_dev, int64_t bytes);
 int frs_ctx_sync(frs_ctx *ctx);
