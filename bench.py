@@ -240,7 +240,7 @@ def bbox_extract(ctx, comm, raster, arena, off, tmin, tmax, H, W, T, row0, count
     mine = [q for q in queries
             if first_tile <= streaming.first_intersecting(index, q)["frame_id"] < first_tile + counts[rank]]
     out = ctx.alloc(T * T * 2)
-    host = np.empty(T * T, dtype=np.int16)
+    host = ctx.pinned(T * T * 2).view(np.int16)  # page-locked: the tile comes back at DMA rate
     lat, checked, lossless = [], 0, True
     ctx.profile(True)
     ctx.profile_reset()

@@ -1,0 +1,56 @@
+"""C5 query latency breakdown on the C4 arena: selection (host), decode call (device + sync), result download."""
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[2]
+sys.path.insert(0, str(ROOT))
+import workloads  # noqa: E402
+from flac_raster_amd import _native, streaming  # noqa: E402
+
+
+def main():
+    nq = int(sys.argv[1]) if len(sys.argv) > 1 else 300
+    H = W = 40000
+    T = 512
+    ctx = _native.Context(0)
+    raster = ctx.alloc(4 * H * W * 2)
+    ctx.synth_raster(raster, 4, H, W, row0=0, full_height=H, seed=1234)
+    desc = ctx.make_desc(H, W, np.int16, nbands=1, band0=0, tile_h=T, tile_w=T, sample_rate=44100, bits_per_sample=16)
+    arena = ctx.alloc(ctx.arena_bound(desc))
+    off, mn, mx, _ = ctx.encode_tiles_device(raster.ptr, desc, arena)
+    ctx.sync()
+    index = workloads.streaming_index(H, W, T, np.diff(off))
+    qs = workloads.c5_queries(H, W, T, nq)
+    out = ctx.alloc(T * T * 2)
+    host = ctx.pinned(T * T * 2).view(np.int16)
+    ts, td, tc = [], [], []
+    ctx.profile(True)
+    ctx.profile_reset()
+    for k, bbox in enumerate(qs[:10] + qs):
+        t0 = time.perf_counter()
+        f = streaming.first_intersecting(index, bbox)
+        i = f["frame_id"]
+        n = f["window"]["width"] * f["window"]["height"]
+        t1 = time.perf_counter()
+        ctx.decode_tiles_device(arena, np.array([off[i], off[i + 1]], dtype=np.int64), [n], channels=1, bps=16,
+                                data_min=[float(mn[i])], data_max=[float(mx[i])], dtype=np.int16, out=out)
+        t2 = time.perf_counter()
+        out.download(n * 2, 0, out=host[:n].view(np.uint8))
+        t3 = time.perf_counter()
+        if k >= 10:
+            ts.append(t1 - t0)
+            td.append(t2 - t1)
+            tc.append(t3 - t2)
+    kern = {k: round(ctx.profile_avg_ms(k), 4) for k in ("decode", "decode_span", "decode_frames")}
+    p = lambda a: round(float(np.percentile(np.array(a) * 1e3, 50)), 4)
+    tot = [a + b + c for a, b, c in zip(ts, td, tc)]
+    print(json.dumps({"select_ms": p(ts), "decode_call_ms": p(td), "download_ms": p(tc), "total_p50": p(tot),
+                      "total_p90": round(float(np.percentile(np.array(tot) * 1e3, 90)), 4), "kernels": kern}))
+
+
+if __name__ == "__main__":
+    main()
