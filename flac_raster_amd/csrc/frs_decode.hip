@@ -186,6 +186,39 @@ __device__ inline uint32_t win_dword(const uint4 &w0, const uint4 &w1, int idx) 
     return r;
 }
 
+// The sync patterns `raw` (bit j: a 0xFF 0xF8/F9 pair at byte j) of one lane's 16 bytes `cur` (blob position p0),
+// `nxt` = the following 16 bytes: the bits whose header parses (header_ok_regs on the 32-byte window; the global
+// parse when the window does not hold the next 16 bytes).  Out of line: the rare path must not keep the caller's
+// step loop from unrolling (a rolled loop indexed the 16 loaded chunks dynamically, i.e. through scratch memory).
+__device__ __attribute__((noinline)) uint32_t sel_check_candidates(uint4 cur, uint4 nxt, uint32_t raw, int64_t p0,
+                                                                   int64_t nbytes, const uint8_t *blob,
+                                                                   const int64_t *soff, int ns, int channels,
+                                                                   int stream_bps, bool regs_ok) {
+    uint32_t mask = 0;
+    while (raw) {
+        const int j = __builtin_ctz(raw);
+        raw &= raw - 1;
+        const int64_t p = p0 + j;
+        if (p < 0 || p + 1 >= nbytes) continue;
+        bool ok;
+        if (regs_ok) {
+            uint32_t h[4];
+            const int wi = j >> 2, sh = j & 3;
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+                const uint32_t lo = win_dword(cur, nxt, wi + d), hi = win_dword(cur, nxt, min(wi + d + 1, 7));
+                h[d] = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)sh);
+            }
+            ok = header_ok_regs(h, min<int64_t>(nbytes - p, 16), channels);
+        } else {
+            const int st = stream_of(soff, ns, p);
+            ok = parse_header(blob, p, soff[st + 1], channels, stream_bps).ok;
+        }
+        if (ok) mask |= 1u << j;
+    }
+    return mask;
+}
+
 // Coalesced candidate flags: wave w of a 64 KB block takes the contiguous 16 KB at qw = block base + 16 KB w; step k
 // of it is the 1 KB at qw + 1024 k, lane L its 16 bytes at + 16 L (one fully coalesced 16-byte load per lane and
 // step).  Bit j of m[k] marks a sync code with a parseable, CRC-8-correct header at qw + 1024 k + 16 L + j, so
@@ -250,27 +283,8 @@ __device__ inline int sel_masks_co(const uint8_t *blob, int64_t nbytes, const in
             nv.w = (uint32_t)__shfl((int)src.w, from);
             const int64_t q0 = qw + 1024 * k + 16 * lane;
             const bool regs_ok = k + 1 < kSelSteps || lane < 63;  // the window holds the next 16 bytes
-            while (raw) {
-                const int j = __builtin_ctz(raw);
-                raw &= raw - 1;
-                const int64_t p = q0 + j - lead;
-                if (p < 0 || p + 1 >= nbytes) continue;
-                bool ok;
-                if (regs_ok) {
-                    uint32_t h[4];
-                    const int wi = j >> 2, sh = j & 3;
-#pragma unroll
-                    for (int d = 0; d < 4; d++) {
-                        const uint32_t lo = win_dword(v[k], nv, wi + d), hi = win_dword(v[k], nv, min(wi + d + 1, 7));
-                        h[d] = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)sh);
-                    }
-                    ok = header_ok_regs(h, min<int64_t>(nbytes - p, 16), channels);
-                } else {
-                    const int st = stream_of(soff, ns, p);
-                    ok = parse_header(blob, p, soff[st + 1], channels, stream_bps).ok;
-                }
-                if (ok) mask |= 1u << j;
-            }
+            if (raw) mask = sel_check_candidates(v[k], nv, raw, q0 - lead, nbytes, blob, soff, ns, channels,
+                                                 stream_bps, regs_ok);
         }
         m[k] = mask;
         cnt += __builtin_popcount(mask);

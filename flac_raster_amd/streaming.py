@@ -453,9 +453,25 @@ def extract_streaming(flac_url: Union[str, Path], output: Path, bbox: Optional[S
     return f
 
 
-def extract_bbox_mosaic(flac_url: Union[str, Path], bbox: Sequence[float], ctx: Optional[Context] = None):
+def bbox_pixel_window(transform: geotiff.Affine, bbox: Sequence[float], width: int, height: int) -> Dict:
+    """Smallest whole-pixel window of a north-up raster that covers bbox [xmin, ymin, xmax, ymax], clipped to the
+    raster: columns floor((xmin - c) / a) .. ceil((xmax - c) / a), rows floor((ymax - f) / e) .. ceil((ymin - f) / e)."""
+    import math
+    t = transform
+    c0 = math.floor((bbox[0] - t.c) / t.a)
+    c1 = math.ceil((bbox[2] - t.c) / t.a)
+    r0 = math.floor((bbox[3] - t.f) / t.e)
+    r1 = math.ceil((bbox[1] - t.f) / t.e)
+    c0, r0 = max(0, c0), max(0, r0)
+    c1, r1 = min(width, max(c1, c0)), min(height, max(r1, r0))
+    return {"col_off": c0, "row_off": r0, "width": c1 - c0, "height": r1 - r0}
+
+
+def extract_bbox_mosaic(flac_url: Union[str, Path], bbox: Sequence[float], ctx: Optional[Context] = None,
+                        crop: bool = True):
     """Extension: decode every tile intersecting bbox in one GPU batch and mosaic them into
-    the raster window they cover.  Returns (array (1, h, w), window dict, transform list)."""
+    the raster window they cover, cropped (crop=True) to the whole-pixel window of the bbox itself
+    (bbox_pixel_window).  Returns (array (1, h, w), window dict, transform list)."""
     src = Source(flac_url)
     n, index = read_index(src)
     hits = intersecting(index, bbox)
@@ -473,5 +489,14 @@ def extract_bbox_mosaic(flac_url: Union[str, Path], bbox: Sequence[float], ctx: 
         w = f["window"]
         out[0, w["row_off"] - r0:w["row_off"] - r0 + w["height"], w["col_off"] - c0:w["col_off"] - c0 + w["width"]] = arr[0]
     t = geotiff.Affine(*index["transform"][:6])
-    wt = geotiff.window_transform(t, c0, r0)
-    return out, {"col_off": c0, "row_off": r0, "width": c1 - c0, "height": r1 - r0}, list(wt)
+    win = {"col_off": c0, "row_off": r0, "width": c1 - c0, "height": r1 - r0}
+    if crop and t.b == 0 and t.d == 0:
+        cw = bbox_pixel_window(t, bbox, int(index["width"]), int(index["height"]))
+        # (the tiles intersecting the bbox cover its pixel window)
+        a0, b0 = max(cw["col_off"], c0), max(cw["row_off"], r0)
+        a1 = min(cw["col_off"] + cw["width"], c1)
+        b1 = min(cw["row_off"] + cw["height"], r1)
+        out = np.ascontiguousarray(out[:, b0 - r0:max(b1, b0) - r0, a0 - c0:max(a1, a0) - c0])
+        win = {"col_off": a0, "row_off": b0, "width": max(a1 - a0, 0), "height": max(b1 - b0, 0)}
+    wt = geotiff.window_transform(t, win["col_off"], win["row_off"])
+    return out, win, list(wt)

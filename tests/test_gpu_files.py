@@ -79,9 +79,14 @@ def test_extract_streaming_roundtrip_lossless(gpu_ctx, golden, tmp_path):
         got = geotiff.read(tif)
         assert np.array_equal(got.data[0], r.data[0, w["row_off"]:w["row_off"] + w["height"],
                                                     w["col_off"]:w["col_off"] + w["width"]])
-    arr, win, tr = streaming.extract_bbox_mosaic(out, [-105.45, 40.1, -105.1, 40.45], ctx=gpu_ctx)
-    assert np.array_equal(arr[0], r.data[0, win["row_off"]:win["row_off"] + win["height"],
-                                          win["col_off"]:win["col_off"] + win["width"]])
+    for crop in (False, True):
+        bb = [-105.45, 40.1, -105.1, 40.45]
+        arr, win, tr = streaming.extract_bbox_mosaic(out, bb, ctx=gpu_ctx, crop=crop)
+        assert np.array_equal(arr[0], r.data[0, win["row_off"]:win["row_off"] + win["height"],
+                                              win["col_off"]:win["col_off"] + win["width"]])
+        assert list(tr) == list(geotiff.window_transform(r.transform, win["col_off"], win["row_off"]))
+        if crop:  # exactly the bbox's pixel window (clipped to the raster)
+            assert win == streaming.bbox_pixel_window(r.transform, bb, r.width, r.height)
 
 
 def test_raw_frames_sample_dem_matches_fixture(gpu_ctx, golden, tmp_path):

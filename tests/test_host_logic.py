@@ -180,3 +180,16 @@ def test_tiff_windowed_rows_equal_full_read(tmp_path, golden):
                     sel = full.data if bands is None else full.data[bands]
                     assert np.array_equal(got, sel[:, r0:r1]), (p.name, r0, r1, bands)
             assert tf.georef()[0] == full.transform
+
+
+def test_bbox_pixel_window_covers_bbox():
+    """Mosaic crop (extension): the smallest whole-pixel window covering the bbox, clipped."""
+    from flac_raster_amd import geotiff, streaming
+    t = geotiff.Affine(10.0, 0.0, 500000.0, 0.0, -10.0, 4000000.0)
+    assert streaming.bbox_pixel_window(t, [500015, 3999900, 500101, 3999985], 100, 100) == \
+        {"col_off": 1, "row_off": 1, "width": 10, "height": 9}
+    assert streaming.bbox_pixel_window(t, [500000, 3999900, 500100, 4000000], 100, 100) == \
+        {"col_off": 0, "row_off": 0, "width": 10, "height": 10}
+    # clipped at the raster edge
+    assert streaming.bbox_pixel_window(t, [499000, 3990000, 500050, 4001000], 100, 100) == \
+        {"col_off": 0, "row_off": 0, "width": 5, "height": 100}
