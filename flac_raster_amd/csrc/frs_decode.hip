@@ -1135,8 +1135,16 @@ __device__ __attribute__((always_inline)) inline void decode_one_frame(const uin
             int i = o;
             int lg = 0;
             while ((1 << lg) < o) lg++;
-            const bool narrow = sbps <= 23 && (lpc ? prec_lpc : 3) + sbps + lg <= 31;
+            const bool safe32 = (lpc ? prec_lpc : 3) + sbps + lg <= 31;  // the 32-bit prediction cannot wrap
+            // libFLAC's level-5 precision makes prec + 16 + log2(order) = 32 for every 16-bit LPC order >= 2, so the
+            // 32-bit sum may wrap in principle; a wrapped sum moves the sample by a multiple of 2^(32 - shift),
+            // which for sbps + shift <= 31 leaves the sbps range -- the restore checks every sample and redoes the
+            // subframe on the exact 64-bit path if one is out (never on a stream libFLAC decodes in 32 bits)
+            const bool wrap_checked = !safe32 && sbps <= 17 && sbps + shift <= 31;
+            const bool narrow = sbps <= 23 && (safe32 || wrap_checked);
+            bool done = false;
             if (resbuf && narrow && bs <= kDecResMax) {
+                const auto br0 = br;
                 // ---- phase 1: every residual of the subframe into LDS (tight Rice loop: refill only when
                 //      fewer than 32 bits are cached, long unary runs via the generic reader)
                 for (int p = 0; p < (1 << po); p++) {
@@ -1196,6 +1204,8 @@ __device__ __attribute__((always_inline)) inline void decode_one_frame(const uin
                 // keep the ring, taps and output cursor in VGPRs (vector ALU; the scalar unit would spill)
                 int32_t vshift = shift;
                 int32_t *xo = x;
+                const int32_t xlo = -(1 << (sbps - 1)), xhi = (1 << (sbps - 1)) - 1;
+                uint32_t oor = 0;
 #pragma unroll
                 for (int m = 0; m < 8; m++) asm volatile("" : "+v"(cq[m]), "+v"(R[m]));
                 asm volatile("" : "+v"(vshift));
@@ -1211,12 +1221,20 @@ __device__ __attribute__((always_inline)) inline void decode_one_frame(const uin
                             for (int m = 1; m < 8; m++) older += __mul24(cq[m], R[(u - 1 - m + 16) & 7]);
                             const int32_t pred = older + __mul24(cq[0], R[(u - 1 + 8) & 7]);
                             const int32_t v = rr[u] + (pred >> vshift);
+                            oor |= (uint32_t)(v < xlo) | (uint32_t)(v > xhi);
                             xo[(int64_t)(i0 + u) * nch] = v;
                             R[u] = v;
                         }
                     }
                 }
                 i = bs;
+                done = !(wrap_checked && oor);
+                if (!done) {  // a wrapped prediction: the subframe's residual bits again, exactly
+                    br = br0;
+                    i = o;
+                }
+            }
+            if (done) {
             } else if (o <= 8) {
                 // history in registers: h[m] = x[i-1-m]; coefficient m = 0 for m >= o (branch-free taps)
                 int32_t cq[8];

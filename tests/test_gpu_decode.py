@@ -185,3 +185,78 @@ def test_decode_rejects_reversed_offsets(gpu_ctx):
         with pytest.raises(_native.FrsError) as e:
             call()
         assert e.value.code == -1 and "non-decreasing" in str(e.value)
+
+
+def _crc8(data: bytes) -> int:
+    c = 0
+    for b in data:
+        c ^= b
+        for _ in range(8):
+            c = ((c << 1) ^ 0x07) & 0xFF if c & 0x80 else (c << 1) & 0xFF
+    return c
+
+
+def _crc16(data: bytes) -> int:
+    c = 0
+    for b in data:
+        c ^= b << 8
+        for _ in range(8):
+            c = ((c << 1) ^ 0x8005) & 0xFFFF if c & 0x8000 else (c << 1) & 0xFFFF
+    return c
+
+
+def _wrapping_lpc_frames(nframes: int, bs: int = 64) -> bytes:
+    """Hand-built mono 16-bit frames (RFC 9639) whose LPC prediction sum needs more than 32 bits: order 8, 15-bit
+    coefficients of 16383, shift 14, every sample 32767 -> sum q.x = 8 * 16383 * 32767 > 2^31.  libFLAC decodes
+    them with its 64-bit restore (prec + bps + log2(order) > 32); a decoder summing mod 2^32 must notice."""
+    out = bytearray()
+    for fno in range(nframes):
+        bits = []
+
+        def put(v, n):
+            for i in range(n - 1, -1, -1):
+                bits.append((v >> i) & 1)
+        hdr = bytes([0xFF, 0xF8, (7 << 4) | 9, (0 << 4) | (4 << 1)])
+        assert fno < 128
+        hdr += bytes([fno]) + (bs - 1).to_bytes(2, "big")
+        hdr += bytes([_crc8(hdr)])
+        o, prec, shift, q, x = 8, 15, 14, 16383, 32767
+        put(0, 1)
+        put(32 + o - 1, 6)
+        put(0, 1)
+        for _ in range(o):
+            put(x & 0xFFFF, 16)
+        put(prec - 1, 4)
+        put(shift, 5)
+        for _ in range(o):
+            put(q & 0x7FFF, 15)
+        put(0, 2)   # Rice, 4-bit parameters
+        put(0, 4)   # partition order 0
+        k = 14
+        put(k, 4)
+        r = x - ((o * q * x) >> shift)
+        u = (r << 1) ^ (r >> 63) if r >= 0 else ((-r) << 1) - 1
+        for _ in range(bs - o):
+            put(0, u >> k)
+            put(1, 1)
+            put(u & ((1 << k) - 1), k)
+        while len(bits) % 8:
+            bits.append(0)
+        body = hdr + bytes(int("".join(map(str, bits[i:i + 8])), 2) for i in range(0, len(bits), 8))
+        out += body + _crc16(body).to_bytes(2, "big")
+    return bytes(out)
+
+
+@pytest.mark.parametrize("kind", list(DECODERS))
+def test_wrapped_lpc_prediction_decodes_exactly(gpu_ctx, kind, monkeypatch):
+    """The 32-bit restore paths sum the LPC prediction mod 2^32 (level 5's 16-bit precision choice reaches
+    prec + bps + log2(order) = 32); a wrapped sum must be detected and the subframe redone exactly."""
+    nf, bs = 80, 64  # > 64 frames: the lane decoder takes the job when forced
+    fr = _wrapping_lpc_frames(nf, bs)
+    n = nf * bs
+    ref = O.decode_frames(fr, 1, 16, n)
+    assert np.all(ref == 32767)
+    dctx = _decoder_ctx(kind, monkeypatch)
+    got = dctx.decode_frames_host(np.frombuffer(fr, np.uint8), [0, len(fr)], [n], channels=1, bps=16, blocksize=bs)
+    assert np.array_equal(got.reshape(-1), ref.reshape(-1))
+    dctx.close()
