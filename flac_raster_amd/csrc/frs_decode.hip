@@ -2137,6 +2137,12 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
                                                            int8_t *fchass = nullptr) {
     static_assert(!MC || OUT == kOutPcm, "channel-planar int32 output");
     constexpr int es = OUT == kOutPcm ? 4 : OUT == kOutU8 ? 1 : 2;  // kOutAny: per-sample dn_store
+    // 1- and 2-byte outputs: a lane's aligned 8-sample groups are staged in LDS (slot-major: every ds op of the wave
+    // is one contiguous 1 KB) and leave 8 groups at a time, i.e. a whole 128-byte line (64 B for bytes) as back-to-back
+    // stores -- one 16-byte store per step to 64 different lines had the L2 write each line back several times
+    // (PMC: 5x the output bytes written)
+    constexpr bool kStage = OUT == kOutI16 || OUT == kOutU16 || OUT == kOutU8;
+    __shared__ uint4 ostage[kStage ? 4 : 1][kStage ? 8 : 1][kStage ? 64 : 1];
     const int64_t fi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint8_t *obytes = MC ? reinterpret_cast<uint8_t *>(planar)
                          : OUT == kOutPcm ? reinterpret_cast<uint8_t *>(pcm) : static_cast<uint8_t *>(dout.out);
@@ -2223,6 +2229,23 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
                 if (take) {
                     const bool vec = OUT != kOutAny && (obase & 7) == 0;  // 8-element groups aligned
                     const bool cst = t == 0;
+                    int nst = 0;              // groups staged in this lane's row
+                    uint8_t *rdst = nullptr;  // output address of the row's first group
+                    uint4 *st = &ostage[kStage ? (threadIdx.x >> 6) : 0][0][0];  // [slot][lane]
+                    const int ln = threadIdx.x & 63;
+                    auto flush = [&]() {
+                        if constexpr (kStage) {
+#pragma unroll
+                            for (int u = 0; u < 8; u++) {
+                                if (u < nst) {
+                                    const uint4 v = st[u * 64 + ln];
+                                    if constexpr (es == 2) reinterpret_cast<uint4 *>(rdst)[u] = v;
+                                    else reinterpret_cast<uint2 *>(rdst)[u] = make_uint2(v.x, v.y);
+                                }
+                            }
+                            nst = 0;
+                        }
+                    };
                     for (int i0 = 0; i0 < bs && take; i0 += 8) {
                         br.top_up();
                         uint32_t ob[8];
@@ -2265,7 +2288,17 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
                             const int nout = min(8, bs - i0);
                             uint8_t *dst = obytes + (obase + i0) * es;
                             if (vec && nout == 8) {
-                                if constexpr (es == 2) {
+                                if constexpr (kStage) {
+                                    if (nst == 0) rdst = dst;
+                                    if constexpr (es == 2)
+                                        st[nst * 64 + ln] = make_uint4(ob[0] | (ob[1] << 16), ob[2] | (ob[3] << 16),
+                                                                 ob[4] | (ob[5] << 16), ob[6] | (ob[7] << 16));
+                                    else
+                                        st[nst * 64 + ln] = make_uint4(ob[0] | (ob[1] << 8) | (ob[2] << 16) | (ob[3] << 24),
+                                                                 ob[4] | (ob[5] << 8) | (ob[6] << 16) | (ob[7] << 24), 0u,
+                                                                 0u);
+                                    if (++nst == 8) flush();
+                                } else if constexpr (es == 2) {
                                     *reinterpret_cast<uint4 *>(dst) =
                                         make_uint4(ob[0] | (ob[1] << 16), ob[2] | (ob[3] << 16), ob[4] | (ob[5] << 16),
                                                    ob[6] | (ob[7] << 16));
@@ -2290,6 +2323,7 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
                         }
                         if (br.bad) break;
                     }
+                    flush();
                 }
                 take_all = take_all && take;
                 }  // channels
