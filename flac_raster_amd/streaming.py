@@ -455,13 +455,18 @@ def extract_streaming(flac_url: Union[str, Path], output: Path, bbox: Optional[S
 
 def bbox_pixel_window(transform: geotiff.Affine, bbox: Sequence[float], width: int, height: int) -> Dict:
     """Smallest whole-pixel window of a north-up raster that covers bbox [xmin, ymin, xmax, ymax], clipped to the
-    raster: columns floor((xmin - c) / a) .. ceil((xmax - c) / a), rows floor((ymax - f) / e) .. ceil((ymin - f) / e)."""
+    raster: columns floor((xmin - c) / a) .. ceil((xmax - c) / a), rows floor((ymax - f) / e) .. ceil((ymin - f) / e).
+    Pixel coordinates within 1e-6 of an integer are snapped to it first, so a bbox edge on a pixel (or tile) edge
+    does not pull in a sliver pixel through float error (-105.1 -> column 400.0000000000057 for a 0.001 grid)."""
     import math
+
+    def snap(v: float) -> float:
+        return float(round(v)) if abs(v - round(v)) < 1e-6 else v
     t = transform
-    c0 = math.floor((bbox[0] - t.c) / t.a)
-    c1 = math.ceil((bbox[2] - t.c) / t.a)
-    r0 = math.floor((bbox[3] - t.f) / t.e)
-    r1 = math.ceil((bbox[1] - t.f) / t.e)
+    c0 = math.floor(snap((bbox[0] - t.c) / t.a))
+    c1 = math.ceil(snap((bbox[2] - t.c) / t.a))
+    r0 = math.floor(snap((bbox[3] - t.f) / t.e))
+    r1 = math.ceil(snap((bbox[1] - t.f) / t.e))
     c0, r0 = max(0, c0), max(0, r0)
     c1, r1 = min(width, max(c1, c0)), min(height, max(r1, r0))
     return {"col_off": c0, "row_off": r0, "width": c1 - c0, "height": r1 - r0}

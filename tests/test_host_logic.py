@@ -193,3 +193,7 @@ def test_bbox_pixel_window_covers_bbox():
     # clipped at the raster edge
     assert streaming.bbox_pixel_window(t, [499000, 3990000, 500050, 4001000], 100, 100) == \
         {"col_off": 0, "row_off": 0, "width": 5, "height": 100}
+    # bbox edges on pixel edges through float error (sample_dem.tif's 0.001-degree grid): no sliver pixel
+    d = geotiff.Affine(0.001, 0.0, -105.5, 0.0, -0.001, 40.5)
+    assert streaming.bbox_pixel_window(d, [-105.45, 40.1, -105.1, 40.45], 512, 512) == \
+        {"col_off": 50, "row_off": 50, "width": 350, "height": 350}
