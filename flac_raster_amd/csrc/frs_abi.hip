@@ -14,21 +14,21 @@
 
 namespace frs {
 
-void prof_begin(frs_ctx *ctx, const char *name, hipEvent_t *start) {
+void prof_begin(frs_ctx *ctx, const char *name, hipEvent_t *start, hipStream_t s) {
     (void)name;
     *start = nullptr;
     if (!ctx->prof) return;
     hipEvent_t e;
     if (hipEventCreate(&e) != hipSuccess) return;
-    hipEventRecord(e, ctx->stream);
+    hipEventRecord(e, s ? s : ctx->stream);
     *start = e;
 }
 
-void prof_end(frs_ctx *ctx, const char *name, hipEvent_t start) {
+void prof_end(frs_ctx *ctx, const char *name, hipEvent_t start, hipStream_t s) {
     if (!ctx->prof || !start) return;
     hipEvent_t e;
     if (hipEventCreate(&e) != hipSuccess) return;
-    hipEventRecord(e, ctx->stream);
+    hipEventRecord(e, s ? s : ctx->stream);
     ctx->ev_pending.push_back({std::string(name), {start, e}});
 }
 
@@ -102,6 +102,8 @@ int frs_ctx_create(int device, frs_ctx **out) {
     ctx->force_generic = fg && fg[0] == '1';
     const char *dl = getenv("FRS_DECODE_LANE");
     ctx->decode_lane = dl ? (dl[0] == '1' ? 1 : 0) : -1;
+    const char *es = getenv("FRS_ENC_SPLIT");
+    if (es) ctx->enc_split = std::max(1, std::min(8, atoi(es)));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return FRS_E_HIP;
@@ -126,6 +128,10 @@ void frs_ctx_destroy(frs_ctx *ctx) {
     ctx->pin.release();
     ctx->ring[0].release();
     ctx->ring[1].release();
+    if (ctx->aux_stream) hipStreamSynchronize(ctx->aux_stream);
+    for (hipEvent_t e : ctx->split_ev)
+        if (e) hipEventDestroy(e);
+    if (ctx->aux_stream) hipStreamDestroy(ctx->aux_stream);
     if (ctx->h2d_stream) hipStreamDestroy(ctx->h2d_stream);
     if (ctx->d2h_stream) hipStreamDestroy(ctx->d2h_stream);
     hipStreamDestroy(ctx->stream);

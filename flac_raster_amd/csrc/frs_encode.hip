@@ -3158,7 +3158,9 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
                                                   const int32_t *__restrict__ ftile, const uint4 *__restrict__ hdr_tab,
                                                   int hdr_n, const uint32_t *__restrict__ pslots,
                                                   const int64_t *__restrict__ pbytes, uint32_t *sub_slots = nullptr,
-                                                  int32_t *sub_bits = nullptr) {
+                                                  int32_t *sub_bits = nullptr, int64_t ubeg = 0, int64_t uend = -1) {
+    // units [ubeg, uend) of the job (uend < 0: to the end): a split job encodes its tile ranges in turn, each launch
+    // with its own ticket counter; the look-back reaches into the previous launch's (inclusive) statuses
     __shared__ EncV3Shared S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int i = threadIdx.x; i < 2048; i += blockDim.x) (&S.crc8x[0][0])[i] = (&c_crc16x8[0][0])[i];
@@ -3171,14 +3173,15 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
     uint32_t *fbuf = S.bits[wave];
     while (true) {
         __syncthreads();  // previous ticket's readers of S.ticket / S.lut are done
-        const int64_t nunits = SUB ? P.nframes * P.nch : P.nframes;
+        const int64_t nunits = uend < 0 ? (SUB ? P.nframes * P.nch : P.nframes) : uend;
         if (threadIdx.x == 0) {
             const int tk = atomicAdd(ticket_ctr, 1);
             S.ticket = tk;
-            S.want = ((int64_t)tk * 4 < nunits) ? ftile[SUB ? (int64_t)tk * 4 / P.nch : (int64_t)tk * 4] : -1;
+            const int64_t u0 = ubeg + (int64_t)tk * 4;
+            S.want = (u0 < nunits) ? ftile[SUB ? u0 / P.nch : u0] : -1;
         }
         __syncthreads();
-        const int64_t fbase = (int64_t)S.ticket * 4;
+        const int64_t fbase = ubeg + (int64_t)S.ticket * 4;
         if (fbase >= nunits) break;
         const int want = S.want;
         if (want != S.lut_tile) {  // WG-uniform
@@ -3204,7 +3207,7 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
             }
         } else {
             const int64_t f = fbase + wave;
-            if (f < P.nframes)
+            if (f < nunits)
                 encode_frame_v3<DT>(raster, P, tiles, norms, luts, ana, arena, arena_cap, frame_off, status, err, S,
                                     want, f, lane, ftile, prev, hdr_tab, hdr_n, pslots, pbytes);
         }
@@ -3533,9 +3536,18 @@ template <int DT>
 static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster_dev, void *arena_dev,
                       int64_t arena_cap, int64_t *tile_off, double *tile_min, double *tile_max, bool allow_fast) {
     using T = typename Elem<DT>::T;
-    std::vector<TileGeom> tiles;
-    int64_t nframes;
-    build_tiles(d, tiles, nframes);
+    // job geometry cache (frs_ctx::geo_*): everything the tile table, partial marking and wave table depend on
+    const std::vector<int64_t> key = {d->height, d->width, d->tile_h, d->tile_w, d->tile_begin, d->tile_end,
+                                      d->blocksize, d->nbands, d->dtype, d->bits_per_sample, d->norm_mode,
+                                      (allow_fast && !ctx->force_generic) ? 1 : 0};
+    const bool geo_hit = !ctx->geo_key.empty() && ctx->geo_key == key;
+    std::vector<TileGeom> tiles_local;
+    std::vector<TileGeom> &tiles = geo_hit ? ctx->geo_tiles : tiles_local;
+    int64_t nframes = ctx->geo_nframes;
+    if (!geo_hit) {
+        ctx->geo_key.clear();  // the device copies are rewritten below; valid again once uploaded
+        build_tiles(d, tiles, nframes);
+    }
     const int ntiles = (int)tiles.size();
     if (ntiles == 0) {
         tile_off[0] = 0;
@@ -3586,12 +3598,18 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                     P.norm_mode == 0 && d->blocksize == 4096 && !Elem<DT>::is_float;
     int64_t npartial = 0;
     int64_t *hplist = ctx->pin.at<int64_t>(pin_pl);
-    if (fast || mc)
+    if (geo_hit) {
+        npartial = (int64_t)ctx->geo_plist.size();
+        if (npartial) memcpy(hplist, ctx->geo_plist.data(), sizeof(int64_t) * (size_t)npartial);
+    } else if (fast || mc) {
         for (TileGeom &tg : tiles)
             if (((int64_t)tg.h * tg.w) % d->blocksize != 0) {
                 hplist[npartial] = tg.frame_base + tg.nframes - 1;
                 tg.partial = (int32_t)(++npartial);
             }
+    }
+    // device copies of the cached geometry still in place (a grown buffer is a new allocation)
+    const bool dev_tiles = geo_hit && ctx->geo_ptrs[0] == ctx->tiles.ptr;
     if (ctx->window_bs != d->blocksize) {
         std::vector<float> win(d->blocksize, 1.0f);
         // FLAC__window_tukey(0.5) computed in double with the host libm cos, stored as float (window.c)
@@ -3608,9 +3626,11 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         FRS_HIP(hipStreamSynchronize(st));
         ctx->window_bs = d->blocksize;
     }
-    memcpy(ctx->pin.at<TileGeom>(pin_tiles), tiles.data(), sizeof(TileGeom) * ntiles);
-    FRS_HIP(hipMemcpyAsync(ctx->tiles.ptr, ctx->pin.at<TileGeom>(pin_tiles), sizeof(TileGeom) * ntiles,
-                           hipMemcpyHostToDevice, st));
+    if (!dev_tiles) {
+        memcpy(ctx->pin.at<TileGeom>(pin_tiles), tiles.data(), sizeof(TileGeom) * ntiles);
+        FRS_HIP(hipMemcpyAsync(ctx->tiles.ptr, ctx->pin.at<TileGeom>(pin_tiles), sizeof(TileGeom) * ntiles,
+                               hipMemcpyHostToDevice, st));
+    }
     int *err_flag = reinterpret_cast<int *>(ctx->frame_bytes.as<int64_t>() + nframes + 1);
     FRS_HIP(hipMemsetAsync(err_flag, 0, sizeof(int), st));
 
@@ -3669,40 +3689,78 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         FRS_HIP(ctx->status.ensure(sizeof(uint64_t) * (nframes + 1) + 64));
         if (!fuse_stats) k_build_lut<DT><<<ntiles, 256, 0, st>>>(dnorms, ctx->luts.as<int16_t>());
         FRS_HIP(ctx->frame_tile.ensure(sizeof(int32_t) * nframes));
-        k_frame_tile<<<ntiles, 64, 0, st>>>(dtiles, ntiles, ctx->frame_tile.as<int32_t>());
-        prof_begin(ctx, "analyze", &ev);
+        if (!(dev_tiles && ctx->geo_ptrs[3] == ctx->frame_tile.ptr))
+            k_frame_tile<<<ntiles, 64, 0, st>>>(dtiles, ntiles, ctx->frame_tile.as<int32_t>());
+        int nsplit = 1;
+        int split_t[9] = {0};  // first wave (= tile, when split) of each range
         {
             // wave table: (tile, first frame) per wave, up to 64 frames of one tile each
-            int2 *wt = ctx->pin.at<int2>(pin_wt);
-            int nwaves = 0;
-            for (int ti = 0; ti < ntiles; ti++)
-                for (int c = 0; c < P.nch; c++)  // (tile, first frame | channel << 24)
-                    for (int k0 = 0; k0 < tiles[ti].nframes; k0 += 64) wt[nwaves++] = make_int2(ti, k0 | (c << 24));
-            FRS_HIP(ctx->wave_tab.ensure(sizeof(int2) * nwaves));
-            FRS_HIP(hipMemcpyAsync(ctx->wave_tab.ptr, wt, sizeof(int2) * nwaves, hipMemcpyHostToDevice, st));
-            const unsigned wgrid = (unsigned)((nwaves + 3) / 4);
-            if (fuse_stats) {
-                if constexpr (sizeof(T) == 2)
-                    k_analyze_v3<DT, false, true><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
-                                                                         ctx->window.as<float>(), dana,
-                                                                         ctx->wave_tab.as<int2>(), nwaves);
-            } else {
-                k_analyze_v3<DT, false><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
-                                                               ctx->window.as<float>(), dana, ctx->wave_tab.as<int2>(),
-                                                               nwaves);
+            int nwaves = ctx->geo_nwaves;
+            if (!(dev_tiles && ctx->geo_ptrs[1] == ctx->wave_tab.ptr)) {
+                int2 *wt = ctx->pin.at<int2>(pin_wt);
+                nwaves = 0;
+                for (int ti = 0; ti < ntiles; ti++)
+                    for (int c = 0; c < P.nch; c++)  // (tile, first frame | channel << 24)
+                        for (int k0 = 0; k0 < tiles[ti].nframes; k0 += 64) wt[nwaves++] = make_int2(ti, k0 | (c << 24));
+                FRS_HIP(ctx->wave_tab.ensure(sizeof(int2) * nwaves));
+                FRS_HIP(hipMemcpyAsync(ctx->wave_tab.ptr, wt, sizeof(int2) * nwaves, hipMemcpyHostToDevice, st));
             }
-            k_analyze_v3<DT, true><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
-                                                          ctx->window.as<float>(), dana, ctx->wave_tab.as<int2>(),
-                                                          nwaves);
+            // split (fused stats, one wave per tile, mono, no partial frames): the wave table's ranges [w_k, w_k+1)
+            // are whole tiles; range k is analysed on the aux stream and encoded on `st` once its event fired
+            nsplit = (fuse_stats && !mc && P.nch == 1 && npartial == 0 && nwaves >= 32 * ctx->enc_split)
+                         ? ctx->enc_split : 1;
+            hipStream_t ast = st;
+            if (nsplit > 1) {
+                if (!ctx->aux_stream) FRS_HIP(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
+                for (int k = 0; k <= nsplit; k++)
+                    if (!ctx->split_ev[k]) FRS_HIP(hipEventCreateWithFlags(&ctx->split_ev[k], hipEventDisableTiming));
+                ast = ctx->aux_stream;
+                FRS_HIP(hipEventRecord(ctx->split_ev[nsplit], st));  // the uploads and setup kernels above
+                FRS_HIP(hipStreamWaitEvent(ast, ctx->split_ev[nsplit], 0));
+            }
+            prof_begin(ctx, "analyze", &ev, ast);
+            for (int k = 0; k < nsplit; k++) {
+                const int w0 = (int)((int64_t)nwaves * k / nsplit), w1 = (int)((int64_t)nwaves * (k + 1) / nsplit);
+                split_t[k] = w0;
+                const int nw = w1 - w0;
+                const unsigned wgrid = (unsigned)((nw + 3) / 4);
+                const int2 *wtk = ctx->wave_tab.as<int2>() + w0;
+                if (fuse_stats) {
+                    if constexpr (sizeof(T) == 2)
+                        k_analyze_v3<DT, false, true><<<wgrid, 256, 0, ast>>>(raster, P, dtiles, dnorms,
+                                                                              ctx->luts.as<int16_t>(),
+                                                                              ctx->window.as<float>(), dana, wtk, nw);
+                } else {
+                    k_analyze_v3<DT, false><<<wgrid, 256, 0, ast>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
+                                                                    ctx->window.as<float>(), dana, wtk, nw);
+                }
+                k_analyze_v3<DT, true><<<wgrid, 256, 0, ast>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
+                                                               ctx->window.as<float>(), dana, wtk, nw);
+                if (nsplit > 1) FRS_HIP(hipEventRecord(ctx->split_ev[k], ast));
+            }
+            split_t[nsplit] = nwaves;
+            prof_end(ctx, "analyze", ev, ast);
+            if (!geo_hit) {  // the geometry's device copies are (being) uploaded on this stream: cache them
+                ctx->geo_tiles = tiles;
+                ctx->geo_plist.assign(hplist, hplist + npartial);
+                ctx->geo_nframes = nframes;
+                ctx->geo_ptrs[2] = nullptr;  // the partial list goes up below
+            }
+            ctx->geo_nwaves = nwaves;
+            ctx->geo_key = key;
+            ctx->geo_ptrs[0] = ctx->tiles.ptr;
+            ctx->geo_ptrs[1] = ctx->wave_tab.ptr;
+            ctx->geo_ptrs[3] = ctx->frame_tile.ptr;
         }
-        prof_end(ctx, "analyze", ev);
         // partial last frames: generic analysis + frame coding into compact slots, CRC-16 sealed in place
         int64_t *dpbytes = ctx->frame_bytes.as<int64_t>();  // [npartial] (< nframes + 1: below err_flag)
         if (npartial > 0) {
             prof_begin(ctx, "partial", &ev);
             FRS_HIP(ctx->plist.ensure(sizeof(int64_t) * (size_t)npartial));
-            FRS_HIP(hipMemcpyAsync(ctx->plist.ptr, hplist, sizeof(int64_t) * (size_t)npartial, hipMemcpyHostToDevice,
-                                   st));
+            if (!(dev_tiles && ctx->geo_ptrs[2] == ctx->plist.ptr))
+                FRS_HIP(hipMemcpyAsync(ctx->plist.ptr, hplist, sizeof(int64_t) * (size_t)npartial,
+                                       hipMemcpyHostToDevice, st));
+            ctx->geo_ptrs[2] = ctx->plist.ptr;
             FRS_HIP(ctx->slots.ensure((size_t)npartial * P.slot_words * 4));
             const int64_t *dpl = ctx->plist.as<int64_t>();
             k_analyze_partial<DT><<<dim3((unsigned)npartial, (unsigned)P.nch), kPartThreads, 0, st>>>(
@@ -3727,8 +3785,8 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
             int64_t *dmcb = ctx->mc_bytes.as<int64_t>();
             prof_begin(ctx, "encode", &ev);
             {
-                int nwg_max = 0;
-                FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nwg_max, k_encode_v3<DT, true>, 256, 0));
+                static int nwg_max = 0;  // (per instantiation; the same gfx950 target for every device)
+                if (nwg_max == 0) FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nwg_max, k_encode_v3<DT, true>, 256, 0));
                 int64_t grid = (int64_t)std::max(1, nwg_max) * ctx->num_cus;
                 grid = std::min<int64_t>(grid, (nsub + 3) / 4);
                 k_encode_v3<DT, true><<<(unsigned)grid, 256, 0, st>>>(
@@ -3777,7 +3835,7 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
             }
             return FRS_OK;
         }
-        FRS_HIP(hipMemsetAsync(dstatus, 0, sizeof(uint64_t) * (nframes + 1), st));
+        FRS_HIP(hipMemsetAsync(dstatus, 0, sizeof(uint64_t) * (nframes + 1) + 64, st));  // + the ticket counters
         // frame-header table by frame number within a stream (fast path: mono, 16-bit, blocksize 4096)
         int hdr_n = 0;
         {
@@ -3841,17 +3899,25 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                 ctx->hdr_tab_sr = d->sample_rate;
             }
         }
-        prof_begin(ctx, "encode", &ev);
         {
-            int nwg_max = 0;
-            FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nwg_max, k_encode_v3<DT>, 256, 0));
-            int64_t grid = (int64_t)std::max(1, nwg_max) * ctx->num_cus;
-            grid = std::min<int64_t>(grid, (nframes + 3) / 4);
-            k_encode_v3<DT><<<(unsigned)grid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(), dana,
-                                                            reinterpret_cast<uint8_t *>(arena_dev), arena_cap,
-                                                            ctx->frame_off.as<int64_t>(), dstatus, ticket, err_flag,
-                                                            ctx->frame_tile.as<int32_t>(), ctx->hdr_tab.as<uint4>(),
-                                                            hdr_n, ctx->slots.as<uint32_t>(), dpbytes);
+            static int nwg_max = 0;  // (per instantiation; the same gfx950 target for every device)
+            if (nwg_max == 0) FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nwg_max, k_encode_v3<DT>, 256, 0));
+            for (int k = 0; k < nsplit; k++) {
+                // frames of range k: its tiles' frames (the whole job when not split)
+                const int64_t f0 = nsplit > 1 ? tiles[split_t[k]].frame_base : 0;
+                const int64_t f1 = nsplit > 1 && k + 1 < nsplit ? tiles[split_t[k + 1]].frame_base : nframes;
+                if (nsplit > 1) FRS_HIP(hipStreamWaitEvent(st, ctx->split_ev[k], 0));
+                if (k == 0) prof_begin(ctx, "encode", &ev);
+                int64_t grid = (int64_t)std::max(1, nwg_max) * ctx->num_cus;
+                grid = std::min<int64_t>(grid, (f1 - f0 + 3) / 4);
+                k_encode_v3<DT><<<(unsigned)grid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(), dana,
+                                                                reinterpret_cast<uint8_t *>(arena_dev), arena_cap,
+                                                                ctx->frame_off.as<int64_t>(), dstatus, ticket + k,
+                                                                err_flag, ctx->frame_tile.as<int32_t>(),
+                                                                ctx->hdr_tab.as<uint4>(), hdr_n,
+                                                                ctx->slots.as<uint32_t>(), dpbytes, nullptr, nullptr,
+                                                                f0, f1);
+            }
         }
         prof_end(ctx, "encode", ev);
         FRS_HIP(ctx->host_pack.ensure(res_bytes));

@@ -88,6 +88,20 @@ struct frs_ctx {
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> ev_pending;
     // cached window (blocksize)
     int window_bs = 0;
+    // cached job geometry of the fast encode path: the tile table (partial frames marked), the analysis wave table,
+    // the partial-frame list and frame -> tile map stay on the device while the descriptor's geometry repeats (a
+    // bench or a server encoding same-shaped jobs skips their rebuild and uploads)
+    std::vector<int64_t> geo_key;      // descriptor geometry the cache holds (empty: nothing cached)
+    std::vector<frs::TileGeom> geo_tiles;  // host tile table, partial frames marked
+    std::vector<int64_t> geo_plist;    // partial-frame list
+    int64_t geo_nframes = 0;
+    int geo_nwaves = 0;
+    void *geo_ptrs[4] = {nullptr, nullptr, nullptr, nullptr};  // tiles, wave_tab, plist, frame_tile as uploaded
+    // fast encode path split into enc_split tile ranges ($FRS_ENC_SPLIT, 1..8): range k's analysis runs on aux_stream
+    // while range k - 1 is encoded on `stream` (the analysis' min/max bursts and last-round tail overlap the encoder)
+    int enc_split = 2;
+    hipStream_t aux_stream = nullptr;
+    hipEvent_t split_ev[9] = {};
 };
 
 #define FRS_HIP(call)                                                                  \
@@ -101,8 +115,8 @@ struct frs_ctx {
 
 namespace frs {
 // Kernel timing helpers (no-ops unless ctx->prof).
-void prof_begin(frs_ctx *ctx, const char *name, hipEvent_t *start);
-void prof_end(frs_ctx *ctx, const char *name, hipEvent_t start);
+void prof_begin(frs_ctx *ctx, const char *name, hipEvent_t *start, hipStream_t s = nullptr);
+void prof_end(frs_ctx *ctx, const char *name, hipEvent_t start, hipStream_t s = nullptr);
 void prof_collect(frs_ctx *ctx);
 
 int encode_job(frs_ctx *ctx, const frs_encode_desc *d, const void *raster_dev, void *arena_dev, int64_t arena_cap,

@@ -237,3 +237,35 @@ def test_host_encode_batched_tile_ranges(gpu_ctx):
     assert np.array_equal(off2, off[5:132] - off[5])
     assert a2.tobytes() == arena[off[5]:off[131]].tobytes()
     assert np.array_equal(mn2, mn[5:131]) and np.array_equal(mx2, mx[5:131])
+
+
+def test_geometry_cache_across_jobs(gpu_ctx):
+    """The context caches the fast path's job geometry (tile table, partial list, wave table, frame -> tile map)
+    while the descriptor repeats: jobs of alternating shapes, dtypes and tile sizes on one context -- each repeat
+    hits the cache, each change rebuilds it -- must all equal the oracle."""
+    rng = np.random.default_rng(11)
+    jobs = [(np.int16, (1100, 700), 512), (np.int16, (1100, 700), 256), (np.uint16, (1100, 700), 512),
+            (np.int16, (900, 1300), 512)]
+    bands = [((rng.normal(0, 40, shape).cumsum(axis=1)) % 20000).astype(dt) for dt, shape, _ in jobs]
+    refs = [O.encode_tiles(b, t)[0].tobytes() for b, (_, _, t) in zip(bands, jobs)]
+    for i in (0, 0, 1, 1, 0, 2, 2, 0, 3, 3, 0):
+        arena, off, mn, mx, bps = _gpu_tiles(gpu_ctx, bands[i], jobs[i][2])
+        assert arena.tobytes() == refs[i], f"job {i}"
+
+
+@pytest.mark.parametrize("split", [1, 2, 3, 8])
+def test_split_encode_matches_oracle(split, monkeypatch):
+    """$FRS_ENC_SPLIT: the fast path encodes its tile ranges in turn on the main stream while the next range is
+    analysed on a second stream.  Every split must give the oracle's bytes (look-back across launches, one ticket
+    counter per range, ranges of whole tiles); the geometry cache is reused across the repeats."""
+    from flac_raster_amd import _native
+    monkeypatch.setenv("FRS_ENC_SPLIT", str(split))
+    rng = np.random.default_rng(21)
+    band = (rng.normal(0, 30, (2048, 3072)).cumsum(axis=0) % 30000).astype(np.int16)  # 384 tiles of 128^2
+    o_arena, o_off, o_mn, o_mx = O.encode_tiles(band, 128, threads=4)
+    with _native.Context(0) as ctx:
+        for _ in range(2):
+            arena, off, mn, mx, bps = _gpu_tiles(ctx, band, 128)
+            assert list(off) == list(o_off)
+            assert arena.tobytes() == o_arena.tobytes()
+            assert list(mn) == list(o_mn) and list(mx) == list(o_mx)
