@@ -1848,7 +1848,39 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     __builtin_amdgcn_wave_barrier();
     if (failed || !info.valid) return;
     const int16_t *x16 = reinterpret_cast<const int16_t *>(xout);
-    for (int i = lane; i < bs; i += 64) put(i, (int32_t)((uint32_t)(int32_t)x16[i] << w));
+    const int dt = fused ? dout.dtype : -1;
+    if ((dt == FRS_DT_I16 || dt == FRS_DT_U16 || dt == FRS_DT_U8) && dout.shift == 0 && (obase & 7) == 0 &&
+        (bs & 7) == 0) {
+        // de-normalised 1- and 2-byte outputs: eight samples per lane and step, one 16-byte LDS read and one 16- (8-)
+        // byte store (the per-sample loop issued 64 scattered 2-byte stores per lane: 13.6 of a frame's 137 us)
+        const uint4 *x8 = reinterpret_cast<const uint4 *>(xout);
+        for (int g = lane; g < (bs >> 3); g += 64) {
+            const uint4 v = x8[g];
+            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+            uint32_t ob[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const int32_t x = (int32_t)(int16_t)(wv[j >> 1] >> (16 * (j & 1)));
+                const float f = (float)((int32_t)((uint32_t)x << w)) * (1.0f / 32768.0f);
+                float a = __fadd_rn(f, 1.0f);
+                a = __fmul_rn(a, 0.5f);  // == __fdiv_rn(a, 2.0f): scaling by a power of two
+                a = __fmul_rn(a, dnp.x);
+                a = __fadd_rn(a, dnp.y);
+                ob[j] = (uint32_t)(int64_t)rintf(a);
+            }
+            if (dt == FRS_DT_U8) {
+                reinterpret_cast<uint2 *>(static_cast<uint8_t *>(dout.out) + obase)[g] =
+                    make_uint2((ob[0] & 0xFF) | ((ob[1] & 0xFF) << 8) | ((ob[2] & 0xFF) << 16) | (ob[3] << 24),
+                               (ob[4] & 0xFF) | ((ob[5] & 0xFF) << 8) | ((ob[6] & 0xFF) << 16) | (ob[7] << 24));
+            } else {
+                reinterpret_cast<uint4 *>(static_cast<uint16_t *>(dout.out) + obase)[g] =
+                    make_uint4((ob[0] & 0xFFFF) | (ob[1] << 16), (ob[2] & 0xFFFF) | (ob[3] << 16),
+                               (ob[4] & 0xFFFF) | (ob[5] << 16), (ob[6] & 0xFFFF) | (ob[7] << 16));
+            }
+        }
+    } else {
+        for (int i = lane; i < bs; i += 64) put(i, (int32_t)((uint32_t)(int32_t)x16[i] << w));
+    }
     if (lane == 0) atomicAdd(nvalid, 1);
 }
 

@@ -40,8 +40,11 @@ def _bands():
     flat[::5, :] = 100
     spiky = (500 + 20 * np.sin(np.linspace(0, 12, 256 * 256)).reshape(256, 256)).astype(np.int16)
     spiky.flat[rng.choice(spiky.size, 40, replace=False)] = rng.choice([-30000, 30000], 40).astype(np.int16)
+    # uint8 output through the decoders' 8-byte vector stores (tile 200: a 3136-sample last frame)
+    u8 = (128 + 90 * np.sin(np.linspace(0, 40, 400 * 600)).reshape(400, 600) + rng.normal(0, 4, (400, 600))
+          ).clip(0, 255).astype(np.uint8)
     return [("dem", dem, 256), ("noise", noise, 128), ("steps", steps, 160), ("odd", odd, 128),
-            ("flat", flat, 256), ("spiky", spiky, 256)]
+            ("flat", flat, 256), ("spiky", spiky, 256), ("u8", u8, 200)]
 
 
 DECODERS = {"pipe": {"FRS_DECODE_LANE": "0"},      # two-wave pipelined decoder (latency; C5 queries)
