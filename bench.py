@@ -242,8 +242,6 @@ def bbox_extract(ctx, comm, raster, arena, off, tmin, tmax, H, W, T, row0, count
     out = ctx.alloc(T * T * 2)
     host = ctx.pinned(T * T * 2).view(np.int16)  # page-locked: the tile comes back at DMA rate
     lat, checked, lossless = [], 0, True
-    ctx.profile(True)
-    ctx.profile_reset()
     nwarm = min(10, len(mine))
     for k, bbox in enumerate(mine[:nwarm] + mine):  # untimed warm-up queries first
         t0 = time.perf_counter()
@@ -264,6 +262,17 @@ def bbox_extract(ctx, comm, raster, arena, off, tmin, tmax, H, W, T, row0, count
             got = host[:n].reshape(wnd["height"], wnd["width"])
             lossless &= bool(np.array_equal(got, ref[:, wnd["col_off"]:wnd["col_off"] + wnd["width"]]))
             checked += 1
+    # kernel times from a separate profiled pass over the first 100 queries (the profile's events between the
+    # kernels add ~10 us each to a query, so the timed pass above runs without them)
+    ctx.profile(True)
+    ctx.profile_reset()
+    for bbox in mine[:100]:
+        f = streaming.first_intersecting(index, bbox)
+        i = f["frame_id"] - first_tile
+        n = f["window"]["width"] * f["window"]["height"]
+        ctx.decode_tiles_device(arena, np.array([off[i], off[i + 1]], dtype=np.int64), [n], channels=1, bps=16,
+                                data_min=[float(tmin[i])], data_max=[float(tmax[i])], dtype=np.int16, out=out)
+    ctx.sync()
     ctx.profile(False)
     kern = {k: round(ctx.profile_avg_ms(k), 4) for k in ("decode", "decode_span", "decode_frames")}
     out.close()

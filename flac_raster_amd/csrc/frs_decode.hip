@@ -27,6 +27,7 @@ namespace frs {
 
 __constant__ uint8_t d_crc8[256];
 __constant__ uint16_t d_crc16[256];
+__device__ __attribute__((aligned(16))) uint16_t d_crc16x4[4][256];  // slice-by-4 tables (T_0 = d_crc16), host-computed once per device
 
 struct FrameHdr {
     int32_t ok;
@@ -119,6 +120,9 @@ __device__ inline int64_t wave_sum_i64(int64_t v) {
 // so candidates are ordered by (k, lane, j).  Returns the lane's candidate count.
 constexpr int kSelSteps = kSelBytes / (kSelThreads / 64) / 1024;  // 16 steps of 1 KB per wave
 static_assert(kSelSteps == 16, "64 KB blocks of 4 waves");
+// small ranges (a C5 query's tile, <= 4 MB): 16 KB blocks of 4 waves x 4 steps, so a 0.5 MB tile spreads over 32
+// work-groups instead of 8 (the one-pass selection is latency-bound there)
+constexpr int kSelStepsSmall = 4;
 
 // CRC-8 (poly 0x07) of one byte folded into c, bitwise (no table: the header check runs from registers)
 __device__ inline uint32_t crc8_byte(uint32_t c, uint32_t b) {
@@ -228,8 +232,10 @@ __device__ __attribute__((noinline)) uint32_t sel_check_candidates(uint4 cur, ui
 // Only a header starting in the wave's last 16 bytes takes the global parse.  Headers are bounded by the blob end
 // (not the stream end: a header straddling a stream boundary becomes a candidate whose CRC span never verifies).
 // Returns the lane's candidate count.
+template <int STEPS = kSelSteps>
 __device__ inline int sel_masks_co(const uint8_t *blob, int64_t nbytes, const int64_t *soff, int ns, int channels,
                                    int stream_bps, int64_t qw, int lane, uint32_t *m) {
+    constexpr int kSelSteps = STEPS;
     const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
     const uint8_t *base = blob - lead;
     const int64_t qend = nbytes + lead;
@@ -304,8 +310,10 @@ __device__ inline int wave_excl_scan_i32(int v, int lane, int &total) {
 }
 
 // candidate positions of one wave in (k, lane, j) order from output index `base`; past the cap only counted
+template <int STEPS = kSelSteps>
 __device__ inline void sel_emit_co(const uint32_t *m, int64_t qw, int lane, int lead, int64_t base, int64_t *cpos,
                                    int64_t cap) {
+    constexpr int kSelSteps = STEPS;
 #pragma unroll
     for (int k = 0; k < kSelSteps; k++) {
         int tot;
@@ -324,10 +332,12 @@ __device__ inline void sel_emit_co(const uint32_t *m, int64_t qw, int lane, int 
     }
 }
 
+template <int STEPS>
 __global__ void __launch_bounds__(kSelThreads) k_sync_select(const uint8_t *blob, int64_t nbytes, const int64_t *soff,
                                                            int ns, int channels, int stream_bps, uint64_t *status,
                                                            unsigned long long *ticket, uint32_t epoch, int64_t nblocks,
                                                            int64_t *cpos, int64_t cap, int *counts) {
+    constexpr int kSelSteps = STEPS, kSelBytes = STEPS * 1024 * (kSelThreads / 64);
     __shared__ int64_t s_ord, s_base;
     __shared__ int s_wsum[kSelThreads / 64];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -341,7 +351,7 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_select(const uint8_t *blob
     const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
     const int64_t qw = ord * kSelBytes + (int64_t)(kSelBytes / 4) * wv;
     uint32_t m[kSelSteps];
-    int cnt = sel_masks_co(blob, nbytes, soff, ns, channels, stream_bps, qw, lane, m);
+    int cnt = sel_masks_co<STEPS>(blob, nbytes, soff, ns, channels, stream_bps, qw, lane, m);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
     if (lane == 0) s_wsum[wv] = cnt;
@@ -393,7 +403,7 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_select(const uint8_t *blob
         }
     }
     __syncthreads();
-    sel_emit_co(m, qw, lane, lead, s_base + wbase, cpos, cap);
+    sel_emit_co<STEPS>(m, qw, lane, lead, s_base + wbase, cpos, cap);
 }
 
 // Large ranges (a whole arena): the single pass above serialises on its look-back (the inclusive prefix advances one
@@ -545,7 +555,7 @@ __device__ inline uint32_t load_word_guarded(const uint8_t *blob, int64_t k, int
 }
 
 constexpr int kSpanWords = 6144;  // 24 KB stage
-__device__ uint16_t d_xpow_lo[256];   // x^(8m) mod P, m < 256
+__device__ __attribute__((aligned(16))) uint16_t d_xpow_lo[256];   // x^(8m) mod P, m < 256
 __device__ uint16_t d_xpow_hi[4096];  // x^(8*256*m) mod P
 
 __device__ inline uint32_t dec_gfmul(uint32_t a, uint32_t b) {
@@ -567,20 +577,13 @@ __global__ void __launch_bounds__(64) k_span_crc_wave(const uint8_t *blob, const
     const int nc = *ncand;
     if ((int)blockIdx.x >= nc || nc > cand_cap) return;
     __shared__ uint32_t stage[kSpanWords + 1];
-    __shared__ uint16_t t4[4][256];
-    __shared__ uint16_t xlo[256];
+    __shared__ __attribute__((aligned(16))) uint16_t t4[4][256];
+    __shared__ __attribute__((aligned(16))) uint16_t xlo[256];
     const int lane = threadIdx.x;
-    for (int k = lane; k < 1024; k += 64) (&t4[0][0])[k] = 0;
-    for (int k = lane; k < 256; k += 64) {
-        uint16_t c = d_crc16[k];
-        t4[0][k] = c;
-#pragma unroll
-        for (int j = 1; j < 4; j++) {
-            c = (uint16_t)(((c << 8) & 0xFFFF) ^ d_crc16[c >> 8]);
-            t4[j][k] = c;
-        }
-        xlo[k] = d_xpow_lo[k];
-    }
+    // tables from their global copies: independent 16-byte loads (deriving T_1..T_3 from T_0 here was three
+    // dependent constant-memory lookups per entry at the start of every work-group)
+    for (int k = lane; k < 128; k += 64) reinterpret_cast<uint4 *>(&t4[0][0])[k] = reinterpret_cast<const uint4 *>(&d_crc16x4[0][0])[k];
+    for (int k = lane; k < 32; k += 64) reinterpret_cast<uint4 *>(xlo)[k] = reinterpret_cast<const uint4 *>(d_xpow_lo)[k];
     __syncthreads();
     for (int i = blockIdx.x; i < nc; i += gridDim.x) {
         const int64_t p = cpos[i];
@@ -659,16 +662,9 @@ __global__ void __launch_bounds__(64) k_span_crc_wave(const uint8_t *blob, const
 __global__ void __launch_bounds__(256) k_span_crc_lane(const uint8_t *blob, const int64_t *soff, int ns,
                                                       const int64_t *cpos, const int *ncand, int cand_cap,
                                                       int64_t max_frame, int64_t *ends, int32_t *nexti) {
-    __shared__ uint16_t t4[4][256];
-    for (int k = threadIdx.x; k < 256; k += blockDim.x) {
-        uint16_t c = d_crc16[k];
-        t4[0][k] = c;
-#pragma unroll
-        for (int j = 1; j < 4; j++) {
-            c = (uint16_t)(((c << 8) & 0xFFFF) ^ d_crc16[c >> 8]);
-            t4[j][k] = c;
-        }
-    }
+    __shared__ __attribute__((aligned(16))) uint16_t t4[4][256];
+    for (int k = threadIdx.x; k < 128; k += blockDim.x)
+        reinterpret_cast<uint4 *>(&t4[0][0])[k] = reinterpret_cast<const uint4 *>(&d_crc16x4[0][0])[k];
     __syncthreads();
     const int nc = *ncand;
     if (nc > cand_cap) return;
@@ -776,14 +772,12 @@ __global__ void __launch_bounds__(64) k_chain_lds(const int64_t *soff, int ns, c
     __syncthreads();
     const int c0 = rng[0], c1 = rng[1];
     const bool in_lds = c1 - c0 <= kChainLds;
-    if (in_lds)
-        for (int k = lane; k < c1 - c0; k += 64) nx[k] = nexti[c0 + k];
-    __syncthreads();
-    if (!in_lds && c0 < c1 && cpos[c0] == soff[s] && nf > 0) {
-        // a long stream (one multi-channel file: tens of thousands of frames) would be walked one dependent global
-        // load per frame.  Optimistic parallel ranking instead: the verified candidates (link != -1) in position
-        // order ARE the chain when there are nf of them, each links to the next and the last to the stream end --
-        // checked below; anything else (a false sync with a verified span) falls back to the exact walk.
+    if (c0 < c1 && cpos[c0] == soff[s] && nf > 0) {
+        // a walk is one dependent load per frame (a long stream: tens of thousands of global loads; a C5 tile: 64
+        // dependent LDS reads by one lane, ~10 us).  Optimistic parallel ranking instead: the verified candidates
+        // (link != -1) in position order ARE the chain when there are nf of them, each links to the next and the last
+        // to the stream end -- checked below; anything else (a false sync with a verified span) falls back to the
+        // exact walk.
         int64_t cnt = 0;
         for (int i0 = c0; i0 < c1; i0 += 256) {
             int32_t v[4];
@@ -815,6 +809,9 @@ __global__ void __launch_bounds__(64) k_chain_lds(const int64_t *soff, int ns, c
         if (good) return;
         __threadfence();
     }
+    if (in_lds)
+        for (int k = lane; k < c1 - c0; k += 64) nx[k] = nexti[c0 + k];
+    __syncthreads();
     if (lane != 0) return;
     bool ok = c0 < c1 && cpos[c0] == soff[s];
     int64_t k = 0;
@@ -1563,16 +1560,19 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
             finish(kPipeDone, ok);
             return;
         }
-        if (t == 1) {  // VERBATIM: samples straight out, 64 per coalesced store
-            uint32_t vo = 0;
-            for (int i = 0; i < bs; i++) {
-                const int32_t x = br.sbits(sbps);
-                vo = lane == (i & 63) ? ((uint32_t)x << w) : vo;
-                if ((i & 63) == 63 || i == bs - 1) {
-                    const int b0 = i & ~63;
-                    if (b0 + lane <= i) put(b0 + lane, (int32_t)vo);
-                }
+        if (t == 1) {  // VERBATIM: fixed-width samples, so sample i sits at bit P0 + i * sbps -- lane-parallel
+            // (the scalar reader took one dependent read per sample: a tile holding one VERBATIM frame took ~0.3 ms
+            // longer than the others, the C5 p90)
+            const uint32_t P0 = br.pos(), Pe = P0 + (uint32_t)bs * (uint32_t)sbps;
+            if (Pe > lim) { finish(kPipeError, 0); return; }
+            for (int i = lane; i < bs; i += 64) {
+                const uint32_t b = P0 + (uint32_t)i * (uint32_t)sbps, wi = b >> 5, sh = b & 31u;
+                const uint32_t hi = stage[wi], lo = stage[wi + 1];
+                const uint32_t v = sh ? __builtin_amdgcn_alignbit(hi, lo, 32u - sh) : hi;
+                const int32_t x = (int32_t)v >> (32 - sbps);
+                put(i, (int32_t)((uint32_t)x << w));
             }
+            br.seek(Pe);
             const int ok = end_ok();
             if (ok && lane == 0) atomicAdd(nvalid, 1);
             finish(kPipeDone, ok);
@@ -2408,6 +2408,16 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         }
         FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(d_crc8), t8, sizeof(t8), 0, hipMemcpyHostToDevice, st));
         FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(d_crc16), t16, sizeof(t16), 0, hipMemcpyHostToDevice, st));
+        static uint16_t t16x4[4][256];
+        for (int i = 0; i < 256; i++) {
+            uint16_t c = t16[i];
+            t16x4[0][i] = c;
+            for (int j = 1; j < 4; j++) {
+                c = (uint16_t)(((c << 8) & 0xFFFF) ^ t16[c >> 8]);
+                t16x4[j][i] = c;
+            }
+        }
+        FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(d_crc16x4), t16x4, sizeof(t16x4), 0, hipMemcpyHostToDevice, st));
         auto mulmod = [](uint32_t a, uint32_t b) {
             uint32_t r = 0;
             for (int i = 15; i >= 0; i--) {
@@ -2465,7 +2475,11 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     // frame data, ~1e-7 per byte) with a wide margin; a crafted stream with more is rejected (nothing is written
     // past the cap).  Indices stay below 2^31.
     const int64_t cand_cap = std::min<int64_t>(2 * frames + blob_bytes / 1024 + 4096, (int64_t)0x7FFFFFF0);
-    const int64_t nblocks = (blob_bytes + (int64_t)(reinterpret_cast<uintptr_t>(blob_dev) & 15) + kSelBytes - 1) / kSelBytes;
+    const int64_t lead_bytes = blob_bytes + (int64_t)(reinterpret_cast<uintptr_t>(blob_dev) & 15);
+    const int64_t kSmallBytes = (int64_t)kSelStepsSmall * 1024 * (kSelThreads / 64);
+    const bool sel_small = (lead_bytes + kSmallBytes - 1) / kSmallBytes <= kSelOnePassBlocks;
+    const int64_t sel_bytes = sel_small ? kSmallBytes : kSelBytes;
+    const int64_t nblocks = (lead_bytes + sel_bytes - 1) / sel_bytes;
     if (nblocks > (int64_t)0xFFFFFFFF) {
         ctx->err = "decode range too large";
         return FRS_E_UNSUPPORTED;
@@ -2519,9 +2533,14 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     hipEvent_t ev;
     prof_begin(ctx, "decode", &ev);
     if (nblocks <= kSelOnePassBlocks) {
-        k_sync_select<<<(unsigned)nblocks, kSelThreads, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams, channels, bps,
-                                                                 ctx->dec_status.as<uint64_t>(), ticket,
-                                                                 ctx->dec_epoch, nblocks, cpos, cand_cap, ncand);
+        if (sel_small)
+            k_sync_select<kSelStepsSmall><<<(unsigned)nblocks, kSelThreads, 0, st>>>(
+                blob_dev, blob_bytes, dsoff, nstreams, channels, bps, ctx->dec_status.as<uint64_t>(), ticket,
+                ctx->dec_epoch, nblocks, cpos, cand_cap, ncand);
+        else
+            k_sync_select<kSelSteps><<<(unsigned)nblocks, kSelThreads, 0, st>>>(
+                blob_dev, blob_bytes, dsoff, nstreams, channels, bps, ctx->dec_status.as<uint64_t>(), ticket,
+                ctx->dec_epoch, nblocks, cpos, cand_cap, ncand);
     } else {
         // (its own buffer: the one-pass status words must keep their epoch tags)
         FRS_HIP(ctx->dec_sel.ensure(sizeof(int64_t) * (size_t)(2 * nblocks + 4)));

@@ -14,16 +14,16 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-
          "-Wno-unused-value"]
 
 
-def build_variant(name, patch_fn, src_name="frs_encode.hip"):
+def build_variant(name, patch_fn, src_name="frs_encode.hip", extra_flags=()):
     OUT.mkdir(exist_ok=True)
     src = (CSRC / src_name).read_text()
     new = patch_fn(src)
-    if new == src and name not in ("base", "cur"):
+    if new == src and name not in ("base", "cur") and not extra_flags:
         raise ValueError(f"variant {name}: patch did not apply")
     tmp = OUT / f"{name}_{src_name}"
     tmp.write_text(new)
     obj = OUT / f"{name}_{src_name}.o"
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", *FLAGS, f"-I{CSRC}", "-c", "-o", str(obj),
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", *FLAGS, *extra_flags, f"-I{CSRC}", "-c", "-o", str(obj),
                     str(tmp)], check=True)
     others = [str(p) for p in sorted(CSRC.glob("*.o")) if p.name != src_name.replace(".hip", ".o")]
     lib = OUT / f"lib{name}.so"

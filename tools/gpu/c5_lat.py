@@ -28,7 +28,8 @@ def main():
     out = ctx.alloc(T * T * 2)
     host = ctx.pinned(T * T * 2).view(np.int16)
     ts, td, tc = [], [], []
-    ctx.profile(True)
+    prof = len(sys.argv) > 2 and sys.argv[2] == "prof"  # kernel times (the profile's events add ~10 us per kernel)
+    ctx.profile(prof)
     ctx.profile_reset()
     for k, bbox in enumerate(qs[:10] + qs):
         t0 = time.perf_counter()
@@ -49,7 +50,9 @@ def main():
     p = lambda a: round(float(np.percentile(np.array(a) * 1e3, 50)), 4)
     tot = [a + b + c for a, b, c in zip(ts, td, tc)]
     print(json.dumps({"select_ms": p(ts), "decode_call_ms": p(td), "download_ms": p(tc), "total_p50": p(tot),
-                      "total_p90": round(float(np.percentile(np.array(tot) * 1e3, 90)), 4), "kernels": kern}))
+                      "total_p90": round(float(np.percentile(np.array(tot) * 1e3, 90)), 4),
+                      "total_pct_10_25_75_95_99": [round(float(np.percentile(np.array(tot) * 1e3, q)), 4)
+                                                   for q in (10, 25, 75, 95, 99)], "kernels": kern}))
 
 
 if __name__ == "__main__":
