@@ -103,7 +103,7 @@ int frs_ctx_create(int device, frs_ctx **out) {
     const char *dl = getenv("FRS_DECODE_LANE");
     ctx->decode_lane = dl ? (dl[0] == '1' ? 1 : 0) : -1;
     const char *av = getenv("FRS_ANA_V4");
-    if (av) ctx->ana_v4 = av[0] != '0';
+    if (av) ctx->ana_v4 = av[0] == '1';
     const char *es = getenv("FRS_ENC_SPLIT");
     if (es) ctx->enc_split = std::max(1, std::min(8, atoi(es)));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {

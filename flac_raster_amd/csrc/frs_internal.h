@@ -103,7 +103,7 @@ struct frs_ctx {
     // slots and flags tagged with a per-call epoch so they are never cleared between calls; $FRS_ANA_V4=0: k_analyze_v3
     DevBuf ana_ctl;
     uint32_t enc_epoch = 0;
-    bool ana_v4 = true;
+    bool ana_v4 = false;  // (experimental: $FRS_ANA_V4=1)
     int enc_split = 1;  // (2-4 measured slower on C4: both kernels are issue-bound, so sharing the CUs gains nothing)
     hipStream_t aux_stream = nullptr;
     hipEvent_t split_ev[9] = {};
