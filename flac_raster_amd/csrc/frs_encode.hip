@@ -2192,7 +2192,12 @@ __global__ void __launch_bounds__(256, 4) k_analyze_v4(const typename Elem<DT>::
                 break;
             }
         }
-        const TileNorm tn = norms[t];
+        // the tile's parameters through VECTOR loads: a wave-uniform address compiles to scalar loads, and the scalar
+        // data cache is not invalidated by the acquire (it still held the line from an earlier tile of this loop,
+        // read before the stats worker wrote it: stale parameters, then a stalled encode)
+        const TileNorm *tnp = norms + t;
+        asm volatile("" : "+v"(tnp));
+        const TileNorm tn = *tnp;
         const int mode = tn.mode;
         if (!(mode == kNormLut || mode == kNormZero)) continue;  // slow class: the SLOW launch analyses it
         // loop-invariant loads (the window) must not be hoisted out of the tile loop: hoisted, they held ~60 VGPRs

@@ -271,7 +271,7 @@ def test_split_encode_matches_oracle(split, monkeypatch):
             assert list(mn) == list(o_mn) and list(mx) == list(o_mx)
 
 
-@pytest.mark.parametrize("v4", ["0"])  # "1": experimental, under investigation (a hang on sample_dem)
+@pytest.mark.parametrize("v4", ["0", "1"])
 def test_role_split_analysis_matches_oracle(v4, monkeypatch):
     """$FRS_ANA_V4: the fused analysis as one wave per tile (k_analyze_v3, 0) or role-split (k_analyze_v4, 1: stats
     workers publish tiles, the other waves run the sums) -- the same bytes as the oracle either way, over repeated
