@@ -2120,126 +2120,6 @@ __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *
     out[f * P.nch + chn] = analysis_finish(acc, or_acc, n, P, ft);
 }
 
-// ------------------------------------------------------------------------------ k_analyze_v4
-// Role-split fused analysis (16-bit mono streams, one wave per tile, 16-B aligned rows): the same per-tile work as
-// k_analyze_v3<DT, false, true>, but the HBM-bound min/max pass no longer holds the slots of the fp64-bound
-// autocorrelation.  In v3 every wave read its tile for min/max before its sums (C4 timeline, tools/ana_timeline.py:
-// stats phase 437 us median against 402 us of sums, ~2000 of the 4096 slots in a stats pass at any time and a
-// 330 us start-up burst with the VALU idle).  Here the first wave to arrive on each SIMD (an epoch-tagged slot per
-// SIMD, keyed by HW_ID / XCC_ID) becomes a stats worker: it takes tiles in order, computes min/max and the
-// normalisation, writes the tile's LUT to HBM and publishes the tile with an epoch-tagged flag; every other wave takes
-// tiles in the same order, waits for the flag, copies the LUT into its LDS slot and runs ana_autoc.  A stats worker
-// whose queue is empty joins the autocorrelation queue.  Roles only place the work: any assignment (one stats worker
-// or all of them) gives the same results.  No deadlock: an autocorrelation wave waits only for a tile whose stats a
-// running stats worker will reach (stats workers never wait, and the first wave of the launch is one).  Slow-class
-// tiles (fast / exact division) only get their parameters here (k_analyze_v3<DT, true> analyses them).
-constexpr int kSimdSlots = 8192;  // role slots: (XCC, SE, SH, CU, SIMD) keys of an MI355X fit in 13 bits
-template <int DT>
-__global__ void __launch_bounds__(256, 4) k_analyze_v4(const typename Elem<DT>::T *raster, EncodeParams P,
-                                                   const TileGeom *tiles, TileNorm *norms, int16_t *luts,
-                                                   const float *__restrict__ window, SubAnalysis *out, int ntiles,
-                                                   uint32_t *ctrs, uint32_t *simd_slot, uint32_t *tile_flag,
-                                                   uint32_t epoch, int *err) {
-    static_assert(sizeof(typename Elem<DT>::T) == 2 && !Elem<DT>::is_float, "16-bit samples");
-    __shared__ int16_t slut[4][kLutCap];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int16_t *wl = slut[wave];
-    // role: the first wave on this SIMD in this launch collects tile stats
-    bool stats_role;
-    {
-        uint32_t prev = 0;
-        if (lane == 0) {
-            const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID
-            const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
-            const uint32_t key = ((((xcc & 15u) * 8u + ((hw >> 13) & 7u)) * 2u + ((hw >> 12) & 1u)) * 16u +
-                                  ((hw >> 8) & 15u)) * 4u + ((hw >> 4) & 3u);
-            prev = atomicExch(&simd_slot[key & (kSimdSlots - 1)], epoch);
-        }
-        stats_role = __builtin_amdgcn_readfirstlane(prev) != epoch;
-    }
-    if (stats_role) {
-        while (true) {
-            uint32_t tq = 0;
-            if (lane == 0) tq = atomicAdd(&ctrs[0], 1u);
-            const int t = (int)__builtin_amdgcn_readfirstlane(tq);
-            if (t >= ntiles) break;
-            const TileGeom g = tiles[t];
-            const typename Elem<DT>::T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
-            TileNorm tn;
-            wave_tile_minmax<DT>(base, P.row_stride, g, lane, tn.imin, tn.imax);
-            tile_norm_finalize<DT>(tn, P.norm_mode, P.scale_bits);
-            if (lane == 0) norms[t] = tn;
-            if (tn.mode == kNormLut) {
-                int16_t *glut = luts + (int64_t)t * kLutCap;
-                const int64_t R = tn.imax - tn.imin;
-                for (int64_t d = lane; d <= R; d += 64) glut[d] = lut_entry<DT>(tn, d);
-            }
-            __threadfence();  // norms + LUT visible device-wide before the flag (release)
-            if (lane == 0) __hip_atomic_store(&tile_flag[t], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    while (true) {
-        uint32_t tq = 0;
-        if (lane == 0) tq = atomicAdd(&ctrs[1], 1u);
-        const int t = (int)__builtin_amdgcn_readfirstlane(tq);
-        if (t >= ntiles) break;
-        // the tile's stats: claimed by a running stats worker (its queue is ahead of this one), published once
-        long spins = 0;
-        while (__hip_atomic_load(&tile_flag[t], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-            __builtin_amdgcn_s_sleep(8);
-            if (++spins > (1l << 22)) {  // (never: a stats worker always finishes its tile) bounded anyway: the
-                if (lane == 0) atomicOr(err, 32);  // host reruns the job on the generic kernels
-                break;
-            }
-        }
-        // the tile's parameters through VECTOR loads: a wave-uniform address compiles to scalar loads, and the scalar
-        // data cache is not invalidated by the acquire (it still held the line from an earlier tile of this loop,
-        // read before the stats worker wrote it: stale parameters, then a stalled encode)
-        const TileNorm *tnp = norms + t;
-        asm volatile("" : "+v"(tnp));
-        const TileNorm tn = *tnp;
-        const int mode = tn.mode;
-        if (!(mode == kNormLut || mode == kNormZero)) continue;  // slow class: the SLOW launch analyses it
-        // loop-invariant loads (the window) must not be hoisted out of the tile loop: hoisted, they held ~60 VGPRs
-        // across the loop (170 VGPRs, 3 waves per SIMD; one iteration compiles to 110)
-        const float *window_t = window;
-        const typename Elem<DT>::T *raster_t = raster;
-        const int16_t *luts_t = luts;
-        int16_t *wl_t = wl;
-        int lane_t = lane;
-        asm volatile("" : "+s"(window_t), "+s"(raster_t), "+s"(luts_t), "+v"(wl_t), "+v"(lane_t) :: "memory");
-        const TileGeom g = tiles[t];
-        const int nfull = g.nframes - (g.partial ? 1 : 0);
-        if (nfull == 0) continue;
-        const typename Elem<DT>::T *base = raster_t + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
-        const bool live = lane_t < nfull;
-        const int64_t fk = live ? lane : nfull - 1;  // dead lanes re-read the tile's last full frame
-        const int64_t f = g.frame_base + fk;
-        const int64_t s0 = fk * P.blocksize;
-        const int64_t tile_px = (int64_t)g.h * g.w;
-        const int n = live ? (int)min((int64_t)P.blocksize, tile_px - s0) : 0;
-        constexpr int kChunk = 64;
-        const int vec = (g.w % kChunk) == 0 ? P.vec_ok : 0;
-        double acc[kMaxLpc + 1];
-#pragma unroll
-        for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
-        uint32_t or_acc = 0, ft[5];
-        const int16_t *glut = luts_t + (int64_t)t * kLutCap;
-        if (mode == kNormLut) {
-            const int64_t R = tn.imax - tn.imin;
-            for (int64_t d = lane_t; d <= R; d += 64) wl_t[d] = glut[d];
-            __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's LUT stores have landed (each wave reads only its own)
-            __builtin_amdgcn_wave_barrier();
-            ana_autoc<DT, kAnaKindLds, kChunk>(base, P, g, s0, tn, wl_t, glut, window_t, vec, acc, or_acc, ft);
-        } else {
-            ana_autoc<DT, kAnaKindZero, kChunk>(base, P, g, s0, tn, wl_t, glut, window_t, vec, acc, or_acc, ft);
-        }
-        if (live) out[f] = analysis_finish(acc, or_acc, n, P, ft);
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_wave_barrier();  // the LDS LUT slot is reused by the next tile
-    }
-}
-
 // ---- wave helpers (64 lanes)
 __device__ inline uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
@@ -3845,28 +3725,7 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                 const int nw = w1 - w0;
                 const unsigned wgrid = (unsigned)((nw + 3) / 4);
                 const int2 *wtk = ctx->wave_tab.as<int2>() + w0;
-                if (fuse_stats && ctx->ana_v4 && nsplit == 1 && P.nch == 1) {
-                    if constexpr (sizeof(T) == 2) {
-                        // role-split analysis: ctl = [2 queue counters | kSimdSlots role slots | ntiles stats flags]
-                        const size_t before = ctx->ana_ctl.bytes;
-                        FRS_HIP(ctx->ana_ctl.ensure(sizeof(uint32_t) * (2 + (size_t)kSimdSlots + (size_t)ntiles)));
-                        if (ctx->ana_ctl.bytes != before || ++ctx->enc_epoch == 0) {  // new words / epoch wrap
-                            FRS_HIP(hipMemsetAsync(ctx->ana_ctl.ptr, 0, ctx->ana_ctl.bytes, ast));
-                            if (ctx->enc_epoch == 0) ctx->enc_epoch = 1;
-                        }
-                        uint32_t *ctl = ctx->ana_ctl.as<uint32_t>();
-                        FRS_HIP(hipMemsetAsync(ctl, 0, 2 * sizeof(uint32_t), ast));
-                        static int occ4 = 0;  // (per instantiation)
-                        if (occ4 == 0)
-                            FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ4, k_analyze_v4<DT>, 256, 0));
-                        const int64_t g4 = std::min<int64_t>((int64_t)std::max(1, occ4) * ctx->num_cus,
-                                                             ((int64_t)ntiles + 4 * ctx->num_cus + 3) / 4);
-                        k_analyze_v4<DT><<<(unsigned)g4, 256, 0, ast>>>(raster, P, dtiles, dnorms,
-                                                                        ctx->luts.as<int16_t>(), ctx->window.as<float>(),
-                                                                        dana, ntiles, ctl, ctl + 2,
-                                                                        ctl + 2 + kSimdSlots, ctx->enc_epoch, err_flag);
-                    }
-                } else if (fuse_stats) {
+                if (fuse_stats) {
                     if constexpr (sizeof(T) == 2)
                         k_analyze_v3<DT, false, true><<<wgrid, 256, 0, ast>>>(raster, P, dtiles, dnorms,
                                                                               ctx->luts.as<int16_t>(),

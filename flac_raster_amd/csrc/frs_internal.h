@@ -99,11 +99,6 @@ struct frs_ctx {
     void *geo_ptrs[4] = {nullptr, nullptr, nullptr, nullptr};  // tiles, wave_tab, plist, frame_tile as uploaded
     // fast encode path split into enc_split tile ranges ($FRS_ENC_SPLIT, 1..8): range k's analysis runs on aux_stream
     // while range k - 1 is encoded on `stream` (the analysis' min/max bursts and last-round tail overlap the encoder)
-    // role-split fused analysis (k_analyze_v4): queue counters | per-SIMD role slots | per-tile stats flags, the
-    // slots and flags tagged with a per-call epoch so they are never cleared between calls; $FRS_ANA_V4=0: k_analyze_v3
-    DevBuf ana_ctl;
-    uint32_t enc_epoch = 0;
-    bool ana_v4 = false;  // (experimental: $FRS_ANA_V4=1)
     int enc_split = 1;  // (2-4 measured slower on C4: both kernels are issue-bound, so sharing the CUs gains nothing)
     hipStream_t aux_stream = nullptr;
     hipEvent_t split_ev[9] = {};

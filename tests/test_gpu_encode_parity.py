@@ -269,24 +269,3 @@ def test_split_encode_matches_oracle(split, monkeypatch):
             assert list(off) == list(o_off)
             assert arena.tobytes() == o_arena.tobytes()
             assert list(mn) == list(o_mn) and list(mx) == list(o_mx)
-
-
-@pytest.mark.parametrize("v4", ["0", "1"])
-def test_role_split_analysis_matches_oracle(v4, monkeypatch):
-    """$FRS_ANA_V4: the fused analysis as one wave per tile (k_analyze_v3, 0) or role-split (k_analyze_v4, 1: stats
-    workers publish tiles, the other waves run the sums) -- the same bytes as the oracle either way, over repeated
-    calls (epoch-tagged role slots and tile flags are never cleared between calls), with constant tiles (zero
-    normaliser) and a slow-class (fast-division) tile mixed in."""
-    from flac_raster_amd import _native
-    monkeypatch.setenv("FRS_ANA_V4", v4)
-    rng = np.random.default_rng(33)
-    band = (rng.normal(0, 25, (1536, 2560)).cumsum(axis=1) % 3000).astype(np.int16)  # 240 tiles of 128^2
-    band[:128, :256] = 77                                   # two constant tiles
-    band[128:256, 256:384] = rng.integers(-32000, 32000, (128, 128)).astype(np.int16)  # range > LUT cap
-    o_arena, o_off, o_mn, o_mx = O.encode_tiles(band, 128, threads=4)
-    with _native.Context(0) as ctx:
-        for _ in range(3):
-            arena, off, mn, mx, bps = _gpu_tiles(ctx, band, 128)
-            assert list(off) == list(o_off)
-            assert arena.tobytes() == o_arena.tobytes()
-            assert list(mn) == list(o_mn) and list(mx) == list(o_mx)
