@@ -408,20 +408,35 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_select(const uint8_t *blob
 
 // Large ranges (a whole arena): the single pass above serialises on its look-back (the inclusive prefix advances one
 // 64-block window per status round trip: ~7 ms over a 3.1 GB arena), so large ranges take two passes instead --
-// per-block counts, one work-group's scan of them, and a scatter pass that recomputes the flags (the range is read
-// twice, at streaming rate).
+// per-block counts (each block also keeps up to kSelBlkCap of its candidate positions, in order, in a per-block
+// scratch), one work-group's scan of the counts, and a placement pass that copies the kept positions to their place;
+// only a block with more candidates than its scratch holds reads its 64 KB again (the range used to be read twice in
+// full: 3.1 GB more per whole-arena decode).
+constexpr int kSelBlkCap = 32;  // candidates kept per 64 KB block (a C4 block holds ~8 frame starts)
 __global__ void __launch_bounds__(kSelThreads) k_sync_count(const uint8_t *blob, int64_t nbytes, const int64_t *soff,
-                                                          int ns, int channels, int stream_bps, int32_t *bcount) {
+                                                          int ns, int channels, int stream_bps, int32_t *bcount,
+                                                          int64_t *bpos) {
     __shared__ int s_wsum[kSelThreads / 64];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
+    const int64_t qw = (int64_t)blockIdx.x * kSelBytes + (int64_t)(kSelBytes / 4) * wv;
     uint32_t m[kSelSteps];
-    int c = sel_masks_co(blob, nbytes, soff, ns, channels, stream_bps,
-                         (int64_t)blockIdx.x * kSelBytes + (int64_t)(kSelBytes / 4) * wv, lane, m);
+    int c = sel_masks_co(blob, nbytes, soff, ns, channels, stream_bps, qw, lane, m);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
     if (lane == 0) s_wsum[wv] = c;
     __syncthreads();
-    if (t == 0) bcount[blockIdx.x] = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+    int wbase = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kSelThreads / 64; k++) {
+        wbase += k < wv ? s_wsum[k] : 0;
+        tot += s_wsum[k];
+    }
+    if (t == 0) bcount[blockIdx.x] = tot;
+    if (tot <= kSelBlkCap) {  // (block-uniform) keep the positions: the placement pass copies them
+        const int64_t slot = (int64_t)blockIdx.x * kSelBlkCap;
+        sel_emit_co(m, qw, lane, lead, slot + wbase, bpos, slot + kSelBlkCap);
+    }
 }
 
 // exclusive scan of the block counts in one work-group (bbase[n] = total -> counts[0]); zeroes the later counters
@@ -458,11 +473,20 @@ __global__ void __launch_bounds__(1024) k_sync_scan(const int32_t *bcount, int64
     }
 }
 
+// placement: a block's kept positions to cpos[bbase ...]; a block whose candidates overflowed its scratch recomputes
+// its flags (re-reads its 64 KB) and emits them directly
 __global__ void __launch_bounds__(kSelThreads) k_sync_scatter(const uint8_t *blob, int64_t nbytes, const int64_t *soff,
                                                             int ns, int channels, int stream_bps, const int64_t *bbase,
-                                                            int64_t *cpos, int64_t cap) {
+                                                            int64_t *cpos, int64_t cap, const int32_t *bcount,
+                                                            const int64_t *bpos) {
     __shared__ int s_wsum[kSelThreads / 64];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int tot = bcount[blockIdx.x];
+    if (tot <= kSelBlkCap) {  // (block-uniform)
+        const int64_t dst = bbase[blockIdx.x] + t;
+        if (t < tot && dst < cap) cpos[dst] = bpos[(int64_t)blockIdx.x * kSelBlkCap + t];
+        return;
+    }
     const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
     const int64_t qw = (int64_t)blockIdx.x * kSelBytes + (int64_t)(kSelBytes / 4) * wv;
     uint32_t m[kSelSteps];
@@ -2543,14 +2567,16 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
                 ctx->dec_epoch, nblocks, cpos, cand_cap, ncand);
     } else {
         // (its own buffer: the one-pass status words must keep their epoch tags)
-        FRS_HIP(ctx->dec_sel.ensure(sizeof(int64_t) * (size_t)(2 * nblocks + 4)));
+        // [bcount int32 | bbase int64 | bpos: kSelBlkCap positions per block]
+        FRS_HIP(ctx->dec_sel.ensure(sizeof(int64_t) * (size_t)(2 * nblocks + 4 + (int64_t)kSelBlkCap * nblocks)));
         int32_t *bcount = ctx->dec_sel.as<int32_t>();
         int64_t *bbase = ctx->dec_sel.as<int64_t>() + (nblocks + 1) / 2 + 1;
+        int64_t *bpos = bbase + nblocks + 1;
         k_sync_count<<<(unsigned)nblocks, kSelThreads, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams, channels, bps,
-                                                                bcount);
+                                                                bcount, bpos);
         k_sync_scan<<<1, 1024, 0, st>>>(bcount, bbase, nblocks, ncand);
         k_sync_scatter<<<(unsigned)nblocks, kSelThreads, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams, channels, bps,
-                                                                  bbase, cpos, cand_cap);
+                                                                  bbase, cpos, cand_cap, bcount, bpos);
     }
     prof_end(ctx, "decode", ev);
     prof_begin(ctx, "decode_span", &ev);

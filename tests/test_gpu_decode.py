@@ -263,3 +263,26 @@ def test_wrapped_lpc_prediction_decodes_exactly(gpu_ctx, kind, monkeypatch):
     got = dctx.decode_frames_host(np.frombuffer(fr, np.uint8), [0, len(fr)], [n], channels=1, bps=16, blocksize=bs)
     assert np.array_equal(got.reshape(-1), ref.reshape(-1))
     dctx.close()
+
+
+def test_large_range_dense_candidates_lossless(gpu_ctx):
+    """Ranges above 16 MB take the two-pass selection: per-64-KB-block counts that keep up to 32 candidate positions
+    per block, a scan, and a placement pass that copies them (a block with more candidates re-reads its bytes).
+    Ramps code to tiny frames (hundreds of sync candidates per block: the re-read path), noise in the other half of
+    the same job to ~8 KB frames (the kept-positions path); all tiles decode losslessly in one call."""
+    from flac_raster_amd import streaming
+    rng = np.random.default_rng(5)
+    H, W, T = 6144, 6144, 512
+    y, x = np.mgrid[0:H, 0:W]
+    band = ((7 * x + 3 * y) % 20000).astype(np.int16)  # ramps: tiny FIXED frames, hundreds of syncs per block
+    band[:, W // 2:] = rng.integers(-30000, 30000, size=(H, W // 2)).astype(np.int16)
+    d = gpu_ctx.make_desc(H, W, band.dtype, tile_h=T, tile_w=T, sample_rate=44100, bits_per_sample=16)
+    arena, off, mn, mx, bps = gpu_ctx.encode_tiles_host(band, d)
+    assert off[-1] > (16 << 20)  # the two-pass selection
+    counts = [w * h for (_, _, w, h) in streaming.tile_grid(H, W, T)]
+    vals = gpu_ctx.decode_tiles_host(arena, off, counts, channels=1, bps=16, data_min=mn, data_max=mx,
+                                     dtype=band.dtype)
+    a = 0
+    for (c0, r0, w, h), n in zip(streaming.tile_grid(H, W, T), counts):
+        assert np.array_equal(vals[a:a + n].reshape(h, w), band[r0:r0 + h, c0:c0 + w]), (r0, c0)
+        a += n
