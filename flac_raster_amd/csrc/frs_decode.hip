@@ -578,6 +578,30 @@ __device__ inline uint32_t load_word_guarded(const uint8_t *blob, int64_t k, int
     return v;
 }
 
+// words [wb, wb + nwords) of the blob (little-endian dwords, zero past `end`; byte-swapped when BSWAP) into an LDS
+// stage by NT threads (tid < NT): eight unconditional dword loads per thread in flight per round (a guarded load per
+// word compiled to a branch and a vmcnt(0) per word: one load in flight, ~10 us to stage an 8 KB frame on one wave).
+// The caller guarantees 4 wb + 4 <= end (the fallback address of a word past the end).
+template <int NT, bool BSWAP = false>
+__device__ inline void stage_words(uint32_t *stage, const uint8_t *blob, int64_t wb, int64_t nwords, int64_t end,
+                                   int tid) {
+    for (int64_t k0 = 0; k0 < nwords; k0 += 8 * NT) {
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int64_t b = 4 * (wb + k0 + NT * u + tid);
+            v[u] = *reinterpret_cast<const uint32_t *>(blob + (b + 4 <= end ? b : 4 * wb));
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int64_t k = k0 + NT * u + tid;
+            if (k < nwords) {
+                const uint32_t w = 4 * (wb + k) + 4 <= end ? v[u] : load_word_guarded(blob, wb + k, end);
+                stage[k] = BSWAP ? __builtin_bswap32(w) : w;
+            }
+        }
+    }
+}
 constexpr int kSpanWords = 6144;  // 24 KB stage
 __device__ __attribute__((aligned(16))) uint16_t d_xpow_lo[256];   // x^(8m) mod P, m < 256
 __device__ uint16_t d_xpow_hi[4096];  // x^(8*256*m) mod P
@@ -625,7 +649,7 @@ __global__ void __launch_bounds__(64) k_span_crc_wave(const uint8_t *blob, const
                 const int64_t nwords = we - wb;
                 uint32_t crc = 0;
                 if (nwords <= kSpanWords) {
-                    for (int64_t k = lane; k < nwords; k += 64) stage[k] = load_word_guarded(blob, wb + k, send);
+                    stage_words<64>(stage, blob, wb, nwords, send, lane);  // (e >= p + 7: 4 wb + 4 <= send)
                     __builtin_amdgcn_s_waitcnt(0xC07F);
                     __builtin_amdgcn_wave_barrier();
                     const uint32_t nb = (uint32_t)(e - 2 - p);  // bytes covered by the CRC
@@ -1500,8 +1524,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     const int64_t wb = fpos >> 2, we = (fend_known + 3) >> 2;
     const bool staged = we - wb <= kDecStageWords;
     if (staged)  // big-endian words: the scalar bit reader needs no byte swap
-        for (int64_t k = threadIdx.x; k < we - wb + 2 * kRiceWinQ + 4; k += 128)
-            stage[k] = __builtin_bswap32(load_word_guarded(blob, wb + k, send));
+        stage_words<128, true>(stage, blob, wb, we - wb + 2 * kRiceWinQ + 4, send, (int)threadIdx.x);
     if (threadIdx.x == 0) {
         info.state = 0;
         info.progress = 0;
