@@ -20,8 +20,8 @@ def convert(
     input_file: Path = typer.Argument(..., help="Input file (TIFF or FLAC)"),
     output_file: Optional[Path] = typer.Option(None, "--output", "-o", help="Output file path"),
     compression_level: int = typer.Option(5, "--compression", "-c", min=0, max=8,
-                                          help="FLAC compression level (0-8); the GPU encoder implements level 5 "
-                                               "(the default, and create-streaming's) and rejects the others"),
+                                          help="FLAC compression level (0-8); the GPU encoder implements 0-5 "
+                                               "(not 1/4 on two bands) and rejects the others"),
     force: bool = typer.Option(False, "--force", "-f", help="Overwrite existing output file"),
     verbose: bool = typer.Option(False, "--verbose", "-v", help="Enable verbose logging"),
     spatial_tiling: bool = typer.Option(False, "--spatial", "-s", help="Enable spatial tiling for HTTP range streaming"),

@@ -24,6 +24,20 @@ log = logging.getLogger("flac_raster.converter")
 FLOAT_DTYPES = (np.dtype(np.float32), np.dtype(np.float64))
 
 
+def check_level(level: int, channels: int) -> None:
+    """libFLAC compression levels this encoder restates (docs/sonos-pyflac.txt:6926-6931): 0..5, except the loose
+    mid/side stereo of levels 1 and 4 on two channels; 6..8 (subdivide_tukey apodizations) are not implemented.
+    The C-ABI rejects the same set (FRS_E_UNSUPPORTED); this raises before any GPU work."""
+    if not 0 <= int(level) <= 8:
+        raise ValueError(f"compression level must be 0..8, got {level}")
+    if level > 5:
+        raise NotImplementedError(f"compression level {level} (subdivide_tukey apodization) is not implemented; "
+                                  "levels 0..5 are")
+    if channels == 2 and level in (1, 4):
+        raise NotImplementedError(f"compression level {level} on two bands (loose mid/side stereo) is not "
+                                  "implemented; levels 0, 2, 3 and 5 are")
+
+
 def audio_params(shape0: int, shape1: int, dtype) -> Tuple[int, int]:
     """converter.py:25-54: (sample_rate, bits_per_sample).  total_pixels = shape[0]*shape[1] of the
     (bands, h, w) array, i.e. bands*h."""
@@ -83,8 +97,8 @@ class RasterFLACConverter:
         return audio_params(raster_data.shape[0], raster_data.shape[1], dtype)
 
     # ------------------------------------------------------------------ encode
-    def encode_array(self, data: np.ndarray) -> Tuple[bytes, float, float, int, int]:
-        """Encode a (bands, h, w) raster as one interleaved-channel FLAC stream's frames.
+    def encode_array(self, data: np.ndarray, compression_level: int = 5) -> Tuple[bytes, float, float, int, int]:
+        """Encode a (bands, h, w) raster as one interleaved-channel FLAC stream's frames at `compression_level`.
         Returns (frames, data_min, data_max, stream_bps, sample_rate)."""
         if data.ndim == 2:
             data = data[None]
@@ -92,23 +106,22 @@ class RasterFLACConverter:
         if B > 8:
             raise ValueError("FLAC supports at most 8 channels (bands)")
         sr, bps = audio_params(B, H, data.dtype)
-        d = self.ctx.make_desc(H, W, data.dtype, nbands=B, tile_h=H, tile_w=W, sample_rate=sr, bits_per_sample=bps)
+        d = self.ctx.make_desc(H, W, data.dtype, nbands=B, tile_h=H, tile_w=W, sample_rate=sr, bits_per_sample=bps,
+                               compression_level=compression_level)
         arena, off, mn, mx, sbps = self.ctx.encode_tiles_host(np.ascontiguousarray(data), d)
         return arena.tobytes(), float(mn[0]), float(mx[0]), sbps, sr
 
     def tiff_to_flac(self, tiff_path: Path, flac_path: Path, compression_level: int = 5,
                      spatial_tiling: bool = False, tile_size: int = 512):
         """converter.py:112-232."""
-        if compression_level != 5:
-            raise NotImplementedError("only compression level 5 (the reference's default and create-streaming's) "
-                                      "is implemented on the GPU encoder")
         tiff_path, flac_path = Path(tiff_path), Path(flac_path)
         if spatial_tiling:
             from .spatial_encoder import SpatialFLACEncoder
             return SpatialFLACEncoder(tile_size=tile_size, ctx=self.ctx).encode_spatial_flac(
                 tiff_path, flac_path, compression_level)
         r = geotiff.read(tiff_path)
-        frames, dmin, dmax, sbps, sr = self.encode_array(r.data)
+        check_level(compression_level, r.count)
+        frames, dmin, dmax, sbps, sr = self.encode_array(r.data, compression_level)
         meta = raster_metadata(r, dmin, dmax)
         self.write_flac(flac_path, frames, meta, r.count, sbps, sr)
         return None

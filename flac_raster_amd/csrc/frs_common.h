@@ -73,7 +73,19 @@ struct EncodeParams {
     int32_t vec_ok;       // alignment class of the row segments: 16, 8 or 4 bytes (vector loads), 0 = gather
     int32_t nvch;         // coded signals per frame: nch, or 4 for a two-channel stream (L, R, mid, side:
                           // libFLAC's exhaustive mid/side search, stream_encoder.c process_subframes_)
+    int32_t max_lpc;      // max_lpc_order of the compression level (0 = fixed predictors only)
+    int32_t max_po;       // max_residual_partition_order of the compression level
 };
+
+// libFLAC compression-level table (docs/sonos-pyflac.txt:6926-6931) for the levels this encoder restates (0..5;
+// loose mid/side -- levels 1 and 4 on two channels -- and the subdivide_tukey levels 6..8 are rejected)
+struct LevelParams {
+    int32_t mid_side, loose, max_lpc, max_po;
+};
+__host__ __device__ inline LevelParams level_params(int level) {
+    constexpr LevelParams t[6] = {{0, 0, 0, 3}, {1, 1, 0, 3}, {1, 0, 0, 3}, {0, 0, 6, 4}, {1, 1, 8, 4}, {1, 0, 8, 5}};
+    return t[level < 0 ? 0 : level > 5 ? 5 : level];
+}
 
 __host__ __device__ inline int ilog2_u32(uint32_t v) { return 31 - __builtin_clz(v); }
 __host__ __device__ inline int ilog2_u64(uint64_t v) { return 63 - __builtin_clzll(v); }

@@ -409,7 +409,7 @@ __device__ inline SubAnalysis generic_decide(const double *acc, const uint64_t *
                 if (k == guess) fg = fb[k];
             if (!(fg >= (float)sbps)) A.flags |= kFlagFixedOk;
 
-            int max_order = kMaxLpc < n ? kMaxLpc : n - 1;
+            int max_order = P.max_lpc < n ? P.max_lpc : n - 1;  // level 5: kMaxLpc
             // autocorrelation of the shifted signal = autoc * 4^-w exactly (power-of-two scaling)
             double autoc[kMaxLpc + 1];
             const double sc = ldexp(1.0, -2 * w);
@@ -989,7 +989,7 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
     const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits, P.norm_mode);
     uint32_t *slot = slots + (size_t)si * P.slot_words;
     const int rice_limit = P.bps > 16 ? 31 : 15;
-    const int max_po_block = min(kMaxPartOrder, __builtin_ctz((unsigned)n));
+    const int max_po_block = min(P.max_po, __builtin_ctz((unsigned)n));  // level 5: kMaxPartOrder
     const int chunk = (n + kEncThreads - 1) / kEncThreads;
     const int i_beg = tid * chunk, i_end = min(n, i_beg + chunk);
 
@@ -3539,7 +3539,7 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     // job geometry cache (frs_ctx::geo_*): everything the tile table, partial marking and wave table depend on
     const std::vector<int64_t> key = {d->height, d->width, d->tile_h, d->tile_w, d->tile_begin, d->tile_end,
                                       d->blocksize, d->nbands, d->dtype, d->bits_per_sample, d->norm_mode,
-                                      (allow_fast && !ctx->force_generic) ? 1 : 0};
+                                      (allow_fast && !ctx->force_generic) ? 1 : 0, d->compression_level};
     const bool geo_hit = !ctx->geo_key.empty() && ctx->geo_key == key;
     std::vector<TileGeom> tiles_local;
     std::vector<TileGeom> &tiles = geo_hit ? ctx->geo_tiles : tiles_local;
@@ -3568,7 +3568,12 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     P.ntiles = ntiles;
     P.norm_mode = d->norm_mode;
     P.vec_ok = 0;
-    P.nvch = P.nch == 2 ? 4 : P.nch;  // two channels: L, R, mid, side (level 5: exhaustive mid/side stereo)
+    const LevelParams lv = level_params(d->compression_level);
+    // two channels with mid/side (levels 2, 5): L, R, mid, side (exhaustive mid/side stereo)
+    P.nvch = (P.nch == 2 && lv.mid_side) ? 4 : P.nch;
+    P.max_lpc = lv.max_lpc;
+    P.max_po = lv.max_po;
+    const bool level5 = d->compression_level == 5;  // the fast kernels hard-code level 5's search
 
     int rc = upload_tables(ctx);
     if (rc) return rc;
@@ -3589,12 +3594,12 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     // fast path: mono 16-bit streams of 4096-sample blocks.  A tile whose pixel count is not a multiple of 4096
     // ends in a partial frame: those frames (at most one per tile) are coded by the generic kernels first and
     // the fast encoder copies them into the arena in stream order
-    const bool fast = allow_fast && !ctx->force_generic && P.bps == 16 && P.nch == 1 && P.norm_mode == 0 &&
+    const bool fast = allow_fast && !ctx->force_generic && level5 && P.bps == 16 && P.nch == 1 && P.norm_mode == 0 &&
                       d->blocksize == 4096 && !Elem<DT>::is_float;
     // multi-channel streams of >= 3 channels (plain convert of a multi-band raster): libFLAC codes their channels
     // independently, so the fast kernels code the subframes and k_mc_assemble joins them (2 channels: libFLAC's
     // stereo decorrelation, generic kernels)
-    const bool mc = allow_fast && !ctx->force_generic && P.bps == 16 && P.nch >= 3 && P.nch <= 8 &&
+    const bool mc = allow_fast && !ctx->force_generic && level5 && P.bps == 16 && P.nch >= 3 && P.nch <= 8 &&
                     P.norm_mode == 0 && d->blocksize == 4096 && !Elem<DT>::is_float;
     int64_t npartial = 0;
     int64_t *hplist = ctx->pin.at<int64_t>(pin_pl);
@@ -3948,7 +3953,7 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     FRS_HIP(ctx->slots.ensure((size_t)nframes * P.slot_words * 4));
     // 2. analysis (lane = coded signal: channel, or L/R/M/S of a two-channel stream)
     const int64_t nsub = nframes * P.nvch;
-    const bool stereo = P.nch == 2;
+    const bool stereo = P.nvch == 4 && P.nch == 2;
     const unsigned agrid = (unsigned)((nsub + 127) / 128);
     prof_begin(ctx, "analyze", &ev);
     if (P.bps > 16) {

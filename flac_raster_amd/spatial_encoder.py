@@ -21,6 +21,7 @@ import numpy as np
 
 from . import container, geotiff
 from ._native import Context, default_context
+from .converter import check_level
 
 log = logging.getLogger("flac_raster.spatial_encoder")
 
@@ -105,15 +106,14 @@ class SpatialFLACEncoder:
                             gzip_mtime: Optional[float] = None) -> SpatialIndex:
         """spatial_encoder.py:136-227 (+ _embed_metadata_in_flac :296-353).  ``date`` / ``gzip_mtime`` default
         to now, as in the reference (which is therefore not byte-reproducible run to run, App. C Q8)."""
-        if compression_level != 5:
-            raise NotImplementedError("only compression level 5 is implemented on the GPU encoder")
         r = geotiff.read(tiff_path)
+        check_level(compression_level, r.count)
         transform = r.transform or geotiff.Affine(1.0, 0.0, 0.0, 0.0, 1.0, 0.0)
         data = np.ascontiguousarray(r.data)
         B, H, W = data.shape
         tiles = self._calculate_tiles(H, W)
         d = self.ctx.make_desc(H, W, data.dtype, nbands=B, tile_h=self.tile_size, tile_w=self.tile_size,
-                               sample_rate=44100, bits_per_sample=24, norm_mode=1)
+                               sample_rate=44100, bits_per_sample=24, norm_mode=1, compression_level=compression_level)
         arena, off, mn, mx, sbps = self.ctx.encode_tiles_host(data, d)
         bare = container.bare_header(B, sbps, 44100)
         self.frames = []

@@ -366,14 +366,15 @@ typedef struct {
     uint32_t est_bits;
 } subframe_t;
 
-/* process_subframe_ of libFLAC 1.4.3 at level 5 (max_lpc_order 8, tukey(0.5), partition orders 0..5,
- * no exhaustive search, no escapes, no qlp precision search).  x is modified in place by the wasted
+/* process_subframe_ of libFLAC 1.4.3 at levels 0..5 (tukey(0.5), no exhaustive search, no escapes, no qlp
+ * precision search; max_lpc_order 8 and partition orders 0..5 at level 5, the other levels' values from the
+ * compression-level table, docs/sonos-pyflac.txt:6926-6931: max_lpc 0 = fixed predictors only).  x is modified in place by the wasted
  * bits shift (as get_wasted_bits_ does).  bps is the STREAM's bits per sample (it sets the RICE2 limit,
  * the qlp precision and the wasted-bits cap); extra = 1 for the side channel of process_subframes_'s
  * mid/side pass (subframe_bps_mid_side[1] = bps - w + 1), 0 otherwise.  Samples are int64 so the side
  * channel of a 32-bit stream (33 bits, integer_signal_33bit_side) takes the same code. */
 static void decide_subframe(int64_t *x, int n, int bps, int extra, int cfg_blocksize, const float *window,
-                            int32_t *scratch_res, float *scratch_d, subframe_t *sf) {
+                            int32_t *scratch_res, float *scratch_d, subframe_t *sf, int cfg_max_lpc, int cfg_max_po) {
     /* get_wasted_bits_ / get_wasted_bits_wide_ */
     int64_t orv = 0;
     for (int i = 0; i < n && !(orv & 1); i++) orv |= x[i];
@@ -391,9 +392,10 @@ static void decide_subframe(int64_t *x, int n, int bps, int extra, int cfg_block
     else if (bps == 16) qlp_precision = cfg_blocksize <= 192 ? 7 : cfg_blocksize <= 384 ? 8 : cfg_blocksize <= 576 ? 9 :
                                         cfg_blocksize <= 1152 ? 10 : cfg_blocksize <= 2304 ? 11 : cfg_blocksize <= 4608 ? 12 : 13;
     else qlp_precision = cfg_blocksize <= 384 ? 13 : cfg_blocksize <= 1152 ? 14 : 15;
-    /* process_subframes_: max partition order from the (possibly short final) block size, capped at 5 */
+    /* process_subframes_: max partition order from the (possibly short final) block size, capped at the level's
+     * max_residual_partition_order */
     int max_po = 0;
-    { int b = n; while (!(b & 1) && max_po < 5) { max_po++; b >>= 1; } }
+    { int b = n; while (!(b & 1) && max_po < cfg_max_po) { max_po++; b >>= 1; } }
 
     /* verbatim baseline */
     sf->type = SF_VERBATIM;
@@ -431,7 +433,7 @@ static void decide_subframe(int64_t *x, int n, int bps, int extra, int cfg_block
         }
     }
     /* lpc */
-    int max_order = ORC_MAX_LPC;
+    int max_order = cfg_max_lpc;
     if (max_order >= n) max_order = n - 1;
     if (max_order <= 0) return;
     for (int i = 0; i < n; i++) scratch_d[i] = (float)x[i] * window[i];
@@ -612,20 +614,27 @@ static void write_frame_header(bw_t *bw, int bs, int sr, int ch_assign, int bps,
 /* ------------------------------------------------------------------ public oracle API */
 
 /* Encode the FLAC frames (no stream header) of `nsamples` interleaved samples with `ch` channels,
- * exactly as libFLAC 1.4.3 level 5 does through FLAC__stream_encoder_process_interleaved + finish
+ * exactly as libFLAC 1.4.3 at `level` does through FLAC__stream_encoder_process_interleaved + finish
  * (a final short block keeps the full-length window: resize_buffers_ only grows).
  *
- * Two channels: level 5 sets do_mid_side_stereo=true, loose_mid_side_stereo=false
+ * Two channels: levels 2 and 5 set do_mid_side_stereo=true, loose_mid_side_stereo=false
  * (docs/sonos-pyflac.txt:6931), so process_subframes_ codes left, right, mid = (L+R)>>1 (bps) and
  * side = L-R (bps+1) and writes the assignment with the fewest estimated bits among independent,
  * left-side, right-side, mid-side (that order; a later one must be strictly smaller), header codes
  * 1/8/9/10 (docs/sonos-pyflac.txt:2571-2576), subframes (L,R), (L,S), (S,R), (M,S).
  * Returns bytes written, or -(bytes needed) on overflow (rough upper bound). */
-int64_t orc_encode_frames(const int32_t *interleaved, int64_t nsamples, int ch, int bps, int sample_rate,
-                          int blocksize, uint8_t *out, int64_t cap) {
+int64_t orc_encode_frames_level(const int32_t *interleaved, int64_t nsamples, int ch, int bps, int sample_rate,
+                                int blocksize, int level, uint8_t *out, int64_t cap) {
     crc_init();
     if (ch < 1 || ch > ORC_MAX_CH || blocksize < 16) return -1;
-    const int stereo = ch == 2;
+    /* compression-level table (docs/sonos-pyflac.txt:6926-6931).  Loose mid/side (levels 1 and 4 on two
+     * channels) and the subdivide_tukey apodizations of levels 6..8 are not restated: -2. */
+    static const int lvl_ms[6] = {0, 1, 1, 0, 1, 1}, lvl_loose[6] = {0, 1, 0, 0, 1, 0};
+    static const int lvl_lpc[6] = {0, 0, 0, 6, 8, 8}, lvl_po[6] = {3, 3, 3, 4, 4, 5};
+    if (level < 0 || level > 5) return -2;
+    if (ch == 2 && lvl_loose[level]) return -2;
+    const int max_lpc = lvl_lpc[level], max_po = lvl_po[level];
+    const int stereo = ch == 2 && lvl_ms[level];
     const int nv = stereo ? 4 : ch; /* coded signals: channels, or L, R, M, S */
     float *window = (float *)malloc(sizeof(float) * (size_t)blocksize);
     float *dbuf = (float *)malloc(sizeof(float) * (size_t)blocksize);
@@ -648,7 +657,8 @@ int64_t orc_encode_frames(const int32_t *interleaved, int64_t nsamples, int ch, 
         }
         for (int v = 0; v < nv; v++) {
             memset(&sf[v], 0, sizeof(sf[v]));
-            decide_subframe(xbuf + (size_t)v * blocksize, n, bps, stereo && v == 3, blocksize, window, res, dbuf, &sf[v]);
+            decide_subframe(xbuf + (size_t)v * blocksize, n, bps, stereo && v == 3, blocksize, window, res, dbuf, &sf[v],
+                            max_lpc, max_po);
         }
         int assign = ch - 1, pick[2] = {0, 1};
         if (stereo) {
@@ -677,6 +687,12 @@ int64_t orc_encode_frames(const int32_t *interleaved, int64_t nsamples, int ch, 
     free(window); free(dbuf); free(xbuf); free(res);
     if (bw.overflow) return -(bw.bits >> 3);
     return bw.bits >> 3;
+}
+
+/* level 5 (cli.py:733, converter.py:112 default) */
+int64_t orc_encode_frames(const int32_t *interleaved, int64_t nsamples, int ch, int bps, int sample_rate,
+                          int blocksize, uint8_t *out, int64_t cap) {
+    return orc_encode_frames_level(interleaved, nsamples, ch, bps, sample_rate, blocksize, 5, out, cap);
 }
 
 /* Bare libFLAC stream header: "fLaC" + STREAMINFO (min/max framesize 0, total 0, MD5 0: pyflac's
@@ -855,7 +871,8 @@ static uint32_t br_unary(br_t *b) {
 /* Decode the frames that follow a stream header; returns samples per channel decoded, or <0 on error.
  * out: interleaved int32, capacity cap_samples per channel. */
 static int64_t decode_frames_impl(const uint8_t *in, int64_t n, int ch, int bps, int32_t *out, int64_t cap_samples,
-                                  int8_t *ca_out, int64_t ca_cap) {
+                                  int8_t *ca_out, int64_t ca_cap, int16_t *sf_out, int64_t sf_cap) {
+    int64_t nsf = 0;
     crc_init();
     int64_t nfr = 0;
     br_t b = {in, n, 0, 0};
@@ -893,6 +910,7 @@ static int64_t decode_frames_impl(const uint8_t *in, int64_t n, int ch, int bps,
             int64_t *x = tmp + (size_t)c * 65536;
             br_u(&b, 1);
             int t = (int)br_u(&b, 6);
+            if (sf_out && nsf < sf_cap) sf_out[nsf] = (int16_t)t;  /* + partition order << 8 for FIXED / LPC */
             int w = 0;
             if (br_u(&b, 1)) w = (int)br_unary(&b) + 1;
             sbps -= w;
@@ -912,6 +930,7 @@ static int64_t decode_frames_impl(const uint8_t *in, int64_t n, int ch, int bps,
                     for (int i = 0; i < o; i++) q[i] = br_s(&b, prec);
                 }
                 int method = (int)br_u(&b, 2), po = (int)br_u(&b, 4);
+                if (sf_out && nsf < sf_cap) sf_out[nsf] = (int16_t)(t | (po << 8));
                 int pb = method == 0 ? 4 : 5, esc = (1 << pb) - 1;
                 int idx = o;
                 for (int p = 0; p < (1 << po); p++) {
@@ -945,6 +964,7 @@ static int64_t decode_frames_impl(const uint8_t *in, int64_t n, int ch, int bps,
                 return -6;
             }
             if (w) for (int i = 0; i < bs; i++) x[i] = (int64_t)((uint64_t)x[i] << w);
+            nsf++;
         }
         /* undo stereo decorrelation */
         if (ca >= 8) {
@@ -973,13 +993,20 @@ static int64_t decode_frames_impl(const uint8_t *in, int64_t n, int ch, int bps,
 }
 
 int64_t orc_decode_frames(const uint8_t *in, int64_t n, int ch, int bps, int32_t *out, int64_t cap_samples) {
-    return decode_frames_impl(in, n, ch, bps, out, cap_samples, NULL, 0);
+    return decode_frames_impl(in, n, ch, bps, out, cap_samples, NULL, 0, NULL, 0);
+}
+
+/* as orc_decode_frames, and every subframe's type code (| residual partition order << 8 for FIXED / LPC) into
+ * sf_out, frame-major (test diagnostics: the compression level's predictor and partition limits) */
+int64_t orc_decode_frames_sf(const uint8_t *in, int64_t n, int ch, int bps, int32_t *out, int64_t cap_samples,
+                             int16_t *sf_out, int64_t sf_cap) {
+    return decode_frames_impl(in, n, ch, bps, out, cap_samples, NULL, 0, sf_out, sf_cap);
 }
 
 /* as orc_decode_frames, and the channel assignment code of every frame into ca_out (test diagnostics) */
 int64_t orc_decode_frames_ca(const uint8_t *in, int64_t n, int ch, int bps, int32_t *out, int64_t cap_samples,
                              int8_t *ca_out, int64_t ca_cap) {
-    return decode_frames_impl(in, n, ch, bps, out, cap_samples, ca_out, ca_cap);
+    return decode_frames_impl(in, n, ch, bps, out, cap_samples, ca_out, ca_cap, NULL, 0);
 }
 
 /* ------------------------------------------------------------------ streaming tiler (cli.py:690-763) */

@@ -38,6 +38,8 @@ def lib():
         i64, i32, vp, dp = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double)
         L.orc_encode_frames.restype = i64
         L.orc_encode_frames.argtypes = [vp, i64, i32, i32, i32, i32, vp, i64]
+        L.orc_encode_frames_level.restype = i64
+        L.orc_encode_frames_level.argtypes = [vp, i64, i32, i32, i32, i32, i32, vp, i64]
         L.orc_stream_header.restype = i64
         L.orc_stream_header.argtypes = [i32, i32, i32, i32, vp, i64]
         L.orc_normalize.restype = i32
@@ -48,6 +50,8 @@ def lib():
         L.orc_decode_frames.argtypes = [vp, i64, i32, i32, vp, i64]
         L.orc_decode_frames_ca.restype = i64
         L.orc_decode_frames_ca.argtypes = [vp, i64, i32, i32, vp, i64, vp, i64]
+        L.orc_decode_frames_sf.restype = i64
+        L.orc_decode_frames_sf.argtypes = [vp, i64, i32, i32, vp, i64, vp, i64]
         L.orc_encode_tiles.restype = i64
         L.orc_encode_tiles.argtypes = [vp, i32, i64, i64, i64, i32, i32, i32, vp, i64, vp, vp, vp, i32]
         L.orc_normalize_spatial.restype = i32
@@ -101,15 +105,17 @@ def normalize_spatial(arr: np.ndarray) -> np.ndarray:
     return out
 
 
-def encode_frames(pcm: np.ndarray, bps: int, sample_rate: int, blocksize: int = 4096) -> bytes:
-    """libFLAC level-5 frames for interleaved pcm [N, C] (int32)."""
+def encode_frames(pcm: np.ndarray, bps: int, sample_rate: int, blocksize: int = 4096, level: int = 5) -> bytes:
+    """libFLAC frames at compression `level` (0..5; not 1 / 4 for two channels) for interleaved pcm [N, C]."""
     x = np.ascontiguousarray(pcm, dtype=np.int32)
     if x.ndim == 1:
         x = x[:, None]
     n, c = x.shape
     cap = n * c * (bps // 8 + 1) + (n // blocksize + 2) * (32 + 16 * c) + 1024
     out = np.empty(cap, dtype=np.uint8)
-    r = lib().orc_encode_frames(_ptr(x), n, c, bps, sample_rate, blocksize, _ptr(out), cap)
+    r = lib().orc_encode_frames_level(_ptr(x), n, c, bps, sample_rate, blocksize, level, _ptr(out), cap)
+    if r == -2:
+        raise ValueError(f"compression level {level} with {c} channels is not restated")
     if r < 0:
         raise RuntimeError(f"oracle encode overflow {r}")
     return out[:r].tobytes()
@@ -139,6 +145,22 @@ def frame_assignments(data: bytes, channels: int, bps: int, max_samples: int) ->
     if r < 0:
         raise RuntimeError(f"oracle decode error {r}")
     return ca[: -(-r // 4096) if r else 0].copy()
+
+
+def subframe_types(data: bytes, channels: int, bps: int, max_samples: int) -> np.ndarray:
+    """(type code, residual partition order) of every subframe, frame-major: type 0 CONSTANT, 1 VERBATIM,
+    8 + order FIXED, 31 + order LPC; partition order -1 for CONSTANT / VERBATIM."""
+    buf = np.frombuffer(data, dtype=np.uint8)
+    out = np.empty((max_samples, channels), dtype=np.int32)
+    cap = (max_samples // 16 + 16) * channels
+    sf = np.full(cap, -1, dtype=np.int16)
+    r = lib().orc_decode_frames_sf(_ptr(buf), len(buf), channels, bps, _ptr(out), max_samples, _ptr(sf), cap)
+    if r < 0:
+        raise RuntimeError(f"oracle decode error {r}")
+    sf = sf[: (-(-r // 4096) if r else 0) * channels]
+    t = sf & 0xFF
+    po = np.where((t >= 8), sf >> 8, -1)
+    return np.stack([t, po], axis=1)
 
 
 def denormalize_i16(pcm: np.ndarray, dmin: float, dmax: float, dtype, pcm_bps: int = 16) -> np.ndarray:

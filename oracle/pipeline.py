@@ -77,14 +77,14 @@ def _window_transform(t, col, row):
             0.0 * a + 1.0 * d, 0.0 * b + 1.0 * e, 0.0 * c + 1.0 * f + ty)
 
 
-def plain_convert(data: np.ndarray, transform, crs, nodata=None, embed=True):
-    """converter.tiff_to_flac -> (flac bytes, sidecar json text or None)."""
+def plain_convert(data: np.ndarray, transform, crs, nodata=None, embed=True, level=5):
+    """converter.tiff_to_flac (compression_level=level) -> (flac bytes, sidecar json text or None)."""
     B, H, W = data.shape
     dt = data.dtype
     flat = data.transpose(1, 2, 0).reshape(-1, B)
     pcm, mn, mx, bps = O.normalize(flat)
     sr = O.sample_rate_for(B, H)
-    bare = O.stream_header(B, bps, sr) + O.encode_frames(pcm, bps, sr)
+    bare = O.stream_header(B, bps, sr) + O.encode_frames(pcm, bps, sr, level=level)
     a, b, c, d, e, f = transform[:6]
     bounds = {"left": c, "bottom": f + e * H, "right": c + a * W, "top": f}
     md = {"width": W, "height": H, "count": B, "dtype": str(dt), "crs": crs, "transform": list(transform),
@@ -119,8 +119,8 @@ def create_streaming(band: np.ndarray, transform, crs, tile: int) -> bytes:
     return len(js).to_bytes(4, "big") + js + b"".join(chunks)
 
 
-def raw_frames(data: np.ndarray, transform, crs, tile: int, date: str, mtime: float) -> bytes:
-    """spatial_encoder.SpatialFLACEncoder.encode_spatial_flac + _embed_metadata_in_flac."""
+def raw_frames(data: np.ndarray, transform, crs, tile: int, date: str, mtime: float, level: int = 5) -> bytes:
+    """spatial_encoder.SpatialFLACEncoder.encode_spatial_flac (compression_level=level) + _embed_metadata_in_flac."""
     B, H, W = data.shape
     streams, frames = [], []
     pos = 0
@@ -130,7 +130,7 @@ def raw_frames(data: np.ndarray, transform, crs, tile: int, date: str, mtime: fl
             h, w = min(row + tile, H) - row, min(col + tile, W) - col
             sub = data[:, row:row + h, col:col + w].reshape(B, h * w).T
             pcm = O.normalize_spatial(np.ascontiguousarray(sub))
-            s = O.stream_header(B, 32, 44100) + O.encode_frames(pcm, 32, 44100)
+            s = O.stream_header(B, 32, 44100) + O.encode_frames(pcm, 32, 44100, level=level)
             xmin, ymax = _affine_mul(transform, col, row)
             xmax, ymin = _affine_mul(transform, col + w, row + h)
             frames.append({"frame_id": i, "bbox": [xmin, ymin, xmax, ymax],
