@@ -14,7 +14,8 @@ split 10/10/.../9 and `value` is the whole raster's pixels / the max-over-ranks 
 Also reported (DESIGN.md "Measurement"):
   roofline      dominant kernel's algorithmic bytes / its HIP-event-timed average duration vs 8 TB/s
   bbox_extract  C5: 1000 seed-7 bbox queries against the streaming data in HBM (selection + fused decode +
-                de-normalisation + copy to host); at N > 1 each rank answers the queries whose tile it holds
+                de-normalisation stored straight into page-locked host memory); at N > 1 each rank answers the
+                queries whose tile it holds
   (N = 1 only)  batched_decode (all 6241 tiles in one call), sentinel2 (10980^2 uint16 at tile 1024: partial
                 frames on the fast path), end_to_end (create-streaming array -> .flac file, extract-streaming
                 file -> tile), cpu_baseline (the oracle on bounded samples of the same workloads)
@@ -226,8 +227,8 @@ def parallelism(world: int, backend: str) -> str:
 def bbox_extract(ctx, comm, raster, arena, off, tmin, tmax, H, W, T, row0, counts, nq):
     """C5: `nq` bbox queries (workloads.c5_queries, seed 7) against the streaming data in HBM.  Per
     query: selection of the first intersecting tile (cli.py:976-987, grid-accelerated), fused decode +
-    de-normalisation of that tile's frames, copy of the tile to host memory.  With N ranks the index is replicated
-    and a query is answered by the rank holding its tile.  The decoded tiles are spot-checked against the raster
+    de-normalisation of that tile's frames stored straight into page-locked host memory.  With N ranks the index
+    is replicated and a query is answered by the rank holding its tile.  The decoded tiles are spot-checked against the raster
     (the C4 round trip is lossless)."""
     from flac_raster_amd import distributed, streaming
 
@@ -239,8 +240,10 @@ def bbox_extract(ctx, comm, raster, arena, off, tmin, tmax, H, W, T, row0, count
     queries = workloads.c5_queries(H, W, T, nq)
     mine = [q for q in queries
             if first_tile <= streaming.first_intersecting(index, q)["frame_id"] < first_tile + counts[rank]]
-    out = ctx.alloc(T * T * 2)
-    host = ctx.pinned(T * T * 2).view(np.int16)  # page-locked: the tile comes back at DMA rate
+    # the decode kernels store the de-normalised tile straight into page-locked host memory (frs_host_malloc):
+    # the query's result is host-resident when the call returns, with no separate D2H copy
+    out = ctx.host_buffer(T * T * 2)
+    host = out.array.view(np.int16)
     lat, checked, lossless = [], 0, True
     nwarm = min(10, len(mine))
     for k, bbox in enumerate(mine[:nwarm] + mine):  # untimed warm-up queries first
@@ -248,9 +251,7 @@ def bbox_extract(ctx, comm, raster, arena, off, tmin, tmax, H, W, T, row0, count
         f = streaming.first_intersecting(index, bbox)
         i = f["frame_id"] - first_tile
         n = f["window"]["width"] * f["window"]["height"]
-        ctx.decode_tiles_device(arena, np.array([off[i], off[i + 1]], dtype=np.int64), [n], channels=1, bps=16,
-                                data_min=[float(tmin[i])], data_max=[float(tmax[i])], dtype=np.int16, out=out)
-        out.download(n * 2, 0, out=host[:n].view(np.uint8))
+        ctx.decode_tile_device(arena, off[i], off[i + 1], n, 1, 16, tmin[i], tmax[i], np.int16, out)
         dt = time.perf_counter() - t0
         if k >= nwarm:
             lat.append(dt)
@@ -270,8 +271,7 @@ def bbox_extract(ctx, comm, raster, arena, off, tmin, tmax, H, W, T, row0, count
         f = streaming.first_intersecting(index, bbox)
         i = f["frame_id"] - first_tile
         n = f["window"]["width"] * f["window"]["height"]
-        ctx.decode_tiles_device(arena, np.array([off[i], off[i + 1]], dtype=np.int64), [n], channels=1, bps=16,
-                                data_min=[float(tmin[i])], data_max=[float(tmax[i])], dtype=np.int16, out=out)
+        ctx.decode_tile_device(arena, off[i], off[i + 1], n, 1, 16, tmin[i], tmax[i], np.int16, out)
     ctx.sync()
     ctx.profile(False)
     kern = {k: round(ctx.profile_avg_ms(k), 4) for k in ("decode", "decode_span", "decode_frames")}
@@ -288,8 +288,8 @@ def bbox_extract(ctx, comm, raster, arena, off, tmin, tmax, H, W, T, row0, count
     ms = ns / 1e6
     return {"p50_ms": round(float(np.percentile(ms, 50)), 3), "p90_ms": round(float(np.percentile(ms, 90)), 3),
             "queries": int(len(ms)), "n_gpus": comm.world if comm is not None else 1,
-            "path": "device-resident streaming data: select + fused decode/denormalise + D2H (query -> rank holding "
-                    "the tile)", "kernels_ms_rank0": kern, "lossless_spot_checks": checked, "lossless": lossless}
+            "path": "device-resident streaming data: select + fused decode/denormalise stored straight into "
+                    "page-locked host memory (query -> rank holding the tile)", "kernels_ms_rank0": kern, "lossless_spot_checks": checked, "lossless": lossless}
 
 
 def batched_decode(ctx, arena, off, tmin, tmax, rows, W, T):

@@ -194,6 +194,31 @@ class DeviceBuffer:
             pass
 
 
+class HostBuffer:
+    """Page-locked host memory (frs_host_malloc) the device can address: a decode target the kernels store straight
+    into (no device buffer, no D2H copy).  `array` is its uint8 view; freed with close()."""
+
+    def __init__(self, ctx: "Context", nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        self.ptr = ctx.lib.frs_host_malloc(ctx.handle, self.nbytes)
+        if not self.ptr:
+            raise FrsError(-2, ctx.last_error())  # FRS_E_HIP
+        self.array = np.frombuffer((ctypes.c_uint8 * self.nbytes).from_address(self.ptr), dtype=np.uint8)
+
+    def close(self):
+        if self.ptr:
+            self.array = None
+            self.ctx.lib.frs_host_free(self.ctx.handle, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Context:
     """One frs_ctx (one device, one HIP stream).  Not shared between threads."""
 
@@ -238,6 +263,9 @@ class Context:
     # ---- memory
     def alloc(self, nbytes: int) -> DeviceBuffer:
         return DeviceBuffer(self, nbytes)
+
+    def host_buffer(self, nbytes: int) -> HostBuffer:
+        return HostBuffer(self, nbytes)
 
     def sync(self):
         self._check(self.lib.frs_ctx_sync(self.handle))
@@ -363,9 +391,10 @@ class Context:
         return out
 
     def decode_tiles_device(self, blob: DeviceBuffer, stream_off: np.ndarray, pcm_counts: Sequence[int], channels: int,
-                            bps: int, data_min: Sequence[float], data_max: Sequence[float], dtype, out: DeviceBuffer,
+                            bps: int, data_min: Sequence[float], data_max: Sequence[float], dtype, out,
                             blocksize: int = 4096, blob_ptr: Optional[int] = None) -> np.ndarray:
-        """Device-resident fused decode into `out`; returns the sample offsets (pcm_off)."""
+        """Device-resident fused decode into `out` (a DeviceBuffer, or a HostBuffer the kernels store straight into);
+        returns the sample offsets (pcm_off)."""
         soff = np.ascontiguousarray(np.asarray(stream_off, dtype=np.int64))
         poff = np.zeros(len(pcm_counts) + 1, dtype=np.int64)
         poff[1:] = np.cumsum(np.asarray(pcm_counts, dtype=np.int64))
@@ -380,6 +409,24 @@ class Context:
             poff.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), mn.ctypes.data_as(dp), mx.ctypes.data_as(dp),
             DTYPE_CODES[np.dtype(dtype)], ctypes.c_void_p(out.ptr)))
         return poff
+
+    def decode_tile_device(self, blob, start: int, end: int, count: int, channels: int, bps: int, data_min: float,
+                           data_max: float, dtype, out, blocksize: int = 4096) -> None:
+        """decode_tiles_device for ONE stream (blob bytes [start, end), `count` samples per channel) -- the latency
+        path of a bbox query: argument tables are this context's reused ctypes arrays (no numpy per call)."""
+        dt = np.dtype(dtype)
+        if count * channels * dt.itemsize > out.nbytes:
+            raise ValueError("output buffer too small")
+        tabs = getattr(self, "_one_tabs", None)
+        if tabs is None:
+            tabs = self._one_tabs = ((ctypes.c_int64 * 2)(), (ctypes.c_int64 * 2)(), (ctypes.c_double * 1)(),
+                                     (ctypes.c_double * 1)())
+        soff, poff, mn, mx = tabs
+        soff[0], soff[1] = int(start), int(end)
+        poff[1] = int(count)
+        mn[0], mx[0] = float(data_min), float(data_max)
+        self._check(self.lib.frs_decode_tiles_device(self.handle, ctypes.c_void_p(blob.ptr), soff, 1, channels, bps,
+                                                     blocksize, poff, mn, mx, DTYPE_CODES[dt], ctypes.c_void_p(out.ptr)))
 
     def denormalize_host(self, pcm: np.ndarray, data_min: float, data_max: float, dtype, pcm_bps: int = 16) -> np.ndarray:
         p = np.ascontiguousarray(pcm, dtype=np.int32)

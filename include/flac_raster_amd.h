@@ -136,7 +136,9 @@ int frs_decode_frames(frs_ctx *ctx, const uint8_t *blob_host, const int64_t *str
  * `nstreams` tiles at once.  Same stream layout as frs_decode_frames; stream s carries its own
  * GEOSPATIAL_DATA_MIN/MAX (data_min[s], data_max[s], converter.py:375-427) and its samples are written
  * interleaved as out_dtype at out + (pcm_off[s] + i) * channels + c -- the int32 PCM never reaches memory for
- * mono 16-bit streams (create-streaming tiles).  Errors as frs_decode_frames. */
+ * mono 16-bit streams (create-streaming tiles).  out_dev is device memory, or page-locked host memory from
+ * frs_host_malloc: the kernels then store the result straight into host memory (no separate D2H copy; a C5 query
+ * returns one tile this way).  Errors as frs_decode_frames. */
 int frs_decode_tiles_device(frs_ctx *ctx, const uint8_t *blob_dev, const int64_t *stream_off, int32_t nstreams,
                             int32_t channels, int32_t bps, int32_t blocksize, const int64_t *pcm_off,
                             const double *data_min, const double *data_max, int32_t out_dtype, void *out_dev);

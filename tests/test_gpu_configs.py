@@ -162,6 +162,45 @@ def test_c5_bbox_queries_match_linear_scan_and_oracle(gpu_ctx, c4):
     out.close()
 
 
+def test_c5_host_resident_output(gpu_ctx, c4):
+    """bench.py's C5 path: the fused decode stores each tile straight into page-locked host memory (frs_host_malloc,
+    no D2H copy); results equal the raster windows, and a 3-channel stream (planar scratch + k_interleave_dn into
+    host memory) equals the oracle."""
+    from flac_raster_amd import streaming
+    H, W, off = c4["H"], c4["W"], c4["off"]
+    index = workloads.streaming_index(H, W, T, np.diff(off))
+    hb = gpu_ctx.host_buffer(T * T * 2)
+    host = hb.array.view(np.int16)
+    for q, bbox in enumerate(workloads.c5_queries(H, W, T, 200)):
+        f = streaming.first_intersecting(index, bbox)
+        i = f["frame_id"]
+        wnd = f["window"]
+        n = wnd["width"] * wnd["height"]
+        host[:n] = -1
+        gpu_ctx.decode_tile_device(c4["arena"], off[i], off[i + 1], n, 1, 16, c4["mn"][i], c4["mx"][i], np.int16, hb)
+        r0, c0 = wnd["row_off"], wnd["col_off"]
+        got = host[:n].reshape(wnd["height"], wnd["width"])
+        assert np.array_equal(got, c4["band"][r0:r0 + wnd["height"], c0:c0 + wnd["width"]]), q
+    hb.close()
+    rng = np.random.default_rng(3)
+    data = (1000 + 300 * np.sin(np.arange(3 * 300 * 400) / 50.0).reshape(3, 300, 400)
+            + rng.integers(0, 40, (3, 300, 400))).astype(np.int16)
+    d = gpu_ctx.make_desc(300, 400, np.int16, nbands=3, tile_h=300, tile_w=400, sample_rate=O.sample_rate_for(3, 300),
+                          bits_per_sample=16)
+    arena, toff, mn, mx, bps = gpu_ctx.encode_tiles_host(data, d)
+    arena = np.ascontiguousarray(arena[:toff[-1]])
+    blob = gpu_ctx.alloc(len(arena))
+    blob.upload(arena)
+    hb = gpu_ctx.host_buffer(data.nbytes)
+    gpu_ctx.decode_tiles_device(blob, np.array([0, len(arena)], dtype=np.int64), [300 * 400], channels=3, bps=16,
+                                data_min=[mn[0]], data_max=[mx[0]], dtype=np.int16, out=hb)
+    pcm = O.decode_frames(arena.tobytes(), 3, 16, 300 * 400)
+    ref = O.denormalize_i16(pcm, mn[0], mx[0], np.int16)
+    assert np.array_equal(hb.array.view(np.int16).reshape(-1), ref.reshape(-1))
+    hb.close()
+    blob.close()
+
+
 # ------------------------------------------------------------------------- partial frames on the fast path
 @pytest.mark.parametrize("shape,tile,dtype", [
     ((10980, 10980), 1024, np.uint16),  # the reference's Sentinel-2 B04 example (FLAC-SPATIAL.md:82-88): last tile 740^2

@@ -28,7 +28,26 @@ def main():
     out = ctx.alloc(T * T * 2)
     host = ctx.pinned(T * T * 2).view(np.int16)
     ts, td, tc = [], [], []
-    prof = len(sys.argv) > 2 and sys.argv[2] == "prof"  # kernel times (the profile's events add ~10 us per kernel)
+    mode = sys.argv[2] if len(sys.argv) > 2 else ""
+    prof = mode == "prof"  # kernel times (the profile's events add ~10 us per kernel)
+    hostout = mode.startswith("hostout")
+    one = mode == "hostout1"  # + the single-stream call (decode_tile_device: reused ctypes tables)  # the decode kernels store straight into the page-locked host buffer (no D2H copy)
+
+    class _HostOut:
+        ptr, nbytes = int(host.ctypes.data), host.nbytes
+    if hostout:
+        ref = ctx.alloc(T * T * 2)
+        for bbox in qs[:20]:  # the host-resident result equals the device-resident one
+            f = streaming.first_intersecting(index, bbox)
+            i = f["frame_id"]
+            n = f["window"]["width"] * f["window"]["height"]
+            args = (arena, np.array([off[i], off[i + 1]], dtype=np.int64), [n])
+            kw = dict(channels=1, bps=16, data_min=[float(mn[i])], data_max=[float(mx[i])], dtype=np.int16)
+            ctx.decode_tiles_device(*args, out=ref, **kw)
+            a = ref.download(n * 2).view(np.int16)
+            ctx.decode_tiles_device(*args, out=_HostOut, **kw)
+            assert np.array_equal(a, host[:n]), "host-resident decode differs"
+        out = _HostOut
     ctx.profile(prof)
     ctx.profile_reset()
     for k, bbox in enumerate(qs[:10] + qs):
@@ -37,10 +56,14 @@ def main():
         i = f["frame_id"]
         n = f["window"]["width"] * f["window"]["height"]
         t1 = time.perf_counter()
-        ctx.decode_tiles_device(arena, np.array([off[i], off[i + 1]], dtype=np.int64), [n], channels=1, bps=16,
-                                data_min=[float(mn[i])], data_max=[float(mx[i])], dtype=np.int16, out=out)
+        if one:
+            ctx.decode_tile_device(arena, off[i], off[i + 1], n, 1, 16, mn[i], mx[i], np.int16, out)
+        else:
+            ctx.decode_tiles_device(arena, np.array([off[i], off[i + 1]], dtype=np.int64), [n], channels=1, bps=16,
+                                    data_min=[float(mn[i])], data_max=[float(mx[i])], dtype=np.int16, out=out)
         t2 = time.perf_counter()
-        out.download(n * 2, 0, out=host[:n].view(np.uint8))
+        if not hostout:
+            out.download(n * 2, 0, out=host[:n].view(np.uint8))
         t3 = time.perf_counter()
         if k >= 10:
             ts.append(t1 - t0)
