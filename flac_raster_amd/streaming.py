@@ -418,7 +418,8 @@ class TileDecoder:
                 so = np.zeros(len(sb) + 1, dtype=np.int64)
                 so[1:] = np.cumsum([len(b) for b in sb])
                 cnt = [counts[j] for j in js]
-                allv = self.ctx.decode_tiles_host(np.concatenate(sb), so, cnt, channels=ch, bps=bps,
+                blob = sb[0] if len(sb) == 1 else np.concatenate(sb)  # one tile (extract): no host copy
+                allv = self.ctx.decode_tiles_host(blob, so, cnt, channels=ch, bps=bps,
                                                   data_min=[mds[i]["data_min"] for i in sel],
                                                   data_max=[mds[i]["data_max"] for i in sel], dtype=np.dtype(dts),
                                                   blocksize=bs)
