@@ -120,11 +120,15 @@ def main():
     arena = ctx.alloc(ctx.arena_bound(desc))
     ctx.sync()
 
+    ag_s = []  # per-step wall time of the size all-gather (N > 1)
+
     def step():
         off, mn, mx, _ = ctx.encode_tiles_device(raster.ptr, desc, arena) if rows else \
             (np.zeros(1, np.int64), np.zeros(0), np.zeros(0), 16)
         if comm is not None:  # spatial-index exchange: every rank's per-tile sizes -> global byte offsets (RCCL)
+            t = time.perf_counter()
             distributed.all_gather_sizes(np.diff(off), counts, comm)
+            ag_s.append(time.perf_counter() - t)
         return off, mn, mx
 
     for _ in range(args.warmup):
@@ -139,6 +143,7 @@ def main():
     ctx.profile(True)
     ctx.profile_reset()
     barrier()
+    ag_s.clear()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         off, mn, mx = step()
@@ -190,6 +195,11 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic_for(args.traffic_json, dom, px_rank)},
     }
+    if comm is not None:
+        result["allgather_us"] = allgather_figures(comm, ag_s, np.diff(off), counts)
+        result["config"]["compressed_bytes_total"] = int(comm.allgather_i64(np.array([comp_bytes])).sum())
+    else:
+        result["config"]["compressed_bytes_total"] = comp_bytes
     valu = pmc_for(args.traffic_json, dom, px_rank, "valu_insts")
     if valu:  # the integer encoder is issue-bound, not HBM-bound: its VALU instruction rate vs the issue peak
         rate = valu / (dom_ms * 1e-3) / 1e9
@@ -215,6 +225,29 @@ def main():
     if comm is not None:
         comm.close()
     ctx.close()
+
+
+def allgather_figures(comm, ag_s, sizes, counts, reps=20):
+    """The spatial-index exchange of the N > 1 step, reported apart from the encode.  in_step: the
+    all-gather's wall time inside the timed steps, which includes waiting for the slowest rank's encode (skew);
+    isolated: the same all-gather of the same sizes after a barrier, i.e. the exchange itself.  mean = the mean
+    over steps, max = the slowest step, each then the max over ranks."""
+    from flac_raster_amd import distributed
+    iso = []
+    for _ in range(reps):
+        comm.barrier()
+        t = time.perf_counter()
+        distributed.all_gather_sizes(sizes, counts, comm)
+        iso.append(time.perf_counter() - t)
+
+    def stat(v):
+        v = np.asarray(v if len(v) else [0.0]) * 1e6
+        g = comm.allgather_i64(np.array([int(v.mean() * 1000), int(v.max() * 1000), int(np.median(v) * 1000)]))
+        g = g.reshape(-1, 3) / 1000.0
+        return {"mean": round(float(g[:, 0].max()), 1), "max": round(float(g[:, 1].max()), 1),
+                "p50": round(float(g[:, 2].max()), 1)}
+    return {"in_step": stat(ag_s), "isolated": stat(iso), "steps": len(ag_s), "isolated_reps": reps,
+            "bytes_per_rank": int(8 * max(counts)), "backend": type(comm).__name__}
 
 
 def parallelism(world: int, backend: str) -> str:

@@ -9,6 +9,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
+import weakref
 from pathlib import Path
 from typing import Optional, Sequence, Tuple
 
@@ -232,7 +233,7 @@ class Context:
             raise NativeUnavailable(f"frs_ctx_create({device}) failed: {STATUS.get(rc, rc)}")
         self.handle = h
         self.device = device
-        self._pin_ptr, self._pin_bytes = None, 0
+        self._pin, self._pin_view = None, None  # reusable page-locked buffer, weakref to its last exported view
 
     def close(self):
         if getattr(self, "handle", None):
@@ -271,23 +272,26 @@ class Context:
         self._check(self.lib.frs_ctx_sync(self.handle))
 
     def pinned(self, nbytes: int) -> np.ndarray:
-        """uint8[nbytes] view of this context's page-locked host buffer (frs_host_malloc), grown on demand and reused
-        by the next call: the arena of a large host encode lands in it at DMA rate.  Valid until the next call or
-        release_pinned()."""
-        if nbytes > self._pin_bytes:
-            self.release_pinned()
-            size = max(int(nbytes), 2 * self._pin_bytes if self._pin_bytes else 0)
-            p = self.lib.frs_host_malloc(self.handle, size)
-            if not p:
-                raise FrsError(-2, self.last_error())  # FRS_E_HIP
-            self._pin_ptr, self._pin_bytes = p, size
-        buf = (ctypes.c_uint8 * self._pin_bytes).from_address(self._pin_ptr)
-        return np.frombuffer(buf, dtype=np.uint8, count=int(nbytes))
+        """uint8[nbytes] view of a page-locked host buffer (frs_host_malloc): the arena of a large host encode lands in
+        it at DMA rate.  The returned array owns the buffer (it is freed when the last view of it dies), so a view
+        handed out earlier is never invalidated.  The context keeps one buffer for reuse and hands it out again only
+        while no earlier view of it is alive; a request it cannot serve gets a buffer of exactly its size."""
+        nbytes = int(nbytes)
+        hb = self._pin
+        if hb is not None and (hb.nbytes < nbytes or (self._pin_view is not None and self._pin_view() is not None)):
+            # too small, or still in use by an earlier result: the context lets go of it (live views keep it)
+            self._pin, self._pin_view, hb = None, None, None
+        if hb is None:
+            hb = HostBuffer(self, nbytes)
+            self._pin = hb
+        view = (ctypes.c_uint8 * hb.nbytes).from_address(hb.ptr)
+        view._owner = hb  # the array's base holds the buffer alive
+        self._pin_view = weakref.ref(view)
+        return np.frombuffer(view, dtype=np.uint8, count=nbytes)
 
     def release_pinned(self):
-        if self._pin_ptr:
-            self.lib.frs_host_free(self.handle, self._pin_ptr)
-            self._pin_ptr, self._pin_bytes = None, 0
+        """Drop the context's reusable page-locked buffer (views still alive keep theirs until they die)."""
+        self._pin, self._pin_view = None, None
 
     # ---- encode
     @staticmethod

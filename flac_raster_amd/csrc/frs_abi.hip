@@ -245,14 +245,29 @@ static int encode_tiles_batched(frs_ctx *ctx, const frs_encode_desc *desc, const
     }
     const int nt = host_threads();
     hipEvent_t up[2] = {nullptr, nullptr}, down = nullptr;
-    for (auto &e : up) FRS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    FRS_HIP(hipEventCreateWithFlags(&down, hipEventDisableTiming));
+    // every exit below goes through the tail that drains the copy streams and destroys the events: a pending D2H
+    // must not land in arena_host after the caller saw the error and freed it
+    auto tail = [&](int rc_) -> int {
+        if (ctx->h2d_stream) hipStreamSynchronize(ctx->h2d_stream);
+        if (ctx->d2h_stream) hipStreamSynchronize(ctx->d2h_stream);
+        for (auto &e : up)
+            if (e) hipEventDestroy(e);
+        if (down) hipEventDestroy(down);
+        return rc_;
+    };
+    for (auto &e : up)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return tail(FRS_E_HIP);
+    if (hipEventCreateWithFlags(&down, hipEventDisableTiming) != hipSuccess) return tail(FRS_E_HIP);
+    const int rc = [&]() -> int {
     bool used[2] = {false, false};
     int rc = FRS_OK;
+    // the raster's last row ends `width` elements after its start (a strided descriptor need not hold the stride's
+    // padding after it): a batch that reaches the last row copies only that much of it
+    const int64_t last_row_short = (desc->row_stride - desc->width) * (int64_t)es;
     auto stage = [&](size_t b) -> int {  // host copy into ring slot b % 2, then its DMA
         const int k = (int)(b & 1);
         if (used[k]) FRS_HIP(hipEventSynchronize(up[k]));  // the slot's previous DMA has drained
-        const size_t n = (size_t)((B[b].r1 - B[b].r0) * row_bytes);
+        const size_t n = (size_t)((B[b].r1 - B[b].r0) * row_bytes - (B[b].r1 == desc->height ? last_row_short : 0));
         par_memcpy(ctx->ring[k].ptr, band + (size_t)B[b].r0 * row_bytes, n, nt);
         FRS_HIP(hipMemcpyAsync(ctx->raster_stage.as<uint8_t>() + (size_t)(B[b].r0 - r_lo) * row_bytes, ctx->ring[k].ptr,
                                n, hipMemcpyHostToDevice, ctx->h2d_stream));
@@ -291,11 +306,9 @@ static int encode_tiles_batched(frs_ctx *ctx, const frs_encode_desc *desc, const
                                hipMemcpyDeviceToHost, ctx->d2h_stream));
         aoff += nbytes;
     }
-    hipStreamSynchronize(ctx->h2d_stream);
-    hipStreamSynchronize(ctx->d2h_stream);
-    for (auto &e : up) hipEventDestroy(e);
-    hipEventDestroy(down);
     return rc;
+    }();
+    return tail(rc);
 }
 
 extern "C" {
@@ -540,10 +553,12 @@ void *frs_host_malloc(frs_ctx *ctx, int64_t bytes) {
 }
 
 void frs_host_free(frs_ctx *ctx, void *ptr) {
-    if (!ctx || !ptr) return;
-    hipSetDevice(ctx->device);
-    hipDeviceSynchronize();  // (copies on the context's side streams may still read or write it)
-    hipHostFree(ptr);
+    if (!ptr) return;
+    if (ctx) {
+        hipSetDevice(ctx->device);
+        hipDeviceSynchronize();  // (copies on the context's side streams may still read or write it)
+    }
+    hipHostFree(ptr);  // (ctx may be null: a buffer that outlived its context; its streams are gone)
 }
 
 int frs_memcpy_h2d(frs_ctx *ctx, void *dst_dev, const void *src_host, int64_t bytes) {

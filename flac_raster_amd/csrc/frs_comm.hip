@@ -21,6 +21,7 @@ struct frs_comm {
     int rank = 0, nranks = 1;
     frs_ctx *ctx = nullptr;
     DevBuf buf;  // send | recv staging of the all-gathers
+    bool aborted = false;  // a collective failed or timed out and the communicator was aborted
 };
 
 namespace {
@@ -31,7 +32,7 @@ struct RcclApi {
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
     ncclResult_t (*all_gather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
     const char *(*error_string)(ncclResult_t) = nullptr;
-    ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;                      // optional
+    ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;  // required: the bounded wait of an all-gather needs it
     ncclResult_t (*get_async_error)(ncclComm_t, ncclResult_t *) = nullptr;  // optional
     std::string err;
 };
@@ -54,8 +55,9 @@ bool load_rccl() {
         g_api.error_string = (decltype(g_api.error_string))dlsym(g_api.h, "ncclGetErrorString");
         g_api.comm_abort = (decltype(g_api.comm_abort))dlsym(g_api.h, "ncclCommAbort");
         g_api.get_async_error = (decltype(g_api.get_async_error))dlsym(g_api.h, "ncclCommGetAsyncError");
-        if (!g_api.get_unique_id || !g_api.comm_init_rank || !g_api.comm_destroy || !g_api.all_gather)
-            g_api.err = "librccl.so lacks the nccl* entry points";
+        if (!g_api.get_unique_id || !g_api.comm_init_rank || !g_api.comm_destroy || !g_api.all_gather ||
+            !g_api.comm_abort)
+            g_api.err = "librccl.so lacks the nccl* entry points (incl. ncclCommAbort, which bounds a hung collective)";
     });
     return g_api.h && g_api.err.empty();
 }
@@ -102,7 +104,7 @@ int frs_comm_init(frs_ctx *ctx, const uint8_t *id, int32_t nranks, int32_t rank,
 
 void frs_comm_destroy(frs_comm *c) {
     if (!c) return;
-    if (c->ctx) {
+    if (c->ctx && !c->aborted) {  // (after an abort the stream may hold work that never drains: no sync)
         hipSetDevice(c->ctx->device);
         hipStreamSynchronize(c->ctx->stream);
     }
@@ -114,6 +116,10 @@ void frs_comm_destroy(frs_comm *c) {
 int frs_comm_allgather_i64(frs_comm *c, const int64_t *send_host, int64_t count, int64_t *recv_host) {
     if (!c || count < 0 || (count && (!send_host || !recv_host))) return FRS_E_ARG;
     frs_ctx *ctx = c->ctx;
+    if (c->aborted || !c->comm) {
+        ctx->err = "communicator was aborted after a failed all-gather";
+        return FRS_E_HIP;
+    }
     if (count == 0) return FRS_OK;
     FRS_HIP(hipSetDevice(ctx->device));
     const size_t sb = sizeof(int64_t) * (size_t)count;
@@ -159,9 +165,10 @@ int frs_comm_allgather_i64(frs_comm *c, const int64_t *send_host, int64_t count,
         std::this_thread::sleep_for(std::chrono::microseconds(spin < 1000 ? 5 : 200));
     }
     hipEventDestroy(done);
-    if (rc != FRS_OK && g_api.comm_abort && c->comm) {
+    if (rc != FRS_OK && c->comm) {
         g_api.comm_abort(c->comm);  // frees the pending collective; the communicator is unusable afterwards
         c->comm = nullptr;
+        c->aborted = true;
     }
     return rc;
 }

@@ -211,7 +211,13 @@ class TiffFile:
 
     def close(self):
         if self._mm:
-            self._mm.close()
+            try:
+                self._mm.close()
+            except BufferError:
+                # numpy views of the map are still alive (e.g. held by an exception's traceback): leave the map to
+                # the garbage collector rather than masking the caller's error with this one
+                pass
+            self._mm = None
         self._f.close()
 
     def __enter__(self):

@@ -135,8 +135,8 @@ class EncodedTiles:
 def encode_band_tiles(band: np.ndarray, tile_size: int, ctx: Optional[Context] = None,
                       pinned: bool = False) -> EncodedTiles:
     """All band-1 tiles in one GPU launch sequence (the reference's tile loop, cli.py:690-763).  pinned=True: the
-    frames land in the context's page-locked buffer (reused by its next pinned call; create-streaming writes them
-    out at once)."""
+    frames land in page-locked memory owned by the returned arena array (Context.pinned: the DMA writes at full
+    rate, and the buffer lives as long as any view of it)."""
     H, W = band.shape
     if H == 0 or W == 0:  # an empty shard (more ranks than tile rows): no tiles, nothing to launch
         z = np.zeros(0, dtype=np.float64)
