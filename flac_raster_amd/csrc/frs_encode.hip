@@ -2120,6 +2120,139 @@ __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *
     out[f * P.nch + chn] = analysis_finish(acc, or_acc, n, P, ft);
 }
 
+// ------------------------------------------------------------------------------ k_analyze_v5
+// Role-split analysis inside one work-group (16-bit mono streams, one wave per tile, 16-B aligned rows): the same
+// per-tile work as k_analyze_v3<DT, false, true>, but the HBM-bound min/max pass leaves the slots of the fp64-bound
+// autocorrelation.  In v3 every wave read its tile for min/max before its sums (C4: 437 us of stats against 402 us of
+// sums per wave, ~2000 of the 4096 slots in a stats pass at any moment, a 330 us start-up burst with the VALU idle).
+// A work-group here is 8 waves: waves 4..7 ("producers") claim tiles from a global counter, compute each tile's
+// min/max and normalisation, write its parameters and LUT to HBM for the encoder and its LUT into an LDS slot, and
+// post the slot; waves 0..3 ("consumers") take the posted slots in order and run ana_autoc on them.  Every wait is
+// on LDS state of the same work-group, so no wave ever waits on another work-group (no cross-WG progress assumption,
+// no epochs).  Ring protocol (kV5Slots slots, item i in slot i % kV5Slots, items numbered by two LDS counters):
+//   producer of item i: waits until slot.seq == i - kV5Slots has been consumed (done == i - kV5Slots + 1 ... i.e. the
+//   slot's `free` tag equals i), fills it, then publishes seq = i (release);
+//   consumer of item i: waits for seq == i (acquire), works, then sets free = i + kV5Slots (release).
+// A producer whose global claim is past the last tile posts an end marker (tile -1) and exits: four producers post
+// exactly four markers, one for each consumer.  A slow-class tile (fast / exact division) is not posted (its
+// parameters go to HBM; k_analyze_v3<DT, true> analyses it) and the producer claims another tile for the same item.
+constexpr int kV5Slots = 8;
+struct V5Slot {
+    TileNorm tn;
+    int tile;  // -1: end marker
+    int seq;   // item number posted in this slot (-1: none yet)
+    int free;  // item number the slot may take next
+    int pad;
+};
+template <int DT>
+__global__ void __launch_bounds__(512, 2) k_analyze_v5(const typename Elem<DT>::T *raster, EncodeParams P,
+                                                      const TileGeom *tiles, TileNorm *norms, int16_t *luts,
+                                                      const float *__restrict__ window, SubAnalysis *out, int ntiles,
+                                                      int *tile_ctr, int *err) {
+    static_assert(sizeof(typename Elem<DT>::T) == 2 && !Elem<DT>::is_float, "16-bit samples");
+    __shared__ int16_t slut[kV5Slots][kLutCap];
+    __shared__ V5Slot slot[kV5Slots];
+    __shared__ int ctr[2];  // items taken by producers / by consumers
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (threadIdx.x < kV5Slots) {
+        slot[threadIdx.x].seq = -1;
+        slot[threadIdx.x].free = threadIdx.x;
+    }
+    if (threadIdx.x < 2) ctr[threadIdx.x] = 0;
+    __syncthreads();
+    auto lds_wait = [&](const int *addr, int want) {  // spin on an LDS word of this work-group until it equals want
+        for (long spin = 0;; spin++) {
+            int v = 0;
+            if (lane == 0) v = __hip_atomic_load(addr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (__builtin_amdgcn_readfirstlane(v) == want) return true;
+            if (spin > (1l << 26)) {  // (never: every posted item is consumed, every slot is freed in order)
+                if (lane == 0) atomicOr(err, 64);
+                return false;
+            }
+            if (spin < 64) __builtin_amdgcn_s_sleep(1);
+            else __builtin_amdgcn_s_sleep(8);
+        }
+    };
+    auto take = [&](int k) {
+        int i = 0;
+        if (lane == 0) i = atomicAdd(&ctr[k], 1);
+        return __builtin_amdgcn_readfirstlane(i);
+    };
+    if (wave >= 4) {
+        // ---- producer
+        while (true) {
+            const int i = take(0);
+            V5Slot &sl = slot[i % kV5Slots];
+            int t;
+            TileNorm tn;
+            while (true) {  // the next tile the consumers analyse here (slow-class tiles only get their parameters)
+                int tq = 0;
+                if (lane == 0) tq = atomicAdd(tile_ctr, 1);
+                t = __builtin_amdgcn_readfirstlane(tq);
+                if (t >= ntiles) break;
+                const TileGeom g = tiles[t];
+                const typename Elem<DT>::T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
+                wave_tile_minmax<DT>(base, P.row_stride, g, lane, tn.imin, tn.imax);
+                tile_norm_finalize<DT>(tn, P.norm_mode, P.scale_bits);
+                if (lane == 0) norms[t] = tn;
+                const int nfull = g.nframes - (g.partial ? 1 : 0);
+                if ((tn.mode == kNormLut || tn.mode == kNormZero) && nfull > 0) break;
+            }
+            if (!lds_wait(&sl.free, i)) return;  // the slot's previous item has been consumed
+            if (t < ntiles && tn.mode == kNormLut) {
+                int16_t *glut = luts + (int64_t)t * kLutCap;
+                int16_t *wl = slut[i % kV5Slots];
+                const int64_t R = tn.imax - tn.imin;
+                for (int64_t d = lane; d <= R; d += 64) {
+                    const int16_t e = lut_entry<DT>(tn, d);
+                    wl[d] = e;
+                    glut[d] = e;
+                }
+            }
+            if (lane == 0) {
+                sl.tn = tn;
+                sl.tile = t < ntiles ? t : -1;
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // the slot's LUT and parameters have landed in LDS
+            if (lane == 0) __hip_atomic_store(&sl.seq, i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (t >= ntiles) return;  // end marker posted
+        }
+    }
+    // ---- consumer
+    while (true) {
+        const int i = take(1);
+        V5Slot &sl = slot[i % kV5Slots];
+        if (!lds_wait(&sl.seq, i)) return;
+        const int t = sl.tile;
+        if (t < 0) return;
+        const TileNorm tn = sl.tn;
+        const TileGeom g = tiles[t];
+        const typename Elem<DT>::T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
+        const int nfull = g.nframes - (g.partial ? 1 : 0);
+        const bool live = lane < nfull;
+        const int64_t fk = live ? lane : nfull - 1;  // dead lanes re-read the tile's last full frame
+        const int64_t f = g.frame_base + fk;
+        const int64_t s0 = fk * P.blocksize;
+        const int64_t tile_px = (int64_t)g.h * g.w;
+        const int n = live ? (int)min((int64_t)P.blocksize, tile_px - s0) : 0;
+        constexpr int kChunk = 64;
+        const int vec = (g.w % kChunk) == 0 ? P.vec_ok : 0;
+        double acc[kMaxLpc + 1];
+#pragma unroll
+        for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
+        uint32_t or_acc = 0, ft[5];
+        const int16_t *wl = slut[i % kV5Slots];
+        const int16_t *glut = luts + (int64_t)t * kLutCap;
+        if (tn.mode == kNormLut)
+            ana_autoc<DT, kAnaKindLds, kChunk>(base, P, g, s0, tn, wl, glut, window, vec, acc, or_acc, ft);
+        else
+            ana_autoc<DT, kAnaKindZero, kChunk>(base, P, g, s0, tn, wl, glut, window, vec, acc, or_acc, ft);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's reads of the slot are done
+        if (lane == 0) __hip_atomic_store(&sl.free, i + kV5Slots, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (live) out[f] = analysis_finish(acc, or_acc, n, P, ft);
+    }
+}
+
 // ---- wave helpers (64 lanes)
 __device__ inline uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
@@ -3730,7 +3863,21 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                 const int nw = w1 - w0;
                 const unsigned wgrid = (unsigned)((nw + 3) / 4);
                 const int2 *wtk = ctx->wave_tab.as<int2>() + w0;
-                if (fuse_stats) {
+                if (fuse_stats && ctx->ana_v5 && nsplit == 1 && P.nch == 1) {
+                    if constexpr (sizeof(T) == 2) {
+                        // role-split analysis: producers (tile stats + LUT) and consumers (sums) in each work-group
+                        FRS_HIP(ctx->ana_ctr.ensure(64));
+                        FRS_HIP(hipMemsetAsync(ctx->ana_ctr.ptr, 0, sizeof(int), ast));
+                        static int occ5 = 0;  // (per instantiation)
+                        if (occ5 == 0)
+                            FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ5, k_analyze_v5<DT>, 512, 0));
+                        const int64_t g5 = std::min<int64_t>((int64_t)std::max(1, occ5) * ctx->num_cus,
+                                                             ((int64_t)ntiles + 3) / 4);
+                        k_analyze_v5<DT><<<(unsigned)g5, 512, 0, ast>>>(raster, P, dtiles, dnorms,
+                                                                        ctx->luts.as<int16_t>(), ctx->window.as<float>(),
+                                                                        dana, ntiles, ctx->ana_ctr.as<int>(), err_flag);
+                    }
+                } else if (fuse_stats) {
                     if constexpr (sizeof(T) == 2)
                         k_analyze_v3<DT, false, true><<<wgrid, 256, 0, ast>>>(raster, P, dtiles, dnorms,
                                                                               ctx->luts.as<int16_t>(),

@@ -99,6 +99,9 @@ struct frs_ctx {
     void *geo_ptrs[4] = {nullptr, nullptr, nullptr, nullptr};  // tiles, wave_tab, plist, frame_tile as uploaded
     // fast encode path split into enc_split tile ranges ($FRS_ENC_SPLIT, 1..8): range k's analysis runs on aux_stream
     // while range k - 1 is encoded on `stream` (the analysis' min/max bursts and last-round tail overlap the encoder)
+    // role-split analysis (k_analyze_v5: stats producers and sums consumers inside each work-group); $FRS_ANA_V5
+    DevBuf ana_ctr;       // its global tile counter
+    bool ana_v5 = false;
     int enc_split = 1;  // (2-4 measured slower on C4: both kernels are issue-bound, so sharing the CUs gains nothing)
     hipStream_t aux_stream = nullptr;
     hipEvent_t split_ev[9] = {};

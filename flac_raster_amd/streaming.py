@@ -245,27 +245,30 @@ def create_streaming_array(band: np.ndarray, transform: geotiff.Affine, crs: Opt
     fd = os.open(output, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
     try:
         os.ftruncate(fd, len(head) + body)
+        t2b = time.perf_counter()  # (truncating an existing file frees its pages: part of the write cost)
         os.pwrite(fd, head, 0)
         write_tiles(fd, len(head), headers, enc)
     finally:
         os.close(fd)
     t3 = time.perf_counter()
-    tm.update(encode_s=t1 - t0, index_s=t2 - t1, write_s=t3 - t2, total_s=t3 - t0)
+    tm.update(encode_s=t1 - t0, index_s=t2 - t1, write_s=t3 - t2, open_truncate_s=t2b - t2, total_s=t3 - t0)
     return index
 
 
 def create_streaming(input_file: Path, output_file: Path, tile_size: int = 1024,
-                     ctx: Optional[Context] = None, timings: Optional[Dict[str, float]] = None) -> Dict:
+                     ctx: Optional[Context] = None, timings: Optional[Dict[str, float]] = None,
+                     materialize: bool = False) -> Dict:
     """cli.py:620-804 without the console output: writes the streaming file, returns the index.  Band 1 only
     (cli.py:698-699): an uncompressed band-sequential (or single-band) file is encoded straight from its memory map
     (no host copy of the band); otherwise its strips / tiles are decoded.  `timings` gets read_s + the stages of
-    create_streaming_array."""
+    create_streaming_array.  materialize=True reads the band into host memory first (read_s is then the whole read;
+    otherwise the band's pages are read while the encode copies them, inside encode_s)."""
     tm = timings if timings is not None else {}
     t0 = time.perf_counter()
     with geotiff.TiffFile(input_file) as tf:
         transform, epsg, _, _ = tf.georef()
         crs = f"EPSG:{epsg}" if epsg else None
-        band = tf.band_view(0)
+        band = None if materialize else tf.band_view(0)
         if band is None:
             band = tf.read_rows(bands=[0])[0]
         tm["read_s"] = time.perf_counter() - t0

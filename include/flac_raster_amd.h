@@ -23,7 +23,7 @@
  * Python host (flac_raster_amd/container.py): they are text/metadata, not data-parallel work.
  *
  * Conventions: plain C types only; every buffer is caller-allocated.  Functions ending in _device take
- * device pointers (hipMalloc / torch tensors on the context's device) and run on the context's HIP
+ * device pointers (hipMalloc memory of the context's device) and run on the context's HIP
  * stream; the others take host pointers and copy through the context's staging buffers.  All functions
  * return FRS_OK (0) or a negative frs_status; frs_last_error() gives the message.  A context is bound to
  * one device and must not be used from two host threads at once (one context per GPU / rank).

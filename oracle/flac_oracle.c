@@ -26,7 +26,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#define ORC_MAX_LPC 8
+#define ORC_MAX_LPC 12  /* level 7/8 max_lpc_order (level 5: 8) */
 #define ORC_MAX_FIXED 4
 #define ORC_MAX_CH 8
 
@@ -373,8 +373,40 @@ typedef struct {
  * the qlp precision and the wasted-bits cap); extra = 1 for the side channel of process_subframes_'s
  * mid/side pass (subframe_bps_mid_side[1] = bps - w + 1), 0 otherwise.  Samples are int64 so the side
  * channel of a 32-bit stream (33 bits, integer_signal_33bit_side) takes the same code. */
+/* libFLAC 1.4.3 lpc.c FLAC__lpc_window_data_partial: part c of a block cut into 1/b parts, windowed by the rising
+ * half then the falling half of the full-length window (tukey(p / parts): its tapers fit the smallest part), a zero
+ * after it (the autocorrelation reads blocksize / b samples) */
+static void window_partial(const int64_t *x, const float *window, float *out, int data_len, int part_size,
+                           int data_shift) {
+    if (part_size + data_shift < data_len) {
+        int i, j;
+        for (i = 0; i < part_size; i++) out[i] = (float)x[data_shift + i] * window[i];
+        i = i < data_len - part_size - data_shift ? i : data_len - part_size - data_shift;
+        for (j = data_len - part_size; j < data_len; i++, j++) out[i] = (float)x[data_shift + i] * window[j];
+        if (i < data_len) out[i] = 0.0f;
+    }
+}
+
+/* stream_encoder.c set_next_subdivide_tukey: the (depth b, part c) after the current one of a subdivide_tukey(parts)
+ * apodization (c even: partial window c / 2; c odd: the punch-out of part c / 2, i.e. the root window's
+ * autocorrelation minus the partial one's; depth 2 has partial windows only).  Returns 0 when the apodization is
+ * done. */
+static int next_subdivide(int parts, int *b, int *c) {
+    if (*b == 2) {
+        if (*c == 0) *c = 2;
+        else { *c = 0; (*b)++; }
+    } else if (*c < 2 * *b - 1) {
+        (*c)++;
+    } else {
+        *c = 0;
+        (*b)++;
+    }
+    return *b <= parts;
+}
+
 static void decide_subframe(int64_t *x, int n, int bps, int extra, int cfg_blocksize, const float *window,
-                            int32_t *scratch_res, float *scratch_d, subframe_t *sf, int cfg_max_lpc, int cfg_max_po) {
+                            int32_t *scratch_res, float *scratch_d, subframe_t *sf, int cfg_max_lpc, int cfg_max_po,
+                            int parts) {
     /* get_wasted_bits_ / get_wasted_bits_wide_ */
     int64_t orv = 0;
     for (int i = 0; i < n && !(orv & 1); i++) orv |= x[i];
@@ -432,37 +464,63 @@ static void decide_subframe(int64_t *x, int n, int bps, int extra, int cfg_block
             sf->type = SF_FIXED; sf->order = o; sf->rice = rc; sf->est_bits = est;
         }
     }
-    /* lpc */
-    int max_order = cfg_max_lpc;
-    if (max_order >= n) max_order = n - 1;
-    if (max_order <= 0) return;
-    for (int i = 0; i < n; i++) scratch_d[i] = (float)x[i] * window[i];
-    double autoc[ORC_MAX_LPC + 1];
-    autocorrelation(scratch_d, n, max_order + 1, autoc);
-    if (autoc[0] == 0.0) return;
-    float lp[ORC_MAX_LPC][ORC_MAX_LPC];
-    double lerr[ORC_MAX_LPC];
-    max_order = lp_coefficients(autoc, max_order, lp, lerr);
-    int o = best_lpc_order(lerr, max_order, n, sbps + qlp_precision);
-    double lbits = expected_bits_scaled(lerr[o - 1], 0.5 / (double)(n - o));
-    if (lbits >= (double)sbps) return;
-    int prec = qlp_precision;
-    if (sbps <= 17) {
-        int lim = 32 - sbps - (int)ilog2_u64((uint64_t)o);
-        if (lim < prec) prec = lim;
-    }
-    int32_t q[ORC_MAX_LPC];
-    int shift;
-    if (quantize_coefs(lp[o - 1], o, prec, q, &shift) != 0) return;
-    if (!lpc_residual(x, n, q, o, shift, scratch_res)) return;
-    rice_t rc;
-    uint32_t rb = find_best_partition(scratch_res, o, n, sbps, rice_limit, max_po, &rc);
-    uint32_t est = (uint32_t)(1 + 6 + 1 + w + 4 + 5 + sbps * o + prec * o);
-    est = (rb < UINT32_MAX - est) ? est + rb : UINT32_MAX;
-    if (est == 0) return;
-    if (est < sf->est_bits) {
-        sf->type = SF_LPC; sf->order = o; sf->prec = prec; sf->shift = shift;
-        memcpy(sf->q, q, sizeof(q)); sf->rice = rc; sf->est_bits = est;
+    /* lpc: one candidate per window of the apodization (tukey(0.5) at levels <= 5: one window; subdivide_tukey(parts)
+     * at levels 6..8: the full block, then at depth b = 2 .. parts its b partial windows and, from depth 3, their
+     * punch-outs), each LPC candidate replacing the best subframe when strictly smaller */
+    const int cfg_order = cfg_max_lpc >= n ? n - 1 : cfg_max_lpc;
+    if (cfg_order <= 0) return;
+    double autoc[ORC_MAX_LPC + 1], autoc_root[ORC_MAX_LPC + 1];
+    int b = 1, c = 0;
+    for (int more = 1; more;) {
+        int max_order = cfg_order;
+        if (b == 1) {
+            for (int i = 0; i < n; i++) scratch_d[i] = (float)x[i] * window[i];
+            autocorrelation(scratch_d, n, max_order + 1, autoc);
+            if (parts > 1) {
+                memcpy(autoc_root, autoc, sizeof(double) * (size_t)(max_order + 1));
+                b = 2;
+                c = 0;
+            } else {
+                more = 0;
+            }
+        } else {
+            if (n / b <= 32) {  /* (FLAC__MAX_LPC_ORDER) parts this small are not windowed */
+                more = next_subdivide(parts, &b, &c);
+                continue;
+            }
+            if (!(c % 2)) {
+                window_partial(x, window, scratch_d, n, n / b / 2, (c / 2 * n) / b);
+                autocorrelation(scratch_d, n / b, max_order + 1, autoc);
+            } else {
+                for (int i = 0; i <= max_order; i++) autoc[i] = autoc_root[i] - autoc[i];
+            }
+            more = next_subdivide(parts, &b, &c);
+        }
+        if (autoc[0] == 0.0) continue;
+        float lp[ORC_MAX_LPC][ORC_MAX_LPC];
+        double lerr[ORC_MAX_LPC];
+        max_order = lp_coefficients(autoc, max_order, lp, lerr);
+        int o = best_lpc_order(lerr, max_order, n, sbps + qlp_precision);
+        double lbits = expected_bits_scaled(lerr[o - 1], 0.5 / (double)(n - o));
+        if (lbits >= (double)sbps) continue;
+        int prec = qlp_precision;
+        if (sbps <= 17) {
+            int lim = 32 - sbps - (int)ilog2_u64((uint64_t)o);
+            if (lim < prec) prec = lim;
+        }
+        int32_t q[ORC_MAX_LPC];
+        int shift;
+        if (quantize_coefs(lp[o - 1], o, prec, q, &shift) != 0) continue;
+        if (!lpc_residual(x, n, q, o, shift, scratch_res)) continue;
+        rice_t rc;
+        uint32_t rb = find_best_partition(scratch_res, o, n, sbps, rice_limit, max_po, &rc);
+        uint32_t est = (uint32_t)(1 + 6 + 1 + w + 4 + 5 + sbps * o + prec * o);
+        est = (rb < UINT32_MAX - est) ? est + rb : UINT32_MAX;
+        if (est == 0) continue;
+        if (est < sf->est_bits) {
+            sf->type = SF_LPC; sf->order = o; sf->prec = prec; sf->shift = shift;
+            memcpy(sf->q, q, sizeof(q)); sf->rice = rc; sf->est_bits = est;
+        }
     }
 }
 
@@ -627,20 +685,27 @@ int64_t orc_encode_frames_level(const int32_t *interleaved, int64_t nsamples, in
                                 int blocksize, int level, uint8_t *out, int64_t cap) {
     crc_init();
     if (ch < 1 || ch > ORC_MAX_CH || blocksize < 16) return -1;
-    /* compression-level table (docs/sonos-pyflac.txt:6926-6931).  Loose mid/side (levels 1 and 4 on two
-     * channels) and the subdivide_tukey apodizations of levels 6..8 are not restated: -2. */
-    static const int lvl_ms[6] = {0, 1, 1, 0, 1, 1}, lvl_loose[6] = {0, 1, 0, 0, 1, 0};
-    static const int lvl_lpc[6] = {0, 0, 0, 6, 8, 8}, lvl_po[6] = {3, 3, 3, 4, 4, 5};
-    if (level < 0 || level > 5) return -2;
-    if (ch == 2 && lvl_loose[level]) return -2;
-    const int max_lpc = lvl_lpc[level], max_po = lvl_po[level];
+    /* compression-level table (docs/sonos-pyflac.txt:6926-6934): mid/side, loose mid/side, max LPC order, max
+     * residual partition order, apodization (tukey(0.5) = 1 part; subdivide_tukey(2) at 6 and 7, (3) at 8) */
+    static const int lvl_ms[9] = {0, 1, 1, 0, 1, 1, 1, 1, 1}, lvl_loose[9] = {0, 1, 0, 0, 1, 0, 0, 0, 0};
+    static const int lvl_lpc[9] = {0, 0, 0, 6, 8, 8, 8, 12, 12}, lvl_po[9] = {3, 3, 3, 4, 4, 5, 6, 6, 6};
+    static const int lvl_parts[9] = {1, 1, 1, 1, 1, 1, 2, 2, 3};
+    if (level < 0 || level > 8) return -2;
+    const int max_lpc = lvl_lpc[level], max_po = lvl_po[level], parts = lvl_parts[level];
     const int stereo = ch == 2 && lvl_ms[level];
+    const int loose = stereo && lvl_loose[level];
+    /* loose mid/side (stream_encoder.c init): a full independent-vs-mid/side evaluation every
+     * (uint32_t)(sample_rate * 0.4 / blocksize + 0.5) frames (at least 1), the last choice kept in between */
+    int loose_frames = (int)(uint32_t)((double)sample_rate * 0.4 / (double)blocksize + 0.5);
+    if (loose_frames == 0) loose_frames = 1;
+    int loose_count = 0, last_assign = 1;
     const int nv = stereo ? 4 : ch; /* coded signals: channels, or L, R, M, S */
     float *window = (float *)malloc(sizeof(float) * (size_t)blocksize);
     float *dbuf = (float *)malloc(sizeof(float) * (size_t)blocksize);
     int64_t *xbuf = (int64_t *)malloc(sizeof(int64_t) * (size_t)blocksize * (size_t)nv);
     int32_t *res = (int32_t *)malloc(sizeof(int32_t) * (size_t)blocksize);
-    orc_window_tukey(window, blocksize, 0.5f);
+    /* subdivide_tukey(parts): set_apodization stores p / parts (float), the window is tukey(p / parts) */
+    orc_window_tukey(window, blocksize, 0.5f / (float)parts);
     bw_t bw = {out, cap, 0, 0};
     uint32_t frame_no = 0;
     subframe_t sf[ORC_MAX_CH];
@@ -655,20 +720,37 @@ int64_t orc_encode_frames_level(const int32_t *interleaved, int64_t nsamples, in
             int64_t *l = xbuf, *r = xbuf + blocksize, *m = xbuf + 2 * (size_t)blocksize, *sd = xbuf + 3 * (size_t)blocksize;
             for (int i = 0; i < n; i++) { m[i] = (l[i] + r[i]) >> 1; sd[i] = l[i] - r[i]; }
         }
+        /* process_frame_: which signals are coded (loose mid/side: both pairs on an evaluation frame, otherwise
+         * only the pair of the last choice) */
+        int do_ind = 1, do_ms = stereo;
+        if (loose && loose_count > 0) {
+            do_ind = last_assign == 1;
+            do_ms = !do_ind;
+        }
         for (int v = 0; v < nv; v++) {
             memset(&sf[v], 0, sizeof(sf[v]));
+            if (stereo && ((v < 2 && !do_ind) || (v >= 2 && !do_ms))) continue;
             decide_subframe(xbuf + (size_t)v * blocksize, n, bps, stereo && v == 3, blocksize, window, res, dbuf, &sf[v],
-                            max_lpc, max_po);
+                            max_lpc, max_po, parts);
         }
         int assign = ch - 1, pick[2] = {0, 1};
         if (stereo) {
-            const uint32_t bits[4] = {sf[0].est_bits + sf[1].est_bits, sf[0].est_bits + sf[3].est_bits,
-                                      sf[1].est_bits + sf[3].est_bits, sf[2].est_bits + sf[3].est_bits};
             static const int picks[4][2] = {{0, 1}, {0, 3}, {3, 1}, {2, 3}};
             int ca = 0;
-            for (int k = 1; k < 4; k++) if (bits[k] < bits[ca]) ca = k;
+            if (loose && loose_count > 0) {
+                ca = last_assign == 1 ? 0 : 3;
+            } else {
+                const uint32_t bits[4] = {sf[0].est_bits + sf[1].est_bits, sf[0].est_bits + sf[3].est_bits,
+                                          sf[1].est_bits + sf[3].est_bits, sf[2].est_bits + sf[3].est_bits};
+                /* strict <, in this order; loose mid/side considers independent and mid-side only */
+                for (int k = loose ? 3 : 1; k < 4; k++) if (bits[k] < bits[ca]) ca = k;
+            }
             assign = ca == 0 ? 1 : 7 + ca;
             pick[0] = picks[ca][0]; pick[1] = picks[ca][1];
+            if (loose) {
+                loose_count = loose_count + 1 >= loose_frames ? 0 : loose_count + 1;
+                last_assign = assign;
+            }
         }
         write_frame_header(&bw, n, sample_rate, assign, bps, frame_no);
         for (int c = 0; c < ch; c++) {

@@ -106,7 +106,8 @@ def normalize_spatial(arr: np.ndarray) -> np.ndarray:
 
 
 def encode_frames(pcm: np.ndarray, bps: int, sample_rate: int, blocksize: int = 4096, level: int = 5) -> bytes:
-    """libFLAC frames at compression `level` (0..5; not 1 / 4 for two channels) for interleaved pcm [N, C]."""
+    """libFLAC frames at compression `level` (0..8) for interleaved pcm [N, C] (levels 6..8 and loose mid/side at
+    levels 1 / 4 on two channels: restated, parity unpinned -- oracle/flac_oracle.c decide_subframe)."""
     x = np.ascontiguousarray(pcm, dtype=np.int32)
     if x.ndim == 1:
         x = x[:, None]

@@ -1,11 +1,12 @@
-"""Compression levels 0..5 (cli.py:36-37 `-c`, converter.py:112/204, spatial_encoder.py:137/281) in the oracle.
+"""Compression levels 0..8 (cli.py:36-37 `-c`, converter.py:112/204, spatial_encoder.py:137/281) in the oracle.
 
-libFLAC's level table (docs/sonos-pyflac.txt:6926-6931) differs between levels 0..5 only in do/loose mid-side stereo,
-max_lpc_order (0, 0, 0, 6, 8, 8) and max_residual_partition_order (3, 3, 3, 4, 4, 5); the window stays tukey(0.5)
-and the blocksize 4096 (converter.py:205).  Parity for levels other than 5 is UNPINNED: no fixture of the reference
-holds one; these tests check the restatement's structure (predictor and partition limits, lossless decode) and that
-level 5 is the pinned encoder unchanged.  Levels 6..8 (subdivide_tukey) and loose mid/side (1, 4 on two channels)
-are rejected by the oracle, the C-ABI and the host (converter.check_level).
+libFLAC's level table (docs/sonos-pyflac.txt:6926-6934): do/loose mid-side stereo, max_lpc_order (0, 0, 0, 6, 8, 8,
+8, 12, 12), max_residual_partition_order (3, 3, 3, 4, 4, 5, 6, 6, 6) and the apodization -- tukey(0.5) up to level 5,
+subdivide_tukey(2) at 6 and 7, subdivide_tukey(3) at 8 (several windows per subframe, the best LPC candidate kept);
+levels 1 and 4 on two channels use loose mid/side (a full independent-vs-mid/side evaluation every
+round(0.4 s / block) frames, the previous choice in between).  Parity for levels other than 5 is UNPINNED: no fixture
+of the reference holds one; these tests check the restatement's structure (predictor and partition limits, lossless
+decode, the loose mid/side schedule) and that level 5 is the pinned encoder unchanged.
 """
 import numpy as np
 import pytest
@@ -13,7 +14,8 @@ import pytest
 from flac_raster_amd.converter import check_level
 from oracle import oracle as O
 
-LIMITS = {0: (0, 3), 1: (0, 3), 2: (0, 3), 3: (6, 4), 4: (8, 4), 5: (8, 5)}  # (max lpc order, max partition order)
+LIMITS = {0: (0, 3), 1: (0, 3), 2: (0, 3), 3: (6, 4), 4: (8, 4), 5: (8, 5), 6: (8, 6), 7: (12, 6), 8: (12, 6)}
+# (max lpc order, max partition order)
 
 
 def level_signal(n, ch, seed, amp=3000.0):
@@ -31,7 +33,7 @@ def level_signal(n, ch, seed, amp=3000.0):
 
 
 def _ok_levels(ch):
-    return [lv for lv in range(6) if not (ch == 2 and lv in (1, 4))]
+    return list(range(9))
 
 
 @pytest.mark.parametrize("ch", [1, 2, 3])
@@ -76,19 +78,51 @@ def test_stereo_assignments_by_level():
         assert (O.frame_assignments(O.encode_frames(x, 16, 44100, level=lv), 2, 16, n) >= 8).any(), lv
 
 
-def test_unsupported_levels_rejected():
-    x = level_signal(4096, 2, 1)
-    for lv in (1, 4, 6, 8):
-        with pytest.raises(ValueError):
-            O.encode_frames(x, 16, 44100, level=lv)
-    with pytest.raises(ValueError):
-        O.encode_frames(x[:, :1], 16, 44100, level=6)
+def test_levels_6_to_8_use_their_windows_and_orders():
+    """Level 7/8 reach LPC orders above 8 on a resonant signal; levels 6..8 differ from level 5 and from each other
+    (extra windows / orders); every level decodes losslessly."""
+    n = 6 * 4096
+    t = np.arange(n)
+    rng = np.random.default_rng(21)
+    x = (6000 * np.sin(t / 7.3) + 5000 * np.sin(t / 3.1) + 3000 * np.sin(t / 2.05) + 2000 * np.sin(t / 1.37) +
+         1500 * np.sin(t / 1.11) + 900 * np.sin(t / 0.83) + rng.normal(0, 2, n)).astype(np.int32)[:, None]
+    fr = {lv: O.encode_frames(x, 16, 44100, level=lv) for lv in (5, 6, 7, 8)}
+    for lv, f in fr.items():
+        assert np.array_equal(O.decode_frames(f, 1, 16, n), x), lv
+    o7 = O.subframe_types(fr[7], 1, 16, n)[:, 0]
+    assert ((o7 >= 32) & (o7 - 31 > 8)).any()  # orders 9..12
+    assert len({fr[5], fr[6], fr[7], fr[8]}) == 4
+    # the best of several windows: level 8's estimate-driven choice is never larger than one window's on this signal
+    assert len(fr[8]) <= len(fr[7]) * 1.01
+
+
+def test_loose_mid_side_schedule():
+    """Levels 1 and 4 on two channels: assignments are independent (1) or mid-side (10) only, and change only on the
+    evaluation frames (every round(44100 * 0.4 / 4096) = 4 frames from frame 0)."""
+    n = 24 * 4096
+    t = np.arange(n)
+    rng = np.random.default_rng(8)
+    L = 3000 * np.sin(t / 200.0) + rng.normal(0, 30, n)
+    R = np.where((t // 4096) % 6 < 3, L + rng.normal(0, 2, n), rng.normal(0, 3000, n))  # correlated, then not
+    x = np.clip(np.stack([L, R], axis=1), -32768, 32767).astype(np.int32)
+    for lv in (1, 4):
+        f = O.encode_frames(x, 16, 44100, level=lv)
+        assert np.array_equal(O.decode_frames(f, 2, 16, n), x)
+        ca = O.frame_assignments(f, 2, 16, n)
+        assert set(np.unique(ca)) <= {1, 10}, lv
+        assert {1, 10} <= set(np.unique(ca)), lv  # both chosen somewhere
+        for k in range(1, len(ca)):
+            if k % 4:
+                assert ca[k] == ca[k - 1], (lv, k)
+    # the exhaustive search (levels 2 / 5) may pick left-side / right-side on the same signal
+    assert set(np.unique(O.frame_assignments(O.encode_frames(x, 16, 44100, level=5), 2, 16, n))) - {1, 10} or True
+
+
+def test_product_level_gate():
+    """The host accepts every level the GPU kernels implement (converter.check_level)."""
     check_level(0, 2)
     check_level(4, 1)
     check_level(5, 2)
-    for lv, ch in ((1, 2), (4, 2), (6, 1), (7, 3), (8, 1)):
-        with pytest.raises(NotImplementedError):
-            check_level(lv, ch)
     for lv in (-1, 9):
         with pytest.raises(ValueError):
             check_level(lv, 1)
