@@ -25,17 +25,13 @@ FLOAT_DTYPES = (np.dtype(np.float32), np.dtype(np.float64))
 
 
 def check_level(level: int, channels: int) -> None:
-    """libFLAC compression levels this encoder restates (docs/sonos-pyflac.txt:6926-6931): 0..5, except the loose
-    mid/side stereo of levels 1 and 4 on two channels; 6..8 (subdivide_tukey apodizations) are not implemented.
-    The C-ABI rejects the same set (FRS_E_UNSUPPORTED); this raises before any GPU work."""
+    """libFLAC compression levels (docs/sonos-pyflac.txt:6926-6934, cli.py:36-37 `-c 0..8`): all of 0..8 are restated
+    -- level 5 on the fast kernels, the others (subdivide_tukey windows at 6..8, loose mid/side stereo at 1 / 4 on
+    two channels) on the generic kernels; parity for levels other than 5 is unpinned (no reference fixture).  The
+    C-ABI rejects the same range (FRS_E_ARG); this raises before any GPU work."""
+    del channels  # (every level is implemented for every channel count)
     if not 0 <= int(level) <= 8:
         raise ValueError(f"compression level must be 0..8, got {level}")
-    if level > 5:
-        raise NotImplementedError(f"compression level {level} (subdivide_tukey apodization) is not implemented; "
-                                  "levels 0..5 are")
-    if channels == 2 and level in (1, 4):
-        raise NotImplementedError(f"compression level {level} on two bands (loose mid/side stereo) is not "
-                                  "implemented; levels 0, 2, 3 and 5 are")
 
 
 def audio_params(shape0: int, shape1: int, dtype) -> Tuple[int, int]:

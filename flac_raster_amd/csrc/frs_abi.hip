@@ -62,17 +62,9 @@ static int check_desc(frs_ctx *ctx, const frs_encode_desc *d) {
     if (d->nbands < 1 || d->nbands > frs::kMaxChannels) { ctx->err = "nbands must be 1..8 (FLAC channels)"; return FRS_E_ARG; }
     if (frs::dtype_size(d->dtype) == 0) { ctx->err = "bad dtype"; return FRS_E_ARG; }
     if (d->blocksize != 4096) { ctx->err = "blocksize must be 4096 (converter.py:205)"; return FRS_E_UNSUPPORTED; }
-    // levels 0..5 (docs/sonos-pyflac.txt:6926-6931); 6..8 use subdivide_tukey apodizations, and levels 1 / 4 on
-    // two channels loose mid/side stereo: neither is restated
+    // levels 0..8 (docs/sonos-pyflac.txt:6926-6934): level 5 on the fast kernels, the others (subdivide_tukey windows at
+    // 6..8, loose mid/side at 1 / 4 on two channels) on the generic kernels
     if (d->compression_level < 0 || d->compression_level > 8) { ctx->err = "compression level must be 0..8"; return FRS_E_ARG; }
-    if (d->compression_level > 5) {
-        ctx->err = "compression levels 6..8 (subdivide_tukey apodization) are not implemented";
-        return FRS_E_UNSUPPORTED;
-    }
-    if (d->nbands == 2 && frs::level_params(d->compression_level).loose) {
-        ctx->err = "loose mid/side stereo (levels 1 and 4 on two channels) is not implemented";
-        return FRS_E_UNSUPPORTED;
-    }
     if (d->bits_per_sample != 16 && d->bits_per_sample != 24) { ctx->err = "bits_per_sample must be 16 or 24"; return FRS_E_ARG; }
     if (d->sample_rate <= 0 || d->sample_rate > 655350) { ctx->err = "bad sample rate"; return FRS_E_ARG; }
     if (d->norm_mode != 0 && d->norm_mode != 1) { ctx->err = "bad norm_mode"; return FRS_E_ARG; }
@@ -132,7 +124,7 @@ void frs_ctx_destroy(frs_ctx *ctx) {
     hipStreamSynchronize(ctx->stream);
     frs::prof_collect(ctx);
     DevBuf *bufs[] = {&ctx->tiles, &ctx->norms, &ctx->analysis, &ctx->slots, &ctx->frame_bytes, &ctx->frame_off,
-                      &ctx->window, &ctx->tile_sizes, &ctx->luts, &ctx->status, &ctx->frame_tile, &ctx->hdr_tab, &ctx->wave_tab, &ctx->plist, &ctx->ana_ctr, &ctx->sub_slots, &ctx->sub_bits, &ctx->mc_bytes, &ctx->raster_stage, &ctx->arena_stage, &ctx->host_pack,
+                      &ctx->window, &ctx->tile_sizes, &ctx->luts, &ctx->status, &ctx->frame_tile, &ctx->hdr_tab, &ctx->wave_tab, &ctx->plist, &ctx->ana_ctr, &ctx->lpc_cand, &ctx->window_hi, &ctx->loose_assign, &ctx->loose_lead, &ctx->sub_slots, &ctx->sub_bits, &ctx->mc_bytes, &ctx->raster_stage, &ctx->arena_stage, &ctx->host_pack,
                       &ctx->dec_cand, &ctx->dec_count, &ctx->dec_pcm, &ctx->dec_soff, &ctx->dec_next, &ctx->dec_status, &ctx->dec_fb, &ctx->dec_sel,
                       &ctx->dec_chass};
     for (DevBuf *b : bufs) b->release();

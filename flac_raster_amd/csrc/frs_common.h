@@ -75,17 +75,36 @@ struct EncodeParams {
                           // libFLAC's exhaustive mid/side search, stream_encoder.c process_subframes_)
     int32_t max_lpc;      // max_lpc_order of the compression level (0 = fixed predictors only)
     int32_t max_po;       // max_residual_partition_order of the compression level
+    int32_t ncand;        // LPC candidates per coded signal from k_analyze_lpc_hi (subdivide_tukey levels), 0 = the
+                          // single tukey(0.5) candidate of the SubAnalysis
+    int32_t loose_frames; // loose mid/side (levels 1 / 4 on two channels): frames per evaluation, 0 = exhaustive
 };
 
-// libFLAC compression-level table (docs/sonos-pyflac.txt:6926-6931) for the levels this encoder restates (0..5;
-// loose mid/side -- levels 1 and 4 on two channels -- and the subdivide_tukey levels 6..8 are rejected)
+// libFLAC compression-level table (docs/sonos-pyflac.txt:6926-6934): mid/side, loose mid/side, max LPC order, max
+// residual partition order, apodization parts (1 = tukey(0.5); n = subdivide_tukey(n): levels 6, 7 -> 2, 8 -> 3)
 struct LevelParams {
-    int32_t mid_side, loose, max_lpc, max_po;
+    int32_t mid_side, loose, max_lpc, max_po, parts;
 };
 __host__ __device__ inline LevelParams level_params(int level) {
-    constexpr LevelParams t[6] = {{0, 0, 0, 3}, {1, 1, 0, 3}, {1, 0, 0, 3}, {0, 0, 6, 4}, {1, 1, 8, 4}, {1, 0, 8, 5}};
-    return t[level < 0 ? 0 : level > 5 ? 5 : level];
+    constexpr LevelParams t[9] = {{0, 0, 0, 3, 1}, {1, 1, 0, 3, 1}, {1, 0, 0, 3, 1}, {0, 0, 6, 4, 1}, {1, 1, 8, 4, 1},
+                                  {1, 0, 8, 5, 1}, {1, 0, 8, 6, 2}, {1, 0, 12, 6, 2}, {1, 0, 12, 6, 3}};
+    return t[level < 0 ? 0 : level > 8 ? 8 : level];
 }
+// windows of a subdivide_tukey(parts) apodization (stream_encoder.c process_subframe_ + set_next_subdivide_tukey):
+// the full block, 2 partial windows at depth 2, then 2 b per depth b >= 3 (partials and their punch-outs)
+__host__ __device__ inline int apod_windows(int parts) {
+    int n = 1;
+    for (int b = 2; b <= parts; b++) n += b == 2 ? 2 : 2 * b;
+    return n;
+}
+constexpr int kMaxLpcHi = 12;  // max_lpc_order of levels 7 and 8
+constexpr int kMaxCand = 9;    // windows of subdivide_tukey(3)
+constexpr int kMaxPo = 6;      // max residual partition order (levels 6..8)
+// one LPC candidate (one window of the apodization) of a coded signal: quantised predictor or ok = 0
+struct LpcCand {
+    int32_t order, prec, shift, ok;
+    int32_t q[kMaxLpcHi];
+};
 
 __host__ __device__ inline int ilog2_u32(uint32_t v) { return 31 - __builtin_clz(v); }
 __host__ __device__ inline int ilog2_u64(uint64_t v) { return 63 - __builtin_clzll(v); }

@@ -277,21 +277,22 @@ template <int DT> __global__ void k_tile_finalize(TileNorm *norms, int ntiles, i
 // ------------------------------------------------------------------------------- LPC helpers (fp64)
 // FLAC__lpc_compute_lp_coefficients (lpc.c): returns the number of orders computed (early stop on
 // err == 0); err[i] = prediction error after order i+1.
+template <int MAXO = kMaxLpc>
 __device__ int levinson_errors(const double *autoc, int max_order, double *err) {
-    double lpc[kMaxLpc];
+    double lpc[MAXO];
     double e = autoc[0];
     int done = max_order;
 #pragma unroll
-    for (int i = 0; i < kMaxLpc; i++) {
+    for (int i = 0; i < MAXO; i++) {
         if (i < done) {
             double r = -autoc[i + 1];
 #pragma unroll
-            for (int j = 0; j < kMaxLpc; j++)
+            for (int j = 0; j < MAXO; j++)
                 if (j < i) r -= lpc[j] * autoc[i - j];
             r /= e;
             lpc[i] = r;
 #pragma unroll
-            for (int j = 0; j < kMaxLpc / 2; j++) {
+            for (int j = 0; j < MAXO / 2; j++) {
                 if (j < (i >> 1)) {
                     double tmp = lpc[j];
                     lpc[j] += r * lpc[i - 1 - j];
@@ -308,20 +309,21 @@ __device__ int levinson_errors(const double *autoc, int max_order, double *err) 
 }
 
 // same recursion, returns the predictor coefficients of order `order` as floats (lp_coeff[order-1])
+template <int MAXO = kMaxLpc>
 __device__ void levinson_coefs(const double *autoc, int order, float *lp) {
-    double lpc[kMaxLpc];
+    double lpc[MAXO];
     double e = autoc[0];
 #pragma unroll
-    for (int i = 0; i < kMaxLpc; i++) {
+    for (int i = 0; i < MAXO; i++) {
         if (i < order) {
             double r = -autoc[i + 1];
 #pragma unroll
-            for (int j = 0; j < kMaxLpc; j++)
+            for (int j = 0; j < MAXO; j++)
                 if (j < i) r -= lpc[j] * autoc[i - j];
             r /= e;
             lpc[i] = r;
 #pragma unroll
-            for (int j = 0; j < kMaxLpc / 2; j++) {
+            for (int j = 0; j < MAXO / 2; j++) {
                 if (j < (i >> 1)) {
                     double tmp = lpc[j];
                     lpc[j] += r * lpc[i - 1 - j];
@@ -333,7 +335,7 @@ __device__ void levinson_coefs(const double *autoc, int order, float *lp) {
         }
     }
 #pragma unroll
-    for (int j = 0; j < kMaxLpc; j++) lp[j] = j < order ? (float)(-lpc[j]) : 0.0f;
+    for (int j = 0; j < MAXO; j++) lp[j] = j < order ? (float)(-lpc[j]) : 0.0f;
 }
 
 // FLAC__lpc_compute_expected_bits_per_residual_sample_with_error_scale
@@ -647,6 +649,176 @@ __global__ void __launch_bounds__(128) k_analyze(const typename Elem<DT>::T *ras
     out[sub] = generic_decide<WIDE>(acc, tt, (uint64_t)or_acc, (uint64_t)diff, n, P, (ST && ch == 3) ? 1 : 0);
 }
 
+// One LPC candidate from a window's autocorrelation (of the wasted-bit-shifted signal): stream_encoder.c
+// process_subframe_'s LPC branch for one apodization window without exhaustive or precision search --
+// FLAC__lpc_compute_lp_coefficients, FLAC__lpc_compute_best_order (overhead subframe_bps + qlp precision), the
+// expected-bits test against subframe_bps, the 32-bit-decode precision clamp, FLAC__lpc_quantize_coefficients.
+template <int MAXO>
+__device__ inline void lpc_candidate(const double *autoc, int max_order, int n, int sbps, const EncodeParams &P,
+                                     LpcCand &c) {
+    c.ok = 0;
+    c.order = 0;
+    c.prec = 0;
+    c.shift = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxLpcHi; j++) c.q[j] = 0;
+    if (max_order <= 0 || autoc[0] == 0.0) return;
+    double err[MAXO];
+    const int mo = levinson_errors<MAXO>(autoc, max_order, err);
+    const double es = 0.5 / (double)n;
+    const int ovh = sbps + P.qlp_precision;
+    int best = 0;
+    double best_bits = (double)(unsigned)(-1);
+#pragma unroll
+    for (int i = 0; i < MAXO; i++) {
+        if (i < mo) {
+            const int o = i + 1;
+            const double b = expected_bits(err[i], es) * (double)(n - o) + (double)(o * ovh);
+            if (b < best_bits) {
+                best = i;
+                best_bits = b;
+            }
+        }
+    }
+    const int o = best + 1;
+    double eo = err[0];
+#pragma unroll
+    for (int i = 1; i < MAXO; i++)
+        if (i == best) eo = err[i];
+    if (expected_bits(eo, 0.5 / (double)(n - o)) >= (double)sbps) return;
+    int prec = P.qlp_precision;
+    if (sbps <= 17) {
+        const int lim = 32 - sbps - ilog2_u32((uint32_t)o);
+        prec = lim < prec ? lim : prec;
+    }
+    float lp[MAXO];
+    levinson_coefs<MAXO>(autoc, o, lp);
+    const int pm1 = prec - 1;
+    const int32_t qmax = (1 << pm1) - 1, qmin = -(1 << pm1);
+    double cmax = 0.0;
+#pragma unroll
+    for (int j = 0; j < MAXO; j++)
+        if (j < o) {
+            const double d = fabs((double)lp[j]);
+            if (d > cmax) cmax = d;
+        }
+    if (!(cmax > 0.0)) return;
+    int shift = pm1 - ilogb(cmax) - 1;
+    if (shift > 15) shift = 15;
+    else if (shift < -16) return;
+    double error = 0.0;
+    const float m = (float)(1 << (shift >= 0 ? shift : -shift));
+#pragma unroll
+    for (int j = 0; j < MAXO; j++)
+        if (j < o) {
+            error += shift >= 0 ? (double)(lp[j] * m) : (double)(lp[j] / m);
+            int64_t qi = lround_exact(error);
+            if (qi > qmax) qi = qmax;
+            else if (qi < qmin) qi = qmin;
+            error -= (double)qi;
+            c.q[j] = (int32_t)qi;
+        }
+    c.order = o;
+    c.prec = prec;
+    c.shift = shift >= 0 ? shift : 0;
+    c.ok = 1;
+}
+
+// k_analyze_lpc_hi: the LPC candidates of the subdivide_tukey(parts) levels (6..8), one lane per coded signal (as
+// k_analyze, which has produced the signal's wasted bits and fixed-predictor decisions with max_lpc 0).  libFLAC
+// evaluates one LPC subframe per window of the apodization (stream_encoder.c process_subframe_ with
+// set_next_subdivide_tukey): window 0 is the whole block under tukey(0.5 / parts); at depth b = 2 .. parts the block
+// is cut into b parts (part j starts at (j n) / b), each windowed by the rising then the falling half of that window
+// (lpc.c FLAC__lpc_window_data_partial, n / b / 2 samples each, autocorrelation over n / b samples); from depth 3
+// every partial window is followed by its punch-out, whose autocorrelation is the whole block's minus the part's.
+// Parts of n / b <= 32 samples are skipped.  Each window's autocorrelation is summed per lag in sample order (as
+// FLAC__lpc_compute_autocorrelation), so the candidates match the oracle's (oracle/flac_oracle.c decide_subframe).
+template <int DT, bool WIDE, bool ST = false>
+__global__ void __launch_bounds__(128) k_analyze_lpc_hi(const typename Elem<DT>::T *raster, EncodeParams P,
+                                                       const TileGeom *tiles, const TileNorm *norms,
+                                                       const float *__restrict__ window, const SubAnalysis *ana,
+                                                       LpcCand *cand, int parts) {
+    using T = typename Elem<DT>::T;
+    using XA = std::conditional_t<ST && WIDE, int64_t, int32_t>;
+    const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= P.nframes * P.nvch) return;
+    const int64_t f = li / P.nvch;
+    const int ch = (int)(li - f * P.nvch);
+    const int t = tile_of_frame(tiles, P.ntiles, f);
+    const TileGeom g = tiles[t];
+    const int64_t s0 = (f - g.frame_base) * P.blocksize;
+    const int64_t tile_px = (int64_t)g.h * g.w;
+    const int n = (int)((tile_px - s0) < P.blocksize ? (tile_px - s0) : P.blocksize);
+    const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits, P.norm_mode);
+    const SubAnalysis A = ana[li];
+    LpcCand *out = cand + li * P.ncand;
+    LpcCand none;
+    none.ok = 0;
+    none.order = none.prec = none.shift = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxLpcHi; j++) none.q[j] = 0;
+    for (int c = 0; c < P.ncand; c++) out[c] = none;
+    const int w = A.wasted;
+    const int sbps = P.bps - w + ((ST && ch == 3) ? 1 : 0);
+    const int max_order = P.max_lpc < n ? P.max_lpc : n - 1;
+    if (n <= 4 || (A.flags & kFlagConstant) || max_order <= 0) return;
+    const double sc = ldexp(1.0, -2 * w);  // autocorrelation of the shifted signal (power-of-two scaling: exact)
+    const T *band = raster + (int64_t)(P.band0 + (ST ? 0 : ch)) * P.band_stride + g.r0 * P.row_stride + g.c0;
+    auto sample = [&](int i) -> XA {  // coded sample i of the frame (unshifted)
+        const int64_t q = s0 + i, r = q / g.w;
+        const T *pp = band + r * P.row_stride + (q - r * g.w);
+        if constexpr (ST) return coded_sample<DT, true, XA>(pp, P.band_stride, nz, ch);
+        else return (XA)nz(*pp);
+    };
+    // autocorrelation (lags 0..12, scaled) of `len` windowed samples from `start`: ps == 0 the whole block with
+    // window[i], else a part with the rising half window[0, ps) then the falling half window[n - ps, n)
+    auto autoc_of = [&](int start, int len, int ps, double *ac) {
+        double h[kMaxLpcHi];
+#pragma unroll
+        for (int l = 0; l <= kMaxLpcHi; l++) ac[l] = 0.0;
+#pragma unroll
+        for (int l = 0; l < kMaxLpcHi; l++) h[l] = 0.0;
+        for (int s = 0; s < len; s++) {
+            const int wi = ps == 0 ? s : (s < ps ? s : n - 2 * ps + s);
+            const double d = (double)((float)sample(start + s) * window[wi]);
+            ac[0] = fma(d, d, ac[0]);
+#pragma unroll
+            for (int l = 1; l <= kMaxLpcHi; l++) ac[l] = fma(d, h[l - 1], ac[l]);
+#pragma unroll
+            for (int l = kMaxLpcHi - 1; l > 0; l--) h[l] = h[l - 1];
+            h[0] = d;
+        }
+#pragma unroll
+        for (int l = 0; l <= kMaxLpcHi; l++) ac[l] *= sc;
+    };
+    double root[kMaxLpcHi + 1], ac[kMaxLpcHi + 1];
+    autoc_of(0, n, 0, root);
+    LpcCand c;
+    lpc_candidate<kMaxLpcHi>(root, max_order, n, sbps, P, c);
+    out[0] = c;
+    int k = 1;
+    for (int b = 2; b <= parts; b++) {
+        for (int j = 0; j < b; j++) {
+            const bool skip = n / b <= 32;  // (FLAC__MAX_LPC_ORDER) too small a part to window
+            if (!skip) {
+                autoc_of((j * n) / b, 2 * (n / b / 2), n / b / 2, ac);
+                lpc_candidate<kMaxLpcHi>(ac, max_order, n, sbps, P, c);
+                out[k] = c;
+            }
+            k++;
+            if (b >= 3) {
+                if (!skip) {
+#pragma unroll
+                    for (int l = 0; l <= kMaxLpcHi; l++) ac[l] = root[l] - ac[l];
+                    lpc_candidate<kMaxLpcHi>(ac, max_order, n, sbps, P, c);
+                    out[k] = c;
+                }
+                k++;
+            }
+        }
+    }
+}
+
 // The fast path's partial last frames (n < blocksize, at most one per tile, 16-bit mono streams): one work-group per
 // frame instead of one lane (k_analyze's lane walks 4096 samples with fp64 divisions: ~0.75 ms for any number of
 // frames).  The frame is normalised and windowed in parallel into LDS; lag l of the autocorrelation is summed by
@@ -857,13 +1029,13 @@ struct RiceChoice {
     uint32_t bits;   // estimated residual bits (find_best_partition_order_)
     int order;       // partition order
     int rice2;
-    uint8_t k[32];   // parameters
+    uint8_t k[1 << kMaxPo];  // parameters
 };
 
 // set_partitioned_rice_ for every order in [0, max_po] from the max-order partition sums; returns best.
 __device__ void rice_search(const uint64_t *sums_max, int max_po, int n, int pred_order, int rice_limit,
                             RiceChoice *rc) {
-    uint64_t sums[64];
+    uint64_t sums[2 << kMaxPo];
     const int parts = 1 << max_po;
     for (int p = 0; p < parts; p++) sums[p] = sums_max[p];
     int from = 0, to = parts, pp = parts;
@@ -881,7 +1053,7 @@ __device__ void rice_search(const uint64_t *sums_max, int max_po, int n, int pre
         const uint32_t pbase = (uint32_t)(n >> po);
         const uint32_t div_base = 0x40000u / pbase;
         uint32_t bits = 2 + 4;
-        uint8_t ks[32];
+        uint8_t ks[1 << kMaxPo];
         bool ok = true;
         for (int p = 0; p < np; p++) {
             uint32_t ns = pbase, div = div_base;
@@ -949,8 +1121,11 @@ template <typename XT> struct EncShared {
     static constexpr int kWords = sizeof(XT) == 8 ? 4096 + 192 : kBitWords;
     XT xs[kMaxBlock + kMaxBlock / 16];
     uint32_t bits[kWords];
-    uint64_t psum[2][32];
+    uint64_t psum[2][1 << kMaxPo];
     RiceChoice rc[2];
+    RiceChoice rc_try;   // an LPC candidate under evaluation (subdivide_tukey levels: several per signal)
+    LpcCand lsel;        // the chosen LPC candidate of the current signal
+    uint32_t lpc_best;   // its estimated bits (0xFFFFFFFF: none)
     int lpc_bad;
     int choice;          // subframe type: 0 const, 1 verbatim, 2 fixed, 3 lpc
     uint32_t best;       // its estimated bits (process_subframe_'s best_bits)
@@ -958,6 +1133,7 @@ template <typename XT> struct EncShared {
     int vtype[4];
     uint32_t vbits[4];
     RiceChoice vrc[4];
+    LpcCand vl[4];
     int assign;          // FLAC__ChannelAssignment: 0 independent, 1 left-side, 2 right-side, 3 mid-side
 };
 
@@ -965,12 +1141,19 @@ template <typename XT> struct EncShared {
 // the assignment with the fewest estimated bits wins (stream_encoder.c process_subframes_, do_mid_side_stereo &&
 // !loose: independent, left-side, right-side, mid-side; a later one only if strictly smaller) and its two subframes
 // are written.
+// cand (subdivide_tukey levels): P.ncand LPC candidates per coded signal (k_analyze_lpc_hi), evaluated in window order
+// (a later one only if strictly smaller).  Loose mid/side (P.loose_frames > 0, levels 1 / 4 on two channels): the
+// assignment of a frame is the one chosen on its group's first frame (frame number within the stream a multiple of
+// loose_frames) between independent and mid-side; loose_pass = 1 evaluates the group leaders (flist) and stores their
+// choice in loose_assign[frame], loose_pass = 0 codes every frame with its leader's choice.
 template <int DT, bool ST = false, typename XT = int32_t>
 __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename Elem<DT>::T *raster, EncodeParams P,
                                                              const TileGeom *tiles, const TileNorm *norms,
                                                              const SubAnalysis *ana, uint32_t *slots,
                                                              int64_t *frame_bytes, int *error_flag,
-                                                             const int64_t *__restrict__ flist) {
+                                                             const int64_t *__restrict__ flist,
+                                                             const LpcCand *__restrict__ cand = nullptr,
+                                                             int8_t *loose_assign = nullptr, int loose_pass = 0) {
     // flist: frames to code (the fast path's partial last frames; slot / frame_bytes indexed by list position),
     // nullptr = frame blockIdx.x
     using T = typename Elem<DT>::T;
@@ -1005,12 +1188,12 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
             const int cc = (int)(p - r * g.w);
             S.xs[xsi(i)] = coded_sample<DT, ST, XT>(base + r * P.row_stride + cc, P.band_stride, nz, ST ? v : 0) >> w;
         }
-        if (tid < 64) S.psum[tid >> 5][tid & 31] = 0;
+        if (tid < (2 << kMaxPo)) S.psum[tid >> kMaxPo][tid & ((1 << kMaxPo) - 1)] = 0;
         if (tid == 0) S.lpc_bad = 0;
         __syncthreads();
     };
-    // residual i of the FIXED (fixed == true) or LPC predictor of order o
-    auto resid = [&](const SubAnalysis &A, bool fixed, int o, int i) -> int64_t {
+    // residual i of the FIXED (fixed == true) or LPC predictor (L) of order o
+    auto resid = [&](const LpcCand &L, bool fixed, int o, int i) -> int64_t {
         int64_t r;
         if (fixed) {
             const int64_t x = S.xs[xsi(i)];
@@ -1023,8 +1206,8 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
             }
         } else {
             int64_t s = 0;
-            for (int j = 0; j < o; j++) s += (int64_t)A.q[j] * S.xs[xsi(i - 1 - j)];
-            r = (int64_t)S.xs[xsi(i)] - (s >> A.lpc_shift);
+            for (int j = 0; j < o; j++) s += (int64_t)L.q[j] * S.xs[xsi(i - 1 - j)];
+            r = (int64_t)S.xs[xsi(i)] - (s >> L.shift);
         }
         return r;
     };
@@ -1034,41 +1217,67 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
         return m;
     };
     // ---- process_subframe_: candidate partition sums, Rice search, choice (VERBATIM, CONSTANT | FIXED, LPC; strict <)
-    //      -> S.choice, S.best, S.rc
-    auto decide = [&](const SubAnalysis &A, int extra) {
+    //      -> S.choice, S.best, S.rc, S.lsel.  LPC candidates: A's single one (tukey(0.5) levels) or the signal's
+    //      P.ncand window candidates, each evaluated in turn and kept when strictly smaller than the best so far.
+    auto decide = [&](const SubAnalysis &A, int extra, const LpcCand *cands) {
         const int w = A.wasted;
         const int sbps = P.bps - w + extra;
         const bool cand_fixed = n > 4 && !(A.flags & kFlagConstant) && (A.flags & kFlagFixedOk);
-        const bool cand_lpc = n > 4 && !(A.flags & kFlagConstant) && (A.flags & kFlagLpcOk);
-        const int mpo[2] = {max_po_for(A.fixed_order), max_po_for(A.lpc_order)};
-        for (int cand = 0; cand < 2; cand++) {
-            if (cand == 0 && !cand_fixed) continue;
-            if (cand == 1 && !cand_lpc) continue;
-            const int o = cand == 0 ? A.fixed_order : A.lpc_order;
-            const int ps = n >> mpo[cand];
-            int cur_p = -1;
-            uint64_t acc = 0;
-            for (int i = max(i_beg, o); i < i_end; i++) {
-                int64_t r = resid(A, cand == 0, o, i);
-                if (cand == 0) r = (int32_t)r;  // libFLAC stores fixed residuals as int32
-                else if (r <= INT32_MIN || r > INT32_MAX) S.lpc_bad = 1;
-                const int p = i / ps;
-                if (p != cur_p) {
-                    if (cur_p >= 0) atomicAdd((unsigned long long *)&S.psum[cand][cur_p], (unsigned long long)acc);
-                    cur_p = p;
-                    acc = 0;
-                }
-                acc += (uint64_t)(r < 0 ? -r : r);
+        LpcCand a1;  // the SubAnalysis' candidate as a candidate record
+        a1.order = A.lpc_order;
+        a1.prec = A.lpc_prec;
+        a1.shift = A.lpc_shift;
+        a1.ok = (A.flags & kFlagLpcOk) ? 1 : 0;
+#pragma unroll
+        for (int j = 0; j < kMaxLpcHi; j++) a1.q[j] = j < kMaxLpc ? A.q[j] : 0;
+        const int nc = cands ? P.ncand : 1;
+        const bool lpc_any = n > 4 && !(A.flags & kFlagConstant);
+        if (tid == 0) S.lpc_best = 0xFFFFFFFFu;
+        for (int c = 0; c < nc; c++) {
+            const LpcCand L = cands ? cands[c] : a1;
+            const bool do_fixed = c == 0 && cand_fixed;
+            const bool do_lpc = lpc_any && L.ok;
+            if (c > 0) {  // the previous candidate's sums have been read
+                if (tid < (1 << kMaxPo)) S.psum[1][tid] = 0;
+                if (tid == 0) S.lpc_bad = 0;
+                __syncthreads();
             }
-            if (cur_p >= 0) atomicAdd((unsigned long long *)&S.psum[cand][cur_p], (unsigned long long)acc);
+            const int mpo[2] = {max_po_for(A.fixed_order), max_po_for(L.order)};
+            for (int cd = 0; cd < 2; cd++) {
+                if (cd == 0 && !do_fixed) continue;
+                if (cd == 1 && !do_lpc) continue;
+                const int o = cd == 0 ? A.fixed_order : L.order;
+                const int ps = n >> mpo[cd];
+                int cur_p = -1;
+                uint64_t acc = 0;
+                for (int i = max(i_beg, o); i < i_end; i++) {
+                    int64_t r = resid(L, cd == 0, o, i);
+                    if (cd == 0) r = (int32_t)r;  // libFLAC stores fixed residuals as int32
+                    else if (r <= INT32_MIN || r > INT32_MAX) S.lpc_bad = 1;
+                    const int p = i / ps;
+                    if (p != cur_p) {
+                        if (cur_p >= 0) atomicAdd((unsigned long long *)&S.psum[cd][cur_p], (unsigned long long)acc);
+                        cur_p = p;
+                        acc = 0;
+                    }
+                    acc += (uint64_t)(r < 0 ? -r : r);
+                }
+                if (cur_p >= 0) atomicAdd((unsigned long long *)&S.psum[cd][cur_p], (unsigned long long)acc);
+            }
+            __syncthreads();
+            if (tid == 0 && do_fixed) rice_search(S.psum[0], mpo[0], n, A.fixed_order, rice_limit, &S.rc[0]);
+            if (tid == 64 && do_lpc && !S.lpc_bad) {
+                rice_search(S.psum[1], mpo[1], n, L.order, rice_limit, &S.rc_try);
+                uint32_t est = (uint32_t)(1 + 6 + 1 + w + 4 + 5 + sbps * L.order + L.prec * L.order);
+                est = (S.rc_try.bits < 0xFFFFFFFFu - est) ? est + S.rc_try.bits : 0xFFFFFFFFu;
+                if (est != 0 && est < S.lpc_best) {
+                    S.lpc_best = est;
+                    S.rc[1] = S.rc_try;
+                    S.lsel = L;
+                }
+            }
+            __syncthreads();
         }
-        __syncthreads();
-        if (tid == 0 || tid == 64) {
-            const int cand = tid == 0 ? 0 : 1;
-            const bool on = cand == 0 ? cand_fixed : (cand_lpc && !S.lpc_bad);
-            if (on) rice_search(S.psum[cand], mpo[cand], n, cand == 0 ? A.fixed_order : A.lpc_order, rice_limit, &S.rc[cand]);
-        }
-        __syncthreads();
         if (tid == 0) {
             uint32_t best = (uint32_t)(1 + 6 + 1 + w + n * sbps);
             int type = 1;
@@ -1088,13 +1297,9 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
                             type = 2;
                         }
                     }
-                    if (cand_lpc && !S.lpc_bad) {
-                        uint32_t est = (uint32_t)(1 + 6 + 1 + w + 4 + 5 + sbps * A.lpc_order + A.lpc_prec * A.lpc_order);
-                        est = (S.rc[1].bits < 0xFFFFFFFFu - est) ? est + S.rc[1].bits : 0xFFFFFFFFu;
-                        if (est != 0 && est < best) {
-                            best = est;
-                            type = 3;
-                        }
+                    if (S.lpc_best != 0xFFFFFFFFu && S.lpc_best < best) {
+                        best = S.lpc_best;
+                        type = 3;
                     }
                 }
             }
@@ -1105,14 +1310,21 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
     };
 
     if constexpr (ST) {
+        // loose mid/side, coding pass: the group leader's assignment (and only that pair is evaluated)
+        const bool loose = P.loose_frames > 0;
+        int lead_ca = -1;
+        if (loose && !loose_pass) lead_ca = loose_assign[f - (fk % P.loose_frames)];
         for (int v = 0; v < 4; v++) {
+            if (lead_ca == 0 && v >= 2) continue;
+            if (lead_ca == 3 && v < 2) continue;
             const SubAnalysis A = ana[f * 4 + v];
             load(v, A.wasted);
-            decide(A, v == 3 ? 1 : 0);
+            decide(A, v == 3 ? 1 : 0, cand ? cand + (f * 4 + v) * P.ncand : nullptr);
             if (tid == 0) {
                 S.vtype[v] = S.choice;
                 S.vbits[v] = S.best;
                 S.vrc[v] = S.rc[S.choice == 2 ? 0 : 1];
+                S.vl[v] = S.lsel;
             }
             __syncthreads();
         }
@@ -1120,11 +1332,14 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
             const uint32_t bits[4] = {S.vbits[0] + S.vbits[1], S.vbits[0] + S.vbits[3], S.vbits[1] + S.vbits[3],
                                       S.vbits[2] + S.vbits[3]};
             int ca = 0;
-            for (int k = 1; k < 4; k++)
+            // strict <, in this order; loose mid/side weighs independent against mid-side only
+            for (int k = loose ? 3 : 1; k < 4; k++)
                 if (bits[k] < bits[ca]) ca = k;
-            S.assign = ca;
+            S.assign = lead_ca >= 0 ? lead_ca : ca;
+            if (loose && loose_pass) loose_assign[f] = (int8_t)ca;
         }
         __syncthreads();
+        if (loose && loose_pass) return;  // (leader pass: the choice only)
     }
 
     // ---- frame header (RFC 9639 9.1; libFLAC FLAC__frame_add_header), thread 0
@@ -1213,19 +1428,23 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
         load(v, w);
         int type;
         const RiceChoice *rcp;
+        const LpcCand *lcp;
         if constexpr (ST) {
             type = S.vtype[v];
             rcp = &S.vrc[v];
+            lcp = &S.vl[v];
         } else {
-            decide(A, 0);
+            decide(A, 0, cand ? cand + (f * P.nvch + v) * P.ncand : nullptr);
             type = S.choice;
             rcp = &S.rc[type == 2 ? 0 : 1];
+            lcp = &S.lsel;
         }
+        const LpcCand Lc = *lcp;
 
         // ---- emit the subframe bits at fb (relative to S.bits)
         const uint64_t sb = fb;
         uint64_t pos = sb;
-        const int typecode = type == 0 ? 0 : type == 1 ? 1 : type == 2 ? 8 + A.fixed_order : 32 + A.lpc_order - 1;
+        const int typecode = type == 0 ? 0 : type == 1 ? 1 : type == 2 ? 8 + A.fixed_order : 32 + Lc.order - 1;
         if (tid == 0) {
             put_bits(S.bits, pos, (uint32_t)(typecode << 1) | (w ? 1u : 0u), 8);
         }
@@ -1242,19 +1461,19 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
             for (int i = tid; i < n; i += kEncThreads) put_sample(S.bits, pos + (uint64_t)i * sbps, S.xs[xsi(i)], sbps);
             sub_end = pos + (uint64_t)n * sbps;
         } else {
-            const int o = type == 2 ? A.fixed_order : A.lpc_order;
+            const int o = type == 2 ? A.fixed_order : Lc.order;
             const RiceChoice &rc = *rcp;
             for (int i = tid; i < o; i++) put_sample(S.bits, pos + (uint64_t)i * sbps, S.xs[xsi(i)], sbps);
             pos += (uint64_t)o * sbps;
             if (type == 3) {
                 if (tid == 0) {
-                    put_bits(S.bits, pos, (uint32_t)(A.lpc_prec - 1), 4);
-                    put_bits(S.bits, pos + 4, mask_bits(A.lpc_shift, 5), 5);
+                    put_bits(S.bits, pos, (uint32_t)(Lc.prec - 1), 4);
+                    put_bits(S.bits, pos + 4, mask_bits(Lc.shift, 5), 5);
                 }
                 pos += 9;
                 for (int j = tid; j < o; j += kEncThreads)
-                    put_bits(S.bits, pos + (uint64_t)j * A.lpc_prec, mask_bits(A.q[j], A.lpc_prec), A.lpc_prec);
-                pos += (uint64_t)o * A.lpc_prec;
+                    put_bits(S.bits, pos + (uint64_t)j * Lc.prec, mask_bits(Lc.q[j], Lc.prec), Lc.prec);
+                pos += (uint64_t)o * Lc.prec;
             }
             if (tid == 0) {
                 put_bits(S.bits, pos, (uint32_t)rc.rice2, 2);
@@ -1267,7 +1486,7 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
             // per-thread code lengths of its chunk, then block exclusive scan
             uint64_t my = 0;
             for (int i = max(i_beg, o); i < i_end; i++) {
-                const int32_t r32 = (int32_t)resid(A, type == 2, o, i);
+                const int32_t r32 = (int32_t)resid(Lc, type == 2, o, i);
                 const uint32_t u = ((uint32_t)r32 << 1) ^ (uint32_t)(r32 >> 31);
                 const int k = rc.k[i / ps];
                 my += 1 + (uint64_t)k + (u >> k);
@@ -1296,9 +1515,9 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
             // bit position of sample i = pos + pbits*(p_i + 1) + (sum of code lengths before i);
             // partition p's parameter field precedes its first code
             uint64_t run = excl;
-            __shared__ uint64_t pstart[32];
+            __shared__ uint64_t pstart[1 << kMaxPo];
             for (int i = max(i_beg, o); i < i_end; i++) {
-                const int32_t r32 = (int32_t)resid(A, type == 2, o, i);
+                const int32_t r32 = (int32_t)resid(Lc, type == 2, o, i);
                 const uint32_t u = ((uint32_t)r32 << 1) ^ (uint32_t)(r32 >> 31);
                 const int p = i / ps;
                 const int k = rc.k[p];
@@ -3706,6 +3925,13 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     P.nvch = (P.nch == 2 && lv.mid_side) ? 4 : P.nch;
     P.max_lpc = lv.max_lpc;
     P.max_po = lv.max_po;
+    P.ncand = lv.parts > 1 ? apod_windows(lv.parts) : 0;
+    // loose mid/side (stream_encoder.c init): an evaluation every (uint32_t)(sample_rate * 0.4 / blocksize + 0.5) frames
+    P.loose_frames = 0;
+    if (P.nch == 2 && lv.mid_side && lv.loose) {
+        P.loose_frames = (int32_t)(uint32_t)((double)d->sample_rate * 0.4 / (double)d->blocksize + 0.5);
+        if (P.loose_frames == 0) P.loose_frames = 1;
+    }
     const bool level5 = d->compression_level == 5;  // the fast kernels hard-code level 5's search
 
     int rc = upload_tables(ctx);
@@ -4098,43 +4324,103 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         return FRS_OK;
     }
     FRS_HIP(ctx->slots.ensure((size_t)nframes * P.slot_words * 4));
-    // 2. analysis (lane = coded signal: channel, or L/R/M/S of a two-channel stream)
+    // 2. analysis (lane = coded signal: channel, or L/R/M/S of a two-channel stream).  subdivide_tukey levels: the
+    //    fixed-predictor / wasted-bits analysis first (max_lpc 0), then the LPC candidates of every window
     const int64_t nsub = nframes * P.nvch;
     const bool stereo = P.nvch == 4 && P.nch == 2;
     const unsigned agrid = (unsigned)((nsub + 127) / 128);
+    EncodeParams Pa = P;
+    LpcCand *dcand = nullptr;
+    if (P.ncand > 0) {
+        Pa.max_lpc = 0;
+        FRS_HIP(ctx->lpc_cand.ensure(sizeof(LpcCand) * (size_t)nsub * (size_t)P.ncand));
+        dcand = ctx->lpc_cand.as<LpcCand>();
+        if (ctx->window_hi_bs != d->blocksize || ctx->window_hi_parts != lv.parts) {
+            // subdivide_tukey(parts): FLAC__stream_encoder_set_apodization stores p / parts, the window is
+            // FLAC__window_tukey(p / parts) (float p = 0.5f)
+            std::vector<float> win(d->blocksize, 1.0f);
+            const float pw = 0.5f / (float)lv.parts;
+            const int L = d->blocksize;
+            const int Np = (int)(pw / 2.0f * (float)L) - 1;
+            if (Np > 0)
+                for (int k = 0; k <= Np; k++) {
+                    win[k] = (float)(0.5f - 0.5f * cos(M_PI * k / Np));
+                    win[L - Np - 1 + k] = (float)(0.5f - 0.5f * cos(M_PI * (k + Np) / Np));
+                }
+            FRS_HIP(ctx->window_hi.ensure(sizeof(float) * L));
+            FRS_HIP(hipMemcpyAsync(ctx->window_hi.ptr, win.data(), sizeof(float) * L, hipMemcpyHostToDevice, st));
+            FRS_HIP(hipStreamSynchronize(st));
+            ctx->window_hi_bs = d->blocksize;
+            ctx->window_hi_parts = lv.parts;
+        }
+    }
     prof_begin(ctx, "analyze", &ev);
     if (P.bps > 16) {
         if (stereo) {
-            k_analyze<DT, true, true><<<agrid, 128, 0, st>>>(raster, P, dtiles, dnorms, ctx->window.as<float>(), dana,
+            k_analyze<DT, true, true><<<agrid, 128, 0, st>>>(raster, Pa, dtiles, dnorms, ctx->window.as<float>(), dana,
                                                                 nullptr, 0);
-            k_analyze_fixed_wide<DT, true><<<agrid, 128, 0, st>>>(raster, P, dtiles, dnorms, dana);
+            k_analyze_fixed_wide<DT, true><<<agrid, 128, 0, st>>>(raster, Pa, dtiles, dnorms, dana);
+            if (dcand)
+                k_analyze_lpc_hi<DT, true, true><<<agrid, 128, 0, st>>>(raster, P, dtiles, dnorms,
+                                                                        ctx->window_hi.as<float>(), dana, dcand, lv.parts);
         } else {
-            k_analyze<DT, true><<<agrid, 128, 0, st>>>(raster, P, dtiles, dnorms, ctx->window.as<float>(), dana,
+            k_analyze<DT, true><<<agrid, 128, 0, st>>>(raster, Pa, dtiles, dnorms, ctx->window.as<float>(), dana,
                                                          nullptr, 0);
-            k_analyze_fixed_wide<DT><<<agrid, 128, 0, st>>>(raster, P, dtiles, dnorms, dana);
+            k_analyze_fixed_wide<DT><<<agrid, 128, 0, st>>>(raster, Pa, dtiles, dnorms, dana);
+            if (dcand)
+                k_analyze_lpc_hi<DT, true><<<agrid, 128, 0, st>>>(raster, P, dtiles, dnorms, ctx->window_hi.as<float>(),
+                                                                  dana, dcand, lv.parts);
         }
     } else {
-        if (stereo)
-            k_analyze<DT, false, true><<<agrid, 128, 0, st>>>(raster, P, dtiles, dnorms, ctx->window.as<float>(), dana,
+        if (stereo) {
+            k_analyze<DT, false, true><<<agrid, 128, 0, st>>>(raster, Pa, dtiles, dnorms, ctx->window.as<float>(), dana,
                                                                  nullptr, 0);
-        else
-            k_analyze<DT, false><<<agrid, 128, 0, st>>>(raster, P, dtiles, dnorms, ctx->window.as<float>(), dana,
+            if (dcand)
+                k_analyze_lpc_hi<DT, false, true><<<agrid, 128, 0, st>>>(raster, P, dtiles, dnorms,
+                                                                         ctx->window_hi.as<float>(), dana, dcand,
+                                                                         lv.parts);
+        } else {
+            k_analyze<DT, false><<<agrid, 128, 0, st>>>(raster, Pa, dtiles, dnorms, ctx->window.as<float>(), dana,
                                                           nullptr, 0);
+            if (dcand)
+                k_analyze_lpc_hi<DT, false><<<agrid, 128, 0, st>>>(raster, P, dtiles, dnorms, ctx->window_hi.as<float>(),
+                                                                   dana, dcand, lv.parts);
+        }
     }
     prof_end(ctx, "analyze", ev);
-    // 3. encode frames into slots
+    // 3. encode frames into slots (loose mid/side: the group leaders' assignments first)
     prof_begin(ctx, "encode", &ev);
     uint32_t *dslots = ctx->slots.as<uint32_t>();
     int64_t *dfb = ctx->frame_bytes.as<int64_t>();
+    int8_t *dloose = nullptr;
+    if (stereo && P.loose_frames > 0) {
+        std::vector<int64_t> leaders;
+        for (const TileGeom &tg : tiles)
+            for (int k = 0; k < tg.nframes; k += P.loose_frames) leaders.push_back(tg.frame_base + k);
+        FRS_HIP(ctx->loose_assign.ensure(sizeof(int8_t) * (size_t)nframes + 64));
+        FRS_HIP(ctx->loose_lead.ensure(sizeof(int64_t) * leaders.size()));
+        FRS_HIP(hipMemcpyAsync(ctx->loose_lead.ptr, leaders.data(), sizeof(int64_t) * leaders.size(),
+                               hipMemcpyHostToDevice, st));
+        dloose = ctx->loose_assign.as<int8_t>();
+        const int64_t *dlead = ctx->loose_lead.as<int64_t>();
+        if (P.bps > 16)
+            k_encode_frames<DT, true, int64_t><<<(unsigned)leaders.size(), kEncThreads, 0, st>>>(
+                raster, P, dtiles, dnorms, dana, dslots, dfb, err_flag, dlead, dcand, dloose, 1);
+        else
+            k_encode_frames<DT, true><<<(unsigned)leaders.size(), kEncThreads, 0, st>>>(
+                raster, P, dtiles, dnorms, dana, dslots, dfb, err_flag, dlead, dcand, dloose, 1);
+        FRS_HIP(hipStreamSynchronize(st));  // (the leader list's host vector goes out of scope)
+    }
     if (stereo && P.bps > 16)
         k_encode_frames<DT, true, int64_t><<<(unsigned)nframes, kEncThreads, 0, st>>>(raster, P, dtiles, dnorms, dana,
-                                                                                     dslots, dfb, err_flag, nullptr);
+                                                                                     dslots, dfb, err_flag, nullptr,
+                                                                                     dcand, dloose, 0);
     else if (stereo)
         k_encode_frames<DT, true><<<(unsigned)nframes, kEncThreads, 0, st>>>(raster, P, dtiles, dnorms, dana, dslots,
-                                                                             dfb, err_flag, nullptr);
+                                                                             dfb, err_flag, nullptr, dcand, dloose, 0);
     else
         k_encode_frames<DT><<<(unsigned)nframes, kEncThreads, 0, st>>>(raster, P, dtiles, dnorms, dana, dslots, dfb,
-                                                                       err_flag, nullptr);
+                                                                       err_flag, nullptr, dcand, nullptr, 0);
     prof_end(ctx, "encode", ev);
     // 4. offsets (frame_off[nframes] = total)
     k_scan_sizes<<<1, kScanThreads, 0, st>>>(ctx->frame_bytes.as<int64_t>(), ctx->frame_off.as<int64_t>(), nframes);

@@ -101,6 +101,10 @@ struct frs_ctx {
     // while range k - 1 is encoded on `stream` (the analysis' min/max bursts and last-round tail overlap the encoder)
     // role-split analysis (k_analyze_v5: stats producers and sums consumers inside each work-group); $FRS_ANA_V5
     DevBuf ana_ctr;       // its global tile counter
+    // subdivide_tukey levels (6..8): LPC candidates per coded signal, the tukey(0.5 / parts) window; loose mid/side:
+    // per-frame assignment of the group leaders and the leader frame list
+    DevBuf lpc_cand, window_hi, loose_assign, loose_lead;
+    int window_hi_bs = 0, window_hi_parts = 0;
     bool ana_v5 = false;
     int enc_split = 1;  // (2-4 measured slower on C4: both kernels are issue-bound, so sharing the CUs gains nothing)
     hipStream_t aux_stream = nullptr;

@@ -78,10 +78,9 @@ def test_convert_errors_exit_1(golden, tmp_path):
     out.write_bytes(b"x")
     r = runner.invoke(app, ["convert", str(golden / "sample_rgb.tif"), "-o", str(out)])
     assert r.exit_code == 1 and "already exists" in r.output
-    # levels 6..8 (subdivide_tukey) are rejected explicitly (before any GPU work); 0..5 are implemented
-    r = runner.invoke(app, ["convert", str(golden / "sample_rgb.tif"), "-o", str(tmp_path / "c7.flac"), "-c", "7"])
-    assert r.exit_code == 1 and "levels 0..5" in r.output
+    # -c 0..8 (cli.py:36-37): out-of-range levels are refused by the option's range before any work
     assert runner.invoke(app, ["convert", str(golden / "sample_rgb.tif"), "-c", "9"]).exit_code != 0  # typer range
+    assert runner.invoke(app, ["convert", str(golden / "sample_rgb.tif"), "-c", "-1"]).exit_code != 0
 
 
 # ------------------------------------------------------------------------------------------------ create-streaming

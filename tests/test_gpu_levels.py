@@ -1,10 +1,12 @@
-"""Compression levels 0..5 on the GPU encoder: bytes equal the oracle's restatement of libFLAC's level table
-(docs/sonos-pyflac.txt:6926-6931; parity UNPINNED for levels other than 5, see tests/test_levels.py).
+"""Compression levels 0..8 on the GPU encoder: bytes equal the oracle's restatement of libFLAC's level table
+(docs/sonos-pyflac.txt:6926-6934; parity UNPINNED for levels other than 5, see tests/test_levels.py).
 
-Levels other than 5 run the generic kernels (k_analyze + k_encode_frames with EncodeParams.max_lpc / max_po); the
-fast kernels hard-code level 5's search and are not selected.  Covered: mono, two channels (independent at 0 / 3,
-exhaustive mid/side at 2 / 5), three channels, a 32-bit stream, the spatial {-1, 0, 1} mode, partial last frames,
-the file-level convert / convert --spatial paths, and the rejections (levels 6..8; 1 and 4 on two bands).
+Levels other than 5 run the generic kernels (k_analyze + k_encode_frames with EncodeParams.max_lpc / max_po; at 6..8
+k_analyze_lpc_hi's per-window LPC candidates of the subdivide_tukey apodizations, LPC order up to 12 and partition
+order 6; at 1 / 4 on two channels loose mid/side: a leader pass per group of frames, then the coding pass); the fast
+kernels hard-code level 5's search and are not selected.  Covered: mono, two channels (independent at 0 / 3,
+exhaustive mid/side at 2 / 5 / 6..8, loose at 1 / 4), three channels, a 32-bit stream, the spatial {-1, 0, 1} mode,
+partial last frames, the file-level convert / convert --spatial paths, and the level range check.
 """
 import numpy as np
 import pytest
@@ -54,7 +56,7 @@ def test_levels_streaming_tiles_match_oracle(gpu_ctx):
     """Mono tiles (the create-streaming shape, 16-bit) with edge tiles at every level: per-tile oracle streams."""
     band = _raster(1, 700, 650, 31)[0]
     T = 256
-    for lv in range(6):
+    for lv in range(9):
         d = gpu_ctx.make_desc(700, 650, band.dtype, tile_h=T, tile_w=T, sample_rate=44100, bits_per_sample=16,
                               compression_level=lv)
         arena, off, mn, mx, bps = gpu_ctx.encode_tiles_host(band, d)
@@ -71,7 +73,7 @@ def test_levels_spatial_mode_matches_oracle(gpu_ctx):
     arr = (_raster(2, 80, 100, 41) // 64).astype(np.int16)
     B, H, W = arr.shape
     pcm = O.normalize_spatial(np.ascontiguousarray(arr.reshape(B, -1).T))
-    for lv in (0, 2, 3, 5):
+    for lv in range(9):
         d = gpu_ctx.make_desc(H, W, arr.dtype, nbands=B, tile_h=H, tile_w=W, sample_rate=44100, bits_per_sample=16,
                               norm_mode=1, compression_level=lv)
         arena, off, mn, mx, bps = gpu_ctx.encode_tiles_host(arr, d)
@@ -87,7 +89,7 @@ def test_level_files_match_oracle_pipeline(gpu_ctx, tmp_path):
     geotiff.write(src, arr, t, 32636)
     r = geotiff.read(src)
     conv = RasterFLACConverter(gpu_ctx)
-    for lv in (0, 3):
+    for lv in (0, 3, 7):
         out = tmp_path / f"one_c{lv}.flac"
         conv.tiff_to_flac(src, out, compression_level=lv)
         ref, _ = P.plain_convert(r.data, list(r.transform), r.crs_string, r.nodata, embed=True, level=lv)
@@ -101,10 +103,29 @@ def test_level_files_match_oracle_pipeline(gpu_ctx, tmp_path):
     assert sp.read_bytes() == P.raw_frames(r.data, list(r.transform), r.crs_string, 64, "2026-01-01", 0, level=3)
 
 
-def test_unsupported_levels_rejected_by_abi(gpu_ctx):
-    arr = _raster(2, 64, 64, 61)
-    for lv, ch in ((1, 2), (4, 2), (6, 1), (8, 2)):
-        d = gpu_ctx.make_desc(64, 64, arr.dtype, nbands=ch, tile_h=64, tile_w=64, sample_rate=44100,
-                              bits_per_sample=16, compression_level=lv)
+def test_level_range_checked_by_abi(gpu_ctx):
+    arr = _raster(1, 64, 64, 61)
+    for lv in (-1, 9):
+        d = gpu_ctx.make_desc(64, 64, arr.dtype, tile_h=64, tile_w=64, sample_rate=44100, bits_per_sample=16,
+                              compression_level=lv)
         with pytest.raises(_native.FrsError):
-            gpu_ctx.encode_tiles_host(np.ascontiguousarray(arr[:ch]), d)
+            gpu_ctx.encode_tiles_host(arr[0], d)
+
+
+def test_high_levels_and_loose_stereo_long_streams(gpu_ctx):
+    """Many frames per stream: level 8's nine windows per signal, and the loose mid/side schedule of levels 1 / 4
+    over several four-frame groups (the leader pass), against the oracle."""
+    n = 26 * 4096 + 777
+    t = np.arange(n)
+    rng = np.random.default_rng(8)
+    L = 3000 * np.sin(t / 200.0) + rng.normal(0, 30, n)
+    R = np.where((t // 4096) % 6 < 3, L + rng.normal(0, 2, n), rng.normal(0, 3000, n))
+    x = np.clip(np.stack([L, R], axis=1), -32768, 32767).astype(np.int16)
+    H, W = 1, n
+    arr = np.ascontiguousarray(x.T.reshape(2, H, W))
+    pcm, omn, omx, obps = O.normalize(x)
+    for lv in (1, 4, 6, 8):
+        d = gpu_ctx.make_desc(H, W, arr.dtype, nbands=2, tile_h=H, tile_w=W, sample_rate=44100, bits_per_sample=16,
+                              compression_level=lv)
+        arena, off, mn, mx, bps = gpu_ctx.encode_tiles_host(arr, d)
+        assert arena[:off[-1]].tobytes() == O.encode_frames(pcm, obps, 44100, level=lv), lv
