@@ -215,6 +215,9 @@ def main():
         result["batched_decode"] = batched_decode(ctx, arena, off, mn, mx, rows, W, T)
         result["sentinel2"] = sentinel2(ctx)
         result["convert_multiband"] = convert_multiband(ctx)
+        result["convert_2band"] = convert_2band(ctx)
+        result["raw_frames"] = raw_frames(ctx)
+        result["convert_level8"] = convert_level8(ctx)
         result["end_to_end"] = end_to_end(ctx, raster, arena, off, rows, W, T, args)
     if rank == 0 and world == 1 and not args.no_cpu:  # (the CPU baseline is an N = 1 figure)
         result["cpu_baseline"] = cpu_baseline(ctx, raster, rows, W, T, off, arena, args)
@@ -426,6 +429,69 @@ def convert_multiband(ctx, steps=3):
             "kernels_ms": {k: v for k, v in kern.items() if v > 0},
             "decode": {"ms": round(ddt * 1e3, 3), "Mpixels_s": round(H * W / ddt / 1e6, 1), "lossless": lossless,
                        "kernels_ms": {k: v for k, v in dkern.items() if v > 0}}}
+
+
+def _timed_encode(ctx, buf, d, steps):
+    """Device-resident encode of descriptor d: warm-up, then the mean of `steps` timed calls and the kernel times."""
+    arena = ctx.alloc(ctx.arena_bound(d))
+    ctx.encode_tiles_device(buf.ptr, d, arena)
+    ctx.profile(True)
+    ctx.profile_reset()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        off, _, _, _ = ctx.encode_tiles_device(buf.ptr, d, arena)
+    ctx.sync()
+    dt = (time.perf_counter() - t0) / steps
+    ctx.profile(False)
+    kern = {k: round(ctx.profile_avg_ms(k), 4) for k in ("stats", "analyze", "partial", "encode", "assemble", "compact")}
+    arena.close()
+    return dt, int(off[-1]), {k: v for k, v in kern.items() if v > 0}
+
+
+def convert_2band(ctx, steps=3):
+    """Plain `convert` of a 16384 x 16384 x 2 int16 raster as ONE two-channel stream (converter.py:185-216): libFLAC
+    level 5's exhaustive mid/side search (L, R, M, S coded per frame, the cheapest assignment kept) -- the generic
+    kernels, device-resident."""
+    B, H, W = 2, 16384, 16384
+    buf = ctx.alloc(B * H * W * 2)
+    ctx.synth_raster(buf, B, H, W, seed=6)
+    d = ctx.make_desc(H, W, np.int16, nbands=B, tile_h=H, tile_w=W, sample_rate=44100, bits_per_sample=16)
+    dt, nbytes, kern = _timed_encode(ctx, buf, d, steps)
+    buf.close()
+    return {"raster": f"{H}x{W}x{B} int16", "streams": 1, "channels": B, "ms_per_step": round(dt * 1e3, 3),
+            "Mpixels_s": round(H * W / dt / 1e6, 1), "compressed_bytes": nbytes, "kernels_ms": kern,
+            "path": "generic kernels (k_analyze L/R/M/S + k_encode_frames, frame per work-group)"}
+
+
+def raw_frames(ctx, steps=3):
+    """`convert --spatial` (spatial_encoder.py:136-294, the C1 recipe) at C3 size: a 16384 x 16384 int16 band in 256 x
+    256 tiles, each a 32-bit stream of the {-1, 0, 1} samples pyflac makes of the float normalisation -- the generic
+    kernels (32-bit streams), device-resident."""
+    H = W = 16384
+    T = 256
+    buf = ctx.alloc(H * W * 2)
+    ctx.synth_raster(buf, 1, H, W, seed=7)
+    d = ctx.make_desc(H, W, np.int16, tile_h=T, tile_w=T, sample_rate=44100, bits_per_sample=24, norm_mode=1)
+    dt, nbytes, kern = _timed_encode(ctx, buf, d, steps)
+    buf.close()
+    return {"raster": f"{H}x{W} int16", "tile_size": T, "tiles": (H // T) * (W // T), "bps": 32,
+            "ms_per_step": round(dt * 1e3, 3), "Mpixels_s": round(H * W / dt / 1e6, 1), "compressed_bytes": nbytes,
+            "kernels_ms": kern, "path": "generic kernels (32-bit streams)"}
+
+
+def convert_level8(ctx, steps=2):
+    """`convert -c 8` of a 4096 x 4096 x 3 int16 raster (one 3-channel stream): subdivide_tukey(3) -- nine LPC
+    windows per subframe, LPC order up to 12, partition order up to 6 -- on the generic kernels, device-resident."""
+    B, H, W = 3, 4096, 4096
+    buf = ctx.alloc(B * H * W * 2)
+    ctx.synth_raster(buf, B, H, W, seed=8)
+    d = ctx.make_desc(H, W, np.int16, nbands=B, tile_h=H, tile_w=W, sample_rate=44100, bits_per_sample=16,
+                      compression_level=8)
+    dt, nbytes, kern = _timed_encode(ctx, buf, d, steps)
+    buf.close()
+    return {"raster": f"{H}x{W}x{B} int16", "level": 8, "ms_per_step": round(dt * 1e3, 3),
+            "Mpixels_s": round(H * W / dt / 1e6, 1), "compressed_bytes": nbytes, "kernels_ms": kern}
 
 
 def end_to_end(ctx, raster, arena, off_dev, rows, W, T, args):

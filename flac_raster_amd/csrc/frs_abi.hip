@@ -105,6 +105,7 @@ int frs_ctx_create(int device, frs_ctx **out) {
     const char *dl = getenv("FRS_DECODE_LANE");
     ctx->decode_lane = dl ? (dl[0] == '1' ? 1 : 0) : -1;
     if (const char *av = getenv("FRS_ANA_V5")) ctx->ana_v5 = av[0] == '1';
+    if (const char *p2 = getenv("FRS_PIPE2")) ctx->pipe2 = p2[0] == '1';
     const char *es = getenv("FRS_ENC_SPLIT");
     if (es) ctx->enc_split = std::max(1, std::min(8, atoi(es)));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {

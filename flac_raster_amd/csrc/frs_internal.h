@@ -106,6 +106,7 @@ struct frs_ctx {
     DevBuf lpc_cand, window_hi, loose_assign, loose_lead;
     int window_hi_bs = 0, window_hi_parts = 0;
     bool ana_v5 = false;
+    bool pipe2 = false;   // $FRS_PIPE2: the pipelined decoder's Rice decode by a resolver + two builder waves
     int enc_split = 1;  // (2-4 measured slower on C4: both kernels are issue-bound, so sharing the CUs gains nothing)
     hipStream_t aux_stream = nullptr;
     hipEvent_t split_ev[9] = {};

@@ -234,7 +234,21 @@ PWT2 = chain(PWT,
     __syncthreads();"""),
              PWT2_LOOP)
 
-VARIANTS = {"base": lambda s: s, "pwt": PWT, "crc2": CRC2, "pwt_crc2": chain(PWT, CRC2), "pwt2": PWT2, "pwt2_crc2": chain(PWT2, CRC2)}
+# early: the previous frame's look-back + store + buffer re-zero right after this frame's sample loads are issued (its
+#        latency hides behind them) instead of between this frame's phases A and B
+EARLY = chain(
+    sub("""        ch.load(base, P.row_stride, g.w, row, (int)(sl0 - row * (uint32_t)g.w), (g.w % 64) == 0 ? P.vec_ok : 0, 64);
+        if (sizeof(T) == 2 && tn.mode == kNormLut && w == 0) {  // (wave-uniform) the common case""",
+        """        ch.load(base, P.row_stride, g.w, row, (int)(sl0 - row * (uint32_t)g.w), (g.w % 64) == 0 ? P.vec_ok : 0, 64);
+        if constexpr (!SUB)
+            if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
+        if (sizeof(T) == 2 && tn.mode == kNormLut && w == 0) {  // (wave-uniform) the common case"""),
+    sub("""    if constexpr (!SUB)
+        if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
+    __builtin_amdgcn_s_setprio(0);""", """    __builtin_amdgcn_s_setprio(0);"""),
+)
+
+VARIANTS = {"base": lambda s: s, "pwt": PWT, "crc2": CRC2, "pwt_crc2": chain(PWT, CRC2), "pwt2": PWT2, "pwt2_crc2": chain(PWT2, CRC2), "early": EARLY, "early_crc2": chain(EARLY, CRC2)}
 
 if __name__ == "__main__":
     for name in sys.argv[1:] or list(VARIANTS):
