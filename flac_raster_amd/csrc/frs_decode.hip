@@ -2532,6 +2532,46 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
                     for (int i0 = 0; i0 < bs && take; i0 += 8) {
                         br.top_up();
                         uint32_t ob[8];
+                        // the general per-sample body only where some lane needs it: warm-up samples (step 0), the
+                        // block's end, a partition boundary of a Rice-coded subframe inside this step
+                        const bool gen = i0 == 0 || i0 + 8 > bs || (!raw && !cst && part_end < i0 + 8);
+                        if (!__ballot(gen)) {
+#pragma unroll
+                            for (int u = 0; u < 8; u++) {
+                                // one code per sample: VERBATIM = sbps raw bits, Rice = unary run + stop bit + k low
+                                // bits, CONSTANT = nothing read
+                                const int z = br.c ? __builtin_clzll(br.c) : 64;
+                                const int pre = (raw || cst) ? 0 : z + 1;
+                                const int kk = raw ? sbps : (cst ? 0 : k);
+                                const int used = pre + kk;
+                                uint32_t v;
+                                if (used > br.n) {  // (rare: a Rice code longer than the >= 33 cached bits)
+                                    const uint32_t q = br.unary();
+                                    v = (q << k) | br.bits(k);
+                                } else {
+                                    const uint64_t tb = pre >= 64 ? 0ull : (br.c << pre);
+                                    const uint32_t low = kk ? (uint32_t)(tb >> (64 - kk)) : 0u;
+                                    br.c = used >= 64 ? 0ull : (br.c << used);
+                                    br.n -= used;
+                                    br.ensure();
+                                    v = raw ? low : (((uint32_t)z << k) | low);
+                                }
+                                const int32_t r = raw ? ((int32_t)(v << (32 - sbps)) >> (32 - sbps))
+                                                      : (int32_t)((v >> 1) ^ (uint32_t)(-(int32_t)(v & 1)));
+                                int32_t pred = 0;
+#pragma unroll
+                                for (int m = 0; m < 8; m++) pred += __mul24(cq[m], R[(u + 7 - m) & 7]);
+                                const int32_t x = cst ? cval : r + (pred >> shift);
+                                R[u] = x;
+                                const int32_t xo = (int32_t)((uint32_t)x << w);
+                                if constexpr (OUT == kOutAny) {
+                                    dn_store(dout, obase + i0 + u, xo, dnp);
+                                    ob[u] = 0;
+                                } else {
+                                    ob[u] = dn_bits_t<OUT>(dout, xo, dnp);
+                                }
+                            }
+                        } else
 #pragma unroll
                         for (int u = 0; u < 8; u++) {
                             const int i = i0 + u;
