@@ -2363,11 +2363,15 @@ struct V5Slot {
     int free;  // item number the slot may take next
     int pad;
 };
-template <int DT>
-__global__ void __launch_bounds__(512, 2) k_analyze_v5(const typename Elem<DT>::T *raster, EncodeParams P,
+// NC consumer and NP producer waves per work-group (NC a multiple of NP: each producer posts NC / NP end markers);
+// dbg (optional, $FRS_ANA_DBG): wave-cycle totals [consumer wait, consumer sums, items, producer stats, producer slot
+// wait, items].
+template <int DT, int NC = 4, int NP = 4, bool DBG = false>
+__global__ void __launch_bounds__(64 * (NC + NP), 4) k_analyze_v5(const typename Elem<DT>::T *raster, EncodeParams P,
                                                       const TileGeom *tiles, TileNorm *norms, int16_t *luts,
                                                       const float *__restrict__ window, SubAnalysis *out, int ntiles,
-                                                      int *tile_ctr, int *err) {
+                                                      int *tile_ctr, int *err, unsigned long long *dbg = nullptr) {
+    static_assert(NC % NP == 0 && NC + NP <= kV5Slots, "end markers / slots");
     static_assert(sizeof(typename Elem<DT>::T) == 2 && !Elem<DT>::is_float, "16-bit samples");
     __shared__ int16_t slut[kV5Slots][kLutCap];
     __shared__ V5Slot slot[kV5Slots];
@@ -2397,10 +2401,20 @@ __global__ void __launch_bounds__(512, 2) k_analyze_v5(const typename Elem<DT>::
         if (lane == 0) i = atomicAdd(&ctr[k], 1);
         return __builtin_amdgcn_readfirstlane(i);
     };
-    if (wave >= 4) {
+    uint64_t tw = 0, tb = 0, nit = 0;  // (dbg) wait cycles, busy cycles, items
+    auto dbg_flush = [&](int base) {
+        if (DBG && lane == 0) {
+            atomicAdd(&dbg[base], (unsigned long long)tw);
+            atomicAdd(&dbg[base + 1], (unsigned long long)tb);
+            atomicAdd(&dbg[base + 2], (unsigned long long)nit);
+        }
+    };
+    if (wave >= NC) {
         // ---- producer
+        int ends_left = NC / NP;  // end markers this producer posts once the tiles are out
         while (true) {
             const int i = take(0);
+            uint64_t t0 = DBG ? __builtin_amdgcn_s_memtime() : 0;
             V5Slot &sl = slot[i % kV5Slots];
             int t;
             TileNorm tn;
@@ -2417,7 +2431,14 @@ __global__ void __launch_bounds__(512, 2) k_analyze_v5(const typename Elem<DT>::
                 const int nfull = g.nframes - (g.partial ? 1 : 0);
                 if ((tn.mode == kNormLut || tn.mode == kNormZero) && nfull > 0) break;
             }
+            uint64_t t1 = DBG ? __builtin_amdgcn_s_memtime() : 0;
+            tb += t1 - t0;
             if (!lds_wait(&sl.free, i)) return;  // the slot's previous item has been consumed
+            if (DBG) {
+                const uint64_t t2 = __builtin_amdgcn_s_memtime();
+                tw += t2 - t1;
+                t1 = t2;
+            }
             if (t < ntiles && tn.mode == kNormLut) {
                 int16_t *glut = luts + (int64_t)t * kLutCap;
                 int16_t *wl = slut[i % kV5Slots];
@@ -2434,16 +2455,29 @@ __global__ void __launch_bounds__(512, 2) k_analyze_v5(const typename Elem<DT>::
             }
             __builtin_amdgcn_s_waitcnt(0xC07F);  // the slot's LUT and parameters have landed in LDS
             if (lane == 0) __hip_atomic_store(&sl.seq, i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (t >= ntiles) return;  // end marker posted
+            if (DBG) {
+                tb += __builtin_amdgcn_s_memtime() - t1;
+                nit++;
+            }
+            if (t >= ntiles && --ends_left == 0) {  // end markers posted
+                dbg_flush(3);
+                return;
+            }
         }
     }
     // ---- consumer
     while (true) {
         const int i = take(1);
         V5Slot &sl = slot[i % kV5Slots];
+        const uint64_t t0 = DBG ? __builtin_amdgcn_s_memtime() : 0;
         if (!lds_wait(&sl.seq, i)) return;
+        const uint64_t t1 = DBG ? __builtin_amdgcn_s_memtime() : 0;
+        tw += t1 - t0;
         const int t = sl.tile;
-        if (t < 0) return;
+        if (t < 0) {
+            dbg_flush(0);
+            return;
+        }
         const TileNorm tn = sl.tn;
         const TileGeom g = tiles[t];
         const typename Elem<DT>::T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
@@ -2469,6 +2503,10 @@ __global__ void __launch_bounds__(512, 2) k_analyze_v5(const typename Elem<DT>::
         __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's reads of the slot are done
         if (lane == 0) __hip_atomic_store(&sl.free, i + kV5Slots, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (live) out[f] = analysis_finish(acc, or_acc, n, P, ft);
+        if (DBG) {
+            tb += __builtin_amdgcn_s_memtime() - t1;
+            nit++;
+        }
     }
 }
 
@@ -4094,14 +4132,33 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                         // role-split analysis: producers (tile stats + LUT) and consumers (sums) in each work-group
                         FRS_HIP(ctx->ana_ctr.ensure(64));
                         FRS_HIP(hipMemsetAsync(ctx->ana_ctr.ptr, 0, sizeof(int), ast));
-                        static int occ5 = 0;  // (per instantiation)
-                        if (occ5 == 0)
-                            FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ5, k_analyze_v5<DT>, 512, 0));
-                        const int64_t g5 = std::min<int64_t>((int64_t)std::max(1, occ5) * ctx->num_cus,
-                                                             ((int64_t)ntiles + 3) / 4);
-                        k_analyze_v5<DT><<<(unsigned)g5, 512, 0, ast>>>(raster, P, dtiles, dnorms,
-                                                                        ctx->luts.as<int16_t>(), ctx->window.as<float>(),
-                                                                        dana, ntiles, ctx->ana_ctr.as<int>(), err_flag);
+                        unsigned long long *dbg = nullptr;
+                        if (ctx->ana_dbg) {
+                            FRS_HIP(ctx->ana_dbgbuf.ensure(64));
+                            FRS_HIP(hipMemsetAsync(ctx->ana_dbgbuf.ptr, 0, 64, ast));
+                            dbg = ctx->ana_dbgbuf.as<unsigned long long>();
+                        }
+                        const int64_t g5 = std::min<int64_t>(2 * (int64_t)ctx->num_cus, ((int64_t)ntiles + 3) / 4);
+                        auto v5 = [&](auto kern) {
+                            kern<<<(unsigned)g5, 512, 0, ast>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
+                                                               ctx->window.as<float>(), dana, ntiles,
+                                                               ctx->ana_ctr.as<int>(), err_flag, dbg);
+                        };
+                        if (ctx->ana_v5 == 2) {
+                            if (dbg) v5(k_analyze_v5<DT, 6, 2, true>);
+                            else v5(k_analyze_v5<DT, 6, 2>);
+                        } else {
+                            if (dbg) v5(k_analyze_v5<DT, 4, 4, true>);
+                            else v5(k_analyze_v5<DT, 4, 4>);
+                        }
+                        if (dbg) {
+                            unsigned long long h[8];
+                            FRS_HIP(hipMemcpyAsync(h, dbg, 64, hipMemcpyDeviceToHost, ast));
+                            FRS_HIP(hipStreamSynchronize(ast));
+                            fprintf(stderr, "ana_v5 dbg: cons wait %.3g busy %.3g items %llu | prod busy %.3g wait %.3g "
+                                            "items %llu (wave-cycles)\n", (double)h[0], (double)h[1], h[2], (double)h[3],
+                                    (double)h[4], h[5]);
+                        }
                     }
                 } else if (fuse_stats) {
                     if constexpr (sizeof(T) == 2)

@@ -105,7 +105,9 @@ struct frs_ctx {
     // per-frame assignment of the group leaders and the leader frame list
     DevBuf lpc_cand, window_hi, loose_assign, loose_lead;
     int window_hi_bs = 0, window_hi_parts = 0;
-    bool ana_v5 = false;
+    int ana_v5 = 0;       // 1: 4 consumer + 4 producer waves per work-group, 2: 6 + 2
+    bool ana_dbg = false; // $FRS_ANA_DBG: k_analyze_v5 wave-cycle totals to stderr
+    DevBuf ana_dbgbuf;
     bool pipe2 = false;   // $FRS_PIPE2: the pipelined decoder's Rice decode by a resolver + two builder waves
     int enc_split = 1;  // (2-4 measured slower on C4: both kernels are issue-bound, so sharing the CUs gains nothing)
     hipStream_t aux_stream = nullptr;
