@@ -2807,6 +2807,74 @@ __device__ inline void lut_gather_pairs(const uint32_t *w, const int16_t *lut, i
 
 __device__ inline uint32_t zigzag(int32_t r) { return ((uint32_t)r << 1) ^ (uint32_t)(r >> 31); }
 
+// ---- hand-off between the work-groups of one launch (k_fused_v6): the analysis wave stores a tile's parameters,
+// LUT and frame analyses with sc1 stores (relaxed agent-scope atomics), waits for them (vmcnt(0)) and sets the
+// tile's flag to the launch's epoch with an sc1 store; every read of those bytes on the encoder side is an sc1 load
+// behind a matched sc1 poll of the flag (MI355X_MICROARCH.md, inter-workgroup visibility: the sc1 form, no L1 copy).
+struct TileHand {
+    TileNorm tn;
+    uint8_t pad[128 - sizeof(TileNorm)];  // the LUT starts on a line of its own
+    int16_t lut[kLutCap];
+};
+static_assert(sizeof(TileNorm) % 4 == 0 && sizeof(SubAnalysis) % 4 == 0 && sizeof(TileNorm) <= 128, "sc1 units");
+// a frame's analysis in the hand-off: one per 128-B line (frames of two tiles never share a line)
+constexpr int kAnaHandStride = 128;
+static_assert(sizeof(SubAnalysis) <= kAnaHandStride, "analysis line");
+__device__ inline SubAnalysis *ana_hand(SubAnalysis *base, int64_t f) {
+    return reinterpret_cast<SubAnalysis *>(reinterpret_cast<char *>(base) + f * kAnaHandStride);
+}
+template <typename S> using Sc1Unit = std::conditional_t<sizeof(S) % 8 == 0, uint64_t, uint32_t>;
+template <typename S> __device__ inline void sc1_store(S *dst, const S &v) {
+    using U = Sc1Unit<S>;
+    const U *src = reinterpret_cast<const U *>(&v);
+    U *d = reinterpret_cast<U *>(dst);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(S) / sizeof(U)); i++)
+        __hip_atomic_store(d + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename S> __device__ inline S sc1_load(const S *src) {
+    using U = Sc1Unit<S>;
+    S v;
+    U *d = reinterpret_cast<U *>(&v);
+    U *q = reinterpret_cast<U *>(const_cast<S *>(src));
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(S) / sizeof(U)); i++)
+        d[i] = __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+}
+// the same for a wave-uniform address, the value made wave-uniform (SGPRs, not one VGPR per dword)
+template <typename S> __device__ inline S sc1_load_uni(const S *src) {
+    static_assert(sizeof(S) % 4 == 0, "dwords");
+    S v;
+    uint32_t *d = reinterpret_cast<uint32_t *>(&v);
+    uint32_t *q = reinterpret_cast<uint32_t *>(const_cast<S *>(src));
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(S) / 4); i++)
+        d[i] = (uint32_t)__builtin_amdgcn_readfirstlane(
+            (int)__hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    return v;
+}
+// (wave-uniform) poll a tile's flag until it holds this launch's epoch; the analysis of every tile is claimed by a
+// running wave before any encoder work-group starts, so the wait is bounded by one tile's analysis.  Flags sit one
+// per 128-B line (kFlagStride) and pollers back off to ~3 us: a small job's dozens of encoder work-groups polling a
+// few flags on one line flooded that line's memory channel and stalled the analysis waves' own loads behind them.
+constexpr int kFlagStride = 32;
+__device__ inline void wait_tile(const uint32_t *flags, int tile, uint32_t epoch, int *err) {
+    uint32_t *flag = const_cast<uint32_t *>(flags) + (size_t)tile * kFlagStride;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
+    for (int spin = 0;; spin++) {
+        const uint32_t v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__builtin_amdgcn_readfirstlane(v) == epoch) return;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s (a tile's analysis takes ~1 ms)
+            if ((threadIdx.x & 63) == 0) atomicOr(err, 32);
+            return;
+        }
+        if (spin < 8) __builtin_amdgcn_s_sleep(8);
+        else if (spin < 32) __builtin_amdgcn_s_sleep(32);
+        else __builtin_amdgcn_s_sleep(127);
+    }
+}
+
 struct PendingFrame {  // a frame whose bytes sit in the wave's bit buffer, offset not yet resolved
     int64_t f = -1;
     uint64_t fbytes = 0;
@@ -3003,19 +3071,21 @@ __device__ inline uint32_t fixed_lane_sum(const uint32_t *E, bool l0) {
 // SUB = true (multi-channel streams, >= 3 independent channels): the wave codes ONE subframe (channel chn of frame f)
 // from bit 0 of its buffer -- no frame header, no look-back, no CRC -- and stores its words to sub_slots[f * nch +
 // chn] with its bit length in sub_bits; k_mc_assemble joins a frame's subframes behind the frame header.
-template <int DT, bool SUB = false>
+template <int DT, bool SUB = false, bool COH = false>
 __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const EncodeParams &P,
                                        const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
                                        const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap, int64_t *frame_off,
                                        uint64_t *status, int *err, EncV3Shared &S, int want, int64_t f, int lane,
                                        const int32_t *ftile, PendingFrame &prev, const uint4 *hdr_tab, int hdr_n,
                                        const uint32_t *pslots, const int64_t *pbytes, int chn = 0,
-                                       uint32_t *sub_slots = nullptr, int32_t *sub_bits = nullptr) {
+                                       uint32_t *sub_slots = nullptr, int32_t *sub_bits = nullptr,
+                                       const TileHand *hand = nullptr, const uint32_t *flags = nullptr,
+                                       uint32_t epoch = 0) {
     using T = typename Elem<DT>::T;
     uint32_t *fbuf = S.bits[threadIdx.x >> 6];
     const int t = ftile[f];
     const TileGeom g = tiles[t];
-    if (!SUB && g.partial && f - g.frame_base == g.nframes - 1) {
+    if (!SUB && !COH && g.partial && f - g.frame_base == g.nframes - 1) {
         // (wave-uniform) the tile's partial last frame: already coded and sealed by the generic kernels, so it
         // only joins the look-back chain -- publish its size, finish the previous frame, and stage its bytes in
         // the bit buffer for resolve_and_store like a frame coded here
@@ -3042,7 +3112,13 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         prev.map = M;
         return;
     }
-    TileNorm tn = norms[t];
+    TileNorm tn;
+    if constexpr (COH) {  // (the ticket's tile was polled by wave 0 before the work-group barrier)
+        if (t != want) wait_tile(flags, t, epoch, err);
+        tn = sc1_load_uni(&hand[t].tn);
+    } else {
+        tn = norms[t];
+    }
     // the WG's LDS LUT belongs to tile `want`; a frame of another tile takes the exact division instead
     if (t != want && tn.mode == kNormLut) tn.mode = kNormSlow;
     const int16_t *lut = S.lut;
@@ -3054,7 +3130,8 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     const int64_t s0 = fk * kMaxBlock;
     constexpr int n = kMaxBlock;
     const int64_t sub = SUB ? f * P.nch + chn : f;
-    const SubAnalysis A = ana[sub];
+    const SubAnalysis *asub = COH ? ana_hand(const_cast<SubAnalysis *>(ana), sub) : ana + sub;
+    const SubAnalysis A = COH ? sc1_load_uni(asub) : *asub;
     const int w = A.wasted;
     const int sbps = 16 - w;
     const T *base = raster + (int64_t)(P.band0 + chn) * P.band_stride + g.r0 * P.row_stride + g.c0;
@@ -3434,7 +3511,10 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         w01 = (i >> 1) == 2 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 2], 0) : w01;
         w01 = (i >> 1) == 3 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 3], 0) : w01;
         const uint32_t xi = (i & 1) ? (w01 >> 16) : (w01 & 0xFFFFu);
-        const int32_t qi = ana[sub].q[i];  // (a lane-indexed load: a select chain over A.q costs registers)
+        // (a lane-indexed load: a select chain over A.q costs registers)
+        const int32_t qi = COH ? __hip_atomic_load(const_cast<int32_t *>(&asub->q[i]), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)
+                               : asub->q[i];
         const bool warm = lane < 8 && i < o, coef = type == 3 && lane >= 8 && lane < 16 && i < o;
         if (warm)
             lds_put_bits2(fbuf, M, pos0 + (uint32_t)i * sbps, xi & ((1u << sbps) - 1u), sbps);
@@ -3604,6 +3684,134 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
     }
     if constexpr (!SUB)
         if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
+}
+
+// ------------------------------------------------------------------------------ k_fused_v6
+// The analysis and the encoder of a 16-bit mono job in ONE persistent launch.  Separate launches leave the chip
+// idle at the analysis' end: a tile's 64 frames are 64 sequential fp64 sums on one wave (~0.4 ms), 6241 C4 tiles on
+// 3-4 K wave slots take two rounds, and the second is a third full.  Here every work-group first claims tiles from a
+// global counter (stats, parameters, LUT, the k_analyze_v3 sums: phase 1) and, once none is left, joins the encoder
+// (k_encode_v3's ticket loop: phase 2), so the last tiles' sums run beside the first frames' coding.  Frames are coded
+// in stream order and a frame's tile was claimed before any encoder started, so an encoder waits at most for one
+// tile's analysis (flag polled per tile; the hand-off protocol above).  No wave of phase 1 waits on anything.
+template <int DT>
+__global__ void __launch_bounds__(256, 3) k_fused_v6(const typename Elem<DT>::T *raster, EncodeParams P,
+                                                 const TileGeom *tiles, TileNorm *norms, TileHand *hand,
+                                                 const float *__restrict__ window, SubAnalysis *ana, uint8_t *arena,
+                                                 int64_t arena_cap, int64_t *frame_off, uint64_t *status,
+                                                 int *ticket_ctr, int *err, const int32_t *__restrict__ ftile,
+                                                 const uint4 *__restrict__ hdr_tab, int hdr_n, uint32_t *flags,
+                                                 uint32_t epoch, int *tile_ctr, int ntiles) {
+    using T = typename Elem<DT>::T;
+    static_assert(sizeof(T) == 2 && !Elem<DT>::is_float, "16-bit samples");
+    union FusedShared {
+        EncV3Shared enc;
+        int16_t alut[4][kLutCap];  // phase 1: one LUT per wave
+    };
+    __shared__ FusedShared U;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // ---- phase 1: tiles (k_analyze_v3<DT, false, true> / <DT, true> per tile, results handed off)
+    while (true) {
+        int tq = 0;
+        if (lane == 0) tq = atomicAdd(tile_ctr, 1);
+        const int t = __builtin_amdgcn_readfirstlane(tq);
+        if (P.dbg && lane == 0 && t < ntiles)
+            printf("frs: block %d wave %d claims tile %d of %d (epoch %u) t=%llu\n", (int)blockIdx.x, wave, t, ntiles,
+                   epoch, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        if (t >= ntiles) break;
+        const TileGeom g = tiles[t];
+        const T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
+        TileNorm tn;
+        wave_tile_minmax<DT>(base, P.row_stride, g, lane, tn.imin, tn.imax);
+        tile_norm_finalize<DT>(tn, P.norm_mode, P.scale_bits);
+        if (lane == 0) {
+            norms[t] = tn;  // (for the host's min/max, after the launch)
+            sc1_store(&hand[t].tn, tn);
+        }
+        const int nfull = g.nframes;  // (no partial frames on this path)
+        const bool live = lane < nfull;
+        const int64_t fk = live ? lane : nfull - 1;  // dead lanes re-read the tile's last frame
+        const int64_t s0 = fk * P.blocksize;
+        double acc[kMaxLpc + 1];
+#pragma unroll
+        for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
+        uint32_t or_acc = 0, ft[5];
+        int16_t *wl = U.alut[wave];
+        if (tn.mode == kNormLut) {
+            const int64_t R = tn.imax - tn.imin;
+            uint32_t *hl = reinterpret_cast<uint32_t *>(hand[t].lut);
+            for (int64_t d2 = lane; 2 * d2 <= R; d2 += 64) {  // entry pairs: 4-byte sc1 stores
+                const int16_t e0 = lut_entry<DT>(tn, 2 * d2);
+                const int16_t e1 = 2 * d2 + 1 <= R ? lut_entry<DT>(tn, 2 * d2 + 1) : (int16_t)0;
+                wl[2 * d2] = e0;
+                wl[2 * d2 + 1] = e1;
+                __hip_atomic_store(hl + d2, (uint32_t)(uint16_t)e0 | ((uint32_t)(uint16_t)e1 << 16), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's LUT stores have landed in LDS
+            __builtin_amdgcn_wave_barrier();
+            ana_autoc<DT, kAnaKindLds, 64>(base, P, g, s0, tn, wl, nullptr, window, (g.w % 64) == 0 ? P.vec_ok : 0,
+                                           acc, or_acc, ft);
+        } else if (tn.mode == kNormZero) {
+            ana_autoc<DT, kAnaKindZero, 64>(base, P, g, s0, tn, wl, nullptr, window, (g.w % 64) == 0 ? P.vec_ok : 0,
+                                            acc, or_acc, ft);
+        } else if (tn.mode == kNormFastDiv) {
+            ana_autoc<DT, kAnaKindFastDiv, 16>(base, P, g, s0, tn, nullptr, nullptr, window,
+                                               (g.w % 16) == 0 ? P.vec_ok : 0, acc, or_acc, ft);
+        } else {
+            ana_autoc<DT, kAnaKindGeneric, 16>(base, P, g, s0, tn, nullptr, nullptr, window,
+                                               (g.w % 16) == 0 ? P.vec_ok : 0, acc, or_acc, ft);
+        }
+        if (live) sc1_store(ana_hand(ana, g.frame_base + fk), analysis_finish(acc, or_acc, P.blocksize, P, ft));
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every handed-off byte of this tile has been written
+        if (lane == 0) __hip_atomic_store(flags + (size_t)t * kFlagStride, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (P.dbg && lane == 0)
+            printf("frs: tile %d published t=%llu\n", t, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
+    __syncthreads();  // the phase-1 LUTs are dead: the LDS becomes the encoder's
+    // ---- phase 2: k_encode_v3's loop; tile parameters, LUTs and analyses come through the hand-off
+    EncV3Shared &S = U.enc;
+    for (int i = threadIdx.x; i < 2048; i += blockDim.x) (&S.crc8x[0][0])[i] = (&c_crc16x8[0][0])[i];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) S.crc8[i] = c_crc8[i];
+    for (int i = threadIdx.x; i < 64; i += blockDim.x) S.xlo[i] = g_xpow_bytes[i];
+    for (int i = threadIdx.x; i < kXpowHi; i += blockDim.x) S.xhi[i] = g_xpow_bytes[64 * i];
+    for (int i = threadIdx.x; i < 4 * kBufWordsV3; i += blockDim.x) (&S.bits[0][0])[i] = 0;
+    if (threadIdx.x == 0) S.lut_tile = -1;
+    PendingFrame prev;
+    uint32_t *fbuf = S.bits[wave];
+    while (true) {
+        __syncthreads();  // previous ticket's readers of S.ticket / S.lut are done
+        if (threadIdx.x == 0) {
+            const int tk = atomicAdd(ticket_ctr, 1);
+            S.ticket = tk;
+            const int64_t u0 = (int64_t)tk * 4;
+            S.want = (u0 < P.nframes) ? ftile[u0] : -1;
+        }
+        __syncthreads();
+        const int64_t fbase = (int64_t)S.ticket * 4;
+        if (fbase >= P.nframes) break;
+        const int want = S.want;
+        if (want != S.lut_tile) {  // WG-uniform
+            if (wave == 0) wait_tile(flags, want, epoch, err);
+            __syncthreads();  // the other waves read the tile's bytes behind wave 0's matched poll
+            const TileNorm tw = sc1_load_uni(&hand[want].tn);
+            if (tw.mode == kNormLut) {
+                const int64_t R = min(tw.imax - tw.imin, (int64_t)kLutCap - 1);  // (a LUT tile's range is below that)
+                uint32_t *hl = reinterpret_cast<uint32_t *>(hand[want].lut);
+                uint32_t *sl = reinterpret_cast<uint32_t *>(S.lut);
+                for (int64_t d2 = threadIdx.x; 2 * d2 <= R; d2 += blockDim.x)
+                    sl[d2] = __hip_atomic_load(hl + d2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) S.lut_tile = want;
+        }
+        const int64_t f = fbase + wave;
+        if (f < P.nframes)
+            encode_frame_v3<DT, false, true>(raster, P, tiles, norms, nullptr, ana, arena, arena_cap, frame_off,
+                                             status, err, S, want, f, lane, ftile, prev, hdr_tab, hdr_n, nullptr,
+                                             nullptr, 0, nullptr, nullptr, hand, flags, epoch);
+    }
+    if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
 }
 
 // ---------------------------------------------------------------- multi-channel streams (>= 3 channels, 16-bit)
@@ -3966,6 +4174,7 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     P.ncand = lv.parts > 1 ? apod_windows(lv.parts) : 0;
     // loose mid/side (stream_encoder.c init): an evaluation every (uint32_t)(sample_rate * 0.4 / blocksize + 0.5) frames
     P.loose_frames = 0;
+    P.dbg = ctx->ana_dbg ? 1 : 0;
     if (P.nch == 2 && lv.mid_side && lv.loose) {
         P.loose_frames = (int32_t)(uint32_t)((double)d->sample_rate * 0.4 / (double)d->blocksize + 0.5);
         if (P.loose_frames == 0) P.loose_frames = 1;
@@ -4094,6 +4303,7 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         if (!(dev_tiles && ctx->geo_ptrs[3] == ctx->frame_tile.ptr))
             k_frame_tile<<<ntiles, 64, 0, st>>>(dtiles, ntiles, ctx->frame_tile.as<int32_t>());
         int nsplit = 1;
+        bool fused = false;
         int split_t[9] = {0};  // first wave (= tile, when split) of each range
         {
             // wave table: (tile, first frame) per wave, up to 64 frames of one tile each
@@ -4111,6 +4321,8 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
             // are whole tiles; range k is analysed on the aux stream and encoded on `st` once its event fired
             nsplit = (fuse_stats && !mc && P.nch == 1 && npartial == 0 && nwaves >= 32 * ctx->enc_split)
                          ? ctx->enc_split : 1;
+            // one launch for analysis + encode (k_fused_v6): 16-bit mono, fused stats, no partial frames
+            fused = ctx->fused && fuse_stats && !mc && P.nch == 1 && npartial == 0 && nsplit == 1;
             hipStream_t ast = st;
             if (nsplit > 1) {
                 if (!ctx->aux_stream) FRS_HIP(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
@@ -4120,8 +4332,8 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                 FRS_HIP(hipEventRecord(ctx->split_ev[nsplit], st));  // the uploads and setup kernels above
                 FRS_HIP(hipStreamWaitEvent(ast, ctx->split_ev[nsplit], 0));
             }
-            prof_begin(ctx, "analyze", &ev, ast);
-            for (int k = 0; k < nsplit; k++) {
+            if (!fused) prof_begin(ctx, "analyze", &ev, ast);
+            for (int k = 0; k < nsplit && !fused; k++) {
                 const int w0 = (int)((int64_t)nwaves * k / nsplit), w1 = (int)((int64_t)nwaves * (k + 1) / nsplit);
                 split_t[k] = w0;
                 const int nw = w1 - w0;
@@ -4174,7 +4386,7 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                 if (nsplit > 1) FRS_HIP(hipEventRecord(ctx->split_ev[k], ast));
             }
             split_t[nsplit] = nwaves;
-            prof_end(ctx, "analyze", ev, ast);
+            if (!fused) prof_end(ctx, "analyze", ev, ast);
             if (!geo_hit) {  // the geometry's device copies are (being) uploaded on this stream: cache them
                 ctx->geo_tiles = tiles;
                 ctx->geo_plist.assign(hplist, hplist + npartial);
@@ -4334,7 +4546,36 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                 ctx->hdr_tab_sr = d->sample_rate;
             }
         }
-        {
+        if (fused) {
+            if constexpr (sizeof(T) == 2) {
+                FRS_HIP(ctx->hand.ensure(sizeof(TileHand) * (size_t)ntiles));
+                FRS_HIP(ctx->analysis.ensure((size_t)kAnaHandStride * nframes));  // frame analyses, one per line
+                dana = ctx->analysis.as<SubAnalysis>();
+                FRS_HIP(ctx->tile_flag.ensure(sizeof(uint32_t) * kFlagStride * (size_t)ntiles));
+                FRS_HIP(ctx->ana_ctr.ensure(64));
+                // flags hold the epoch of the launch that published them.  The epoch is advanced on EVERY launch
+                // (never inside a short-circuited condition: the round-3 k_analyze_v4 kept epoch 0 on its first call,
+                // which matched its zeroed flags), a new allocation is zeroed, and a wrap to 0 zeroes and restarts at 1
+                const bool fresh_flags = ctx->tile_flag.ptr != ctx->tile_flag_zeroed;
+                ++ctx->fuse_epoch;
+                if (fresh_flags || ctx->fuse_epoch == 0) {
+                    FRS_HIP(hipMemsetAsync(ctx->tile_flag.ptr, 0, ctx->tile_flag.bytes, st));
+                    ctx->tile_flag_zeroed = ctx->tile_flag.ptr;
+                    if (ctx->fuse_epoch == 0) ctx->fuse_epoch = 1;
+                }
+                FRS_HIP(hipMemsetAsync(ctx->ana_ctr.ptr, 0, sizeof(int), st));
+                static int nwg_f = 0;
+                if (nwg_f == 0) FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nwg_f, k_fused_v6<DT>, 256, 0));
+                const int64_t grid = std::min<int64_t>((int64_t)std::max(1, nwg_f) * ctx->num_cus, (nframes + 3) / 4);
+                prof_begin(ctx, "fused", &ev);
+                k_fused_v6<DT><<<(unsigned)grid, 256, 0, st>>>(
+                    raster, P, dtiles, dnorms, ctx->hand.as<TileHand>(), ctx->window.as<float>(), dana,
+                    reinterpret_cast<uint8_t *>(arena_dev), arena_cap, ctx->frame_off.as<int64_t>(), dstatus, ticket,
+                    err_flag, ctx->frame_tile.as<int32_t>(), ctx->hdr_tab.as<uint4>(), hdr_n,
+                    ctx->tile_flag.as<uint32_t>(), ctx->fuse_epoch, ctx->ana_ctr.as<int>(), ntiles);
+                prof_end(ctx, "fused", ev);
+            }
+        } else {
             static int nwg_max = 0;  // (per instantiation; the same gfx950 target for every device)
             if (nwg_max == 0) FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nwg_max, k_encode_v3<DT>, 256, 0));
             for (int k = 0; k < nsplit; k++) {
@@ -4353,8 +4594,8 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                                                                 ctx->slots.as<uint32_t>(), dpbytes, nullptr, nullptr,
                                                                 f0, f1);
             }
+            prof_end(ctx, "encode", ev);
         }
-        prof_end(ctx, "encode", ev);
         FRS_HIP(ctx->host_pack.ensure(res_bytes));
         int64_t *dpack = ctx->host_pack.as<int64_t>();
         k_fast_finish<<<(ntiles + 1 + 255) / 256, 256, 0, st>>>(ctx->frame_off.as<int64_t>(), dstatus, dtiles, dnorms,
@@ -4519,6 +4760,7 @@ template <int DT>
 static int run_encode_any(frs_ctx *ctx, const frs_encode_desc *d, const void *raster_dev, void *arena_dev,
                           int64_t arena_cap, int64_t *tile_off, double *tile_min, double *tile_max) {
     int rc = run_encode<DT>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max, true);
+    if (rc == kFastDeclined && ctx->ana_dbg) fprintf(stderr, "frs: %s\n", ctx->err.c_str());
     if (rc == kFastDeclined) rc = run_encode<DT>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max, false);
     return rc;
 }

@@ -105,6 +105,10 @@ struct frs_ctx {
     // per-frame assignment of the group leaders and the leader frame list
     DevBuf lpc_cand, window_hi, loose_assign, loose_lead;
     int window_hi_bs = 0, window_hi_parts = 0;
+    bool fused = false;   // $FRS_FUSED: k_fused_v6 (analysis + encode in one launch) where it applies
+    DevBuf hand, tile_flag;  // k_fused_v6 hand-off: per-tile parameters + LUT, per-tile epoch flags
+    void *tile_flag_zeroed = nullptr;
+    uint32_t fuse_epoch = 0;
     int ana_v5 = 0;       // 1: 4 consumer + 4 producer waves per work-group, 2: 6 + 2
     bool ana_dbg = false; // $FRS_ANA_DBG: k_analyze_v5 wave-cycle totals to stderr
     DevBuf ana_dbgbuf;

@@ -78,8 +78,8 @@ typedef struct {
     int32_t blocksize;          /* FLAC block size (4096, converter.py:205) */
     int32_t sample_rate;        /* STREAMINFO / frame header sample rate (converter.py:25-54) */
     int32_t bits_per_sample;    /* 16 or 24 from _calculate_audio_params (converter.py:29-37) */
-    int32_t compression_level;  /* 0..5 (cli.py:36-37; create-streaming uses 5, cli.py:733); 6..8 and loose
-                                   mid/side (1, 4 on two bands) -> FRS_E_UNSUPPORTED */
+    int32_t compression_level;  /* 0..8 (cli.py:36-37; create-streaming uses 5, cli.py:733); 6..8 with
+                                   subdivide_tukey apodizations, 1 / 4 on two bands with loose mid/side */
     int32_t norm_mode;          /* FRS_NORM_CONVERTER or FRS_NORM_SPATIAL */
     int64_t tile_begin, tile_end;
 } frs_encode_desc;
