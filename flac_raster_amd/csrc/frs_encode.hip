@@ -17,6 +17,7 @@
 #include <type_traits>
 
 #include <cstring>
+#include <unistd.h>
 
 #include "frs_internal.h"
 
@@ -2842,16 +2843,17 @@ template <typename S> __device__ inline S sc1_load(const S *src) {
         d[i] = __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return v;
 }
-// the same for a wave-uniform address, the value made wave-uniform (SGPRs, not one VGPR per dword)
-template <typename S> __device__ inline S sc1_load_uni(const S *src) {
-    static_assert(sizeof(S) % 4 == 0, "dwords");
+// a wave-uniform struct with ONE vector load: lane i reads dword i, then v_readlane per dword (SGPRs)
+template <typename S> __device__ inline S sc1_load_lanes(const S *src) {
+    constexpr int n = (int)(sizeof(S) / 4);
+    static_assert(sizeof(S) % 4 == 0 && n <= 64, "dwords");
+    uint32_t *q = reinterpret_cast<uint32_t *>(const_cast<S *>(src));
+    const int lane = (int)(threadIdx.x & 63);
+    const uint32_t mine = __hip_atomic_load(q + (lane < n ? lane : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     S v;
     uint32_t *d = reinterpret_cast<uint32_t *>(&v);
-    uint32_t *q = reinterpret_cast<uint32_t *>(const_cast<S *>(src));
 #pragma unroll
-    for (int i = 0; i < (int)(sizeof(S) / 4); i++)
-        d[i] = (uint32_t)__builtin_amdgcn_readfirstlane(
-            (int)__hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    for (int i = 0; i < n; i++) d[i] = (uint32_t)__builtin_amdgcn_readlane((int)mine, i);
     return v;
 }
 // (wave-uniform) poll a tile's flag until it holds this launch's epoch; the analysis of every tile is claimed by a
@@ -3080,7 +3082,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
                                        const uint32_t *pslots, const int64_t *pbytes, int chn = 0,
                                        uint32_t *sub_slots = nullptr, int32_t *sub_bits = nullptr,
                                        const TileHand *hand = nullptr, const uint32_t *flags = nullptr,
-                                       uint32_t epoch = 0) {
+                                       uint32_t epoch = 0, const SubAnalysis *hana = nullptr, int tile_begin = 0) {
     using T = typename Elem<DT>::T;
     uint32_t *fbuf = S.bits[threadIdx.x >> 6];
     const int t = ftile[f];
@@ -3112,10 +3114,13 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         prev.map = M;
         return;
     }
+    // COH (k_fused_v6): tiles >= tile_begin were analysed in this launch and come through the hand-off; tiles below it
+    // by k_analyze_v3 before the launch (plain loads)
+    const bool hand_t = COH && t >= tile_begin;  // (wave-uniform)
     TileNorm tn;
-    if constexpr (COH) {  // (the ticket's tile was polled by wave 0 before the work-group barrier)
-        if (t != want) wait_tile(flags, t, epoch, err);
-        tn = sc1_load_uni(&hand[t].tn);
+    if (hand_t) {  // (the ticket's tile was polled by wave 0 before the work-group barrier)
+        if (t != want && flags) wait_tile(flags, t, epoch, err);  // (flags = nullptr: all tiles published)
+        tn = sc1_load_lanes(&hand[t].tn);
     } else {
         tn = norms[t];
     }
@@ -3130,8 +3135,8 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     const int64_t s0 = fk * kMaxBlock;
     constexpr int n = kMaxBlock;
     const int64_t sub = SUB ? f * P.nch + chn : f;
-    const SubAnalysis *asub = COH ? ana_hand(const_cast<SubAnalysis *>(ana), sub) : ana + sub;
-    const SubAnalysis A = COH ? sc1_load_uni(asub) : *asub;
+    const SubAnalysis *asub = hand_t ? ana_hand(const_cast<SubAnalysis *>(hana), sub) : ana + sub;
+    const SubAnalysis A = hand_t ? sc1_load_lanes(asub) : *asub;
     const int w = A.wasted;
     const int sbps = 16 - w;
     const T *base = raster + (int64_t)(P.band0 + chn) * P.band_stride + g.r0 * P.row_stride + g.c0;
@@ -3512,7 +3517,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         w01 = (i >> 1) == 3 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 3], 0) : w01;
         const uint32_t xi = (i & 1) ? (w01 >> 16) : (w01 & 0xFFFFu);
         // (a lane-indexed load: a select chain over A.q costs registers)
-        const int32_t qi = COH ? __hip_atomic_load(const_cast<int32_t *>(&asub->q[i]), __ATOMIC_RELAXED,
+        const int32_t qi = hand_t ? __hip_atomic_load(const_cast<int32_t *>(&asub->q[i]), __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT)
                                : asub->q[i];
         const bool warm = lane < 8 && i < o, coef = type == 3 && lane >= 8 && lane < 16 && i < o;
@@ -3657,7 +3662,7 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
         if (want != S.lut_tile) {  // WG-uniform
             const TileNorm tw = norms[want];
             if (tw.mode == kNormLut) {
-                const int64_t R = tw.imax - tw.imin;
+                const int64_t R = min(tw.imax - tw.imin, (int64_t)kLutCap - 1);  // (a LUT tile's range is below that)
                 const int16_t *src = luts + (int64_t)want * kLutCap;
                 for (int64_t d = threadIdx.x; d <= R; d += blockDim.x) S.lut[d] = src[d];
             }
@@ -3701,7 +3706,9 @@ __global__ void __launch_bounds__(256, 3) k_fused_v6(const typename Elem<DT>::T 
                                                  int64_t arena_cap, int64_t *frame_off, uint64_t *status,
                                                  int *ticket_ctr, int *err, const int32_t *__restrict__ ftile,
                                                  const uint4 *__restrict__ hdr_tab, int hdr_n, uint32_t *flags,
-                                                 uint32_t epoch, int *tile_ctr, int ntiles) {
+                                                 uint32_t epoch, int *tile_ctr, int ntiles, const int16_t *luts,
+                                                 SubAnalysis *hana, int tile_begin,
+                                                 unsigned long long *dbg = nullptr) {
     using T = typename Elem<DT>::T;
     static_assert(sizeof(T) == 2 && !Elem<DT>::is_float, "16-bit samples");
     union FusedShared {
@@ -3709,15 +3716,25 @@ __global__ void __launch_bounds__(256, 3) k_fused_v6(const typename Elem<DT>::T 
         int16_t alut[4][kLutCap];  // phase 1: one LUT per wave
     };
     __shared__ FusedShared U;
+    __shared__ int s_allpub;  // every tile has been published (the done counter reached ntiles): no more flag polls
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int *done_ctr = tile_ctr + 1;  // tiles published (agent-scope add after each tile's flag)
+    const uint64_t t_start = dbg ? __builtin_amdgcn_s_memrealtime() : 0;  // (dbg: per-WG phase times, 100 MHz)
+    // dbg record of this work-group, updated live (system scope: readable by a host copy while the kernel runs):
+    // [start, end of phase 1, end, tickets, last ticket, last tile, state (1 phase 1, 2 flag wait, 3 encode, 4 done),
+    // tiles analysed]
+    auto dbg_put = [&](int i, unsigned long long v) {
+        if (dbg && threadIdx.x == 0)
+            __hip_atomic_store(dbg + 8 * blockIdx.x + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    };
+    dbg_put(0, t_start);
+    dbg_put(6, 1);
+    int ntiles_done = 0;
     // ---- phase 1: tiles (k_analyze_v3<DT, false, true> / <DT, true> per tile, results handed off)
     while (true) {
         int tq = 0;
-        if (lane == 0) tq = atomicAdd(tile_ctr, 1);
+        if (lane == 0) tq = tile_begin + atomicAdd(tile_ctr, 1);
         const int t = __builtin_amdgcn_readfirstlane(tq);
-        if (P.dbg && lane == 0 && t < ntiles)
-            printf("frs: block %d wave %d claims tile %d of %d (epoch %u) t=%llu\n", (int)blockIdx.x, wave, t, ntiles,
-                   epoch, (unsigned long long)__builtin_amdgcn_s_memrealtime());
         if (t >= ntiles) break;
         const TileGeom g = tiles[t];
         const T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
@@ -3762,13 +3779,21 @@ __global__ void __launch_bounds__(256, 3) k_fused_v6(const typename Elem<DT>::T 
             ana_autoc<DT, kAnaKindGeneric, 16>(base, P, g, s0, tn, nullptr, nullptr, window,
                                                (g.w % 16) == 0 ? P.vec_ok : 0, acc, or_acc, ft);
         }
-        if (live) sc1_store(ana_hand(ana, g.frame_base + fk), analysis_finish(acc, or_acc, P.blocksize, P, ft));
+        if (live) sc1_store(ana_hand(hana, g.frame_base + fk), analysis_finish(acc, or_acc, P.blocksize, P, ft));
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every handed-off byte of this tile has been written
-        if (lane == 0) __hip_atomic_store(flags + (size_t)t * kFlagStride, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (P.dbg && lane == 0)
-            printf("frs: tile %d published t=%llu\n", t, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        if (lane == 0) {
+            __hip_atomic_store(flags + (size_t)t * kFlagStride, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(done_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        ntiles_done++;
+        if (wave == 0) dbg_put(7, (unsigned long long)ntiles_done);
     }
+    if (threadIdx.x == 0) s_allpub = 0;
     __syncthreads();  // the phase-1 LUTs are dead: the LDS becomes the encoder's
+    const uint64_t t_p1 = dbg ? __builtin_amdgcn_s_memrealtime() : 0;
+    dbg_put(1, t_p1);
+    dbg_put(6, 3);
+    int ntk = 0;
     // ---- phase 2: k_encode_v3's loop; tile parameters, LUTs and analyses come through the hand-off
     EncV3Shared &S = U.enc;
     for (int i = threadIdx.x; i < 2048; i += blockDim.x) (&S.crc8x[0][0])[i] = (&c_crc16x8[0][0])[i];
@@ -3783,6 +3808,9 @@ __global__ void __launch_bounds__(256, 3) k_fused_v6(const typename Elem<DT>::T 
         __syncthreads();  // previous ticket's readers of S.ticket / S.lut are done
         if (threadIdx.x == 0) {
             const int tk = atomicAdd(ticket_ctr, 1);
+            // (independent of the ticket: both requests in flight together)
+            if (!s_allpub)
+                s_allpub = __hip_atomic_load(done_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ntiles - tile_begin;
             S.ticket = tk;
             const int64_t u0 = (int64_t)tk * 4;
             S.want = (u0 < P.nframes) ? ftile[u0] : -1;
@@ -3790,17 +3818,34 @@ __global__ void __launch_bounds__(256, 3) k_fused_v6(const typename Elem<DT>::T 
         __syncthreads();
         const int64_t fbase = (int64_t)S.ticket * 4;
         if (fbase >= P.nframes) break;
+        ntk++;
         const int want = S.want;
+        const bool allpub = s_allpub;
+        dbg_put(3, (unsigned long long)ntk);
+        dbg_put(4, (unsigned long long)S.ticket);
+        dbg_put(5, (unsigned long long)want);
         if (want != S.lut_tile) {  // WG-uniform
-            if (wave == 0) wait_tile(flags, want, epoch, err);
+            const bool hand_w = want >= tile_begin;
+            dbg_put(6, allpub ? 5 : 2);
+            if (wave == 0 && !allpub && hand_w) wait_tile(flags, want, epoch, err);
+            dbg_put(6, 3);
             __syncthreads();  // the other waves read the tile's bytes behind wave 0's matched poll
-            const TileNorm tw = sc1_load_uni(&hand[want].tn);
-            if (tw.mode == kNormLut) {
-                const int64_t R = min(tw.imax - tw.imin, (int64_t)kLutCap - 1);  // (a LUT tile's range is below that)
-                uint32_t *hl = reinterpret_cast<uint32_t *>(hand[want].lut);
-                uint32_t *sl = reinterpret_cast<uint32_t *>(S.lut);
-                for (int64_t d2 = threadIdx.x; 2 * d2 <= R; d2 += blockDim.x)
-                    sl[d2] = __hip_atomic_load(hl + d2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (hand_w) {
+                const TileNorm tw = sc1_load_lanes(&hand[want].tn);
+                if (tw.mode == kNormLut) {
+                    const int64_t R = min(tw.imax - tw.imin, (int64_t)kLutCap - 1);  // (a LUT tile's range is below)
+                    uint32_t *hl = reinterpret_cast<uint32_t *>(hand[want].lut);
+                    uint32_t *sl = reinterpret_cast<uint32_t *>(S.lut);
+                    for (int64_t d2 = threadIdx.x; 2 * d2 <= R; d2 += blockDim.x)
+                        sl[d2] = __hip_atomic_load(hl + d2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            } else {  // analysed by k_analyze_v3 before this launch
+                const TileNorm tw = norms[want];
+                if (tw.mode == kNormLut) {
+                    const int64_t R = min(tw.imax - tw.imin, (int64_t)kLutCap - 1);
+                    const int16_t *src = luts + (int64_t)want * kLutCap;
+                    for (int64_t d = threadIdx.x; d <= R; d += blockDim.x) S.lut[d] = src[d];
+                }
             }
             __syncthreads();
             if (threadIdx.x == 0) S.lut_tile = want;
@@ -3809,9 +3854,12 @@ __global__ void __launch_bounds__(256, 3) k_fused_v6(const typename Elem<DT>::T 
         if (f < P.nframes)
             encode_frame_v3<DT, false, true>(raster, P, tiles, norms, nullptr, ana, arena, arena_cap, frame_off,
                                              status, err, S, want, f, lane, ftile, prev, hdr_tab, hdr_n, nullptr,
-                                             nullptr, 0, nullptr, nullptr, hand, flags, epoch);
+                                             nullptr, 0, nullptr, nullptr, hand, allpub ? nullptr : flags, epoch,
+                                             hana, tile_begin);
     }
     if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
+    dbg_put(2, dbg ? __builtin_amdgcn_s_memrealtime() : 0);
+    dbg_put(6, 4);
 }
 
 // ---------------------------------------------------------------- multi-channel streams (>= 3 channels, 16-bit)
@@ -4549,8 +4597,22 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         if (fused) {
             if constexpr (sizeof(T) == 2) {
                 FRS_HIP(ctx->hand.ensure(sizeof(TileHand) * (size_t)ntiles));
-                FRS_HIP(ctx->analysis.ensure((size_t)kAnaHandStride * nframes));  // frame analyses, one per line
-                dana = ctx->analysis.as<SubAnalysis>();
+                FRS_HIP(ctx->ana_hand.ensure((size_t)kAnaHandStride * nframes));  // frame analyses, one per line
+                // hybrid (FRS_FUSED=2): k_analyze_v3 takes the first K tiles (one full round of its 4 waves per SIMD),
+                // the fused launch analyses the rest while its early work-groups already encode
+                int K = 0;
+                if (ctx->fused == 2) {
+                    K = ctx->fused_k > 0 ? ctx->fused_k : 16 * ctx->num_cus;
+                    K = std::min(K, ntiles);
+                    prof_begin(ctx, "analyze", &ev);
+                    const unsigned wg = (unsigned)((K + 3) / 4);
+                    k_analyze_v3<DT, false, true><<<wg, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
+                                                                     ctx->window.as<float>(), dana,
+                                                                     ctx->wave_tab.as<int2>(), K);
+                    k_analyze_v3<DT, true><<<wg, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
+                                                              ctx->window.as<float>(), dana, ctx->wave_tab.as<int2>(), K);
+                    prof_end(ctx, "analyze", ev);
+                }
                 FRS_HIP(ctx->tile_flag.ensure(sizeof(uint32_t) * kFlagStride * (size_t)ntiles));
                 FRS_HIP(ctx->ana_ctr.ensure(64));
                 // flags hold the epoch of the launch that published them.  The epoch is advanced on EVERY launch
@@ -4563,17 +4625,49 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                     ctx->tile_flag_zeroed = ctx->tile_flag.ptr;
                     if (ctx->fuse_epoch == 0) ctx->fuse_epoch = 1;
                 }
-                FRS_HIP(hipMemsetAsync(ctx->ana_ctr.ptr, 0, sizeof(int), st));
+                FRS_HIP(hipMemsetAsync(ctx->ana_ctr.ptr, 0, 2 * sizeof(int), st));  // tile counter, done counter
                 static int nwg_f = 0;
                 if (nwg_f == 0) FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nwg_f, k_fused_v6<DT>, 256, 0));
                 const int64_t grid = std::min<int64_t>((int64_t)std::max(1, nwg_f) * ctx->num_cus, (nframes + 3) / 4);
+                unsigned long long *dbg = nullptr;
+                if (ctx->ana_dbg) {
+                    FRS_HIP(ctx->ana_dbgbuf.ensure(64 * (size_t)grid));
+                    FRS_HIP(hipMemsetAsync(ctx->ana_dbgbuf.ptr, 0, 64 * (size_t)grid, st));
+                    FRS_HIP(hipStreamSynchronize(st));
+                    dbg = ctx->ana_dbgbuf.as<unsigned long long>();
+                }
                 prof_begin(ctx, "fused", &ev);
                 k_fused_v6<DT><<<(unsigned)grid, 256, 0, st>>>(
                     raster, P, dtiles, dnorms, ctx->hand.as<TileHand>(), ctx->window.as<float>(), dana,
                     reinterpret_cast<uint8_t *>(arena_dev), arena_cap, ctx->frame_off.as<int64_t>(), dstatus, ticket,
                     err_flag, ctx->frame_tile.as<int32_t>(), ctx->hdr_tab.as<uint4>(), hdr_n,
-                    ctx->tile_flag.as<uint32_t>(), ctx->fuse_epoch, ctx->ana_ctr.as<int>(), ntiles);
+                    ctx->tile_flag.as<uint32_t>(), ctx->fuse_epoch, ctx->ana_ctr.as<int>(), ntiles,
+                    ctx->luts.as<int16_t>(), ctx->ana_hand.as<SubAnalysis>(), K, dbg);
                 prof_end(ctx, "fused", ev);
+                if (dbg) {  // the work-groups' records; a launch still running after 10 s is reported and the process ends
+                    bool done = false;
+                    for (int i = 0; i < 1000 && !done; i++) {
+                        done = hipStreamQuery(st) == hipSuccess;
+                        if (!done) usleep(10000);
+                    }
+                    std::vector<unsigned long long> h(8 * (size_t)grid);
+                    int herr = 0;
+                    hipStream_t ds = st;
+                    if (!done) FRS_HIP(hipStreamCreateWithFlags(&ds, hipStreamNonBlocking));
+                    FRS_HIP(hipMemcpyAsync(h.data(), dbg, 64 * (size_t)grid, hipMemcpyDeviceToHost, ds));
+                    FRS_HIP(hipMemcpyAsync(&herr, err_flag, sizeof(int), hipMemcpyDeviceToHost, ds));
+                    FRS_HIP(hipStreamSynchronize(ds));
+                    for (int64_t b = 0; b < grid; b++)
+                        fprintf(stderr, "frs-wg %lld %llu %llu %llu %llu %llu %llu %llu %llu\n", (long long)b, h[8 * b],
+                                h[8 * b + 1], h[8 * b + 2], h[8 * b + 3], h[8 * b + 4], h[8 * b + 5], h[8 * b + 6],
+                                h[8 * b + 7]);
+                    fprintf(stderr, "frs-fused done=%d err=%d ntiles=%d nframes=%lld grid=%lld epoch=%u\n", (int)done, herr,
+                            (int)ntiles, (long long)nframes, (long long)grid, ctx->fuse_epoch);
+                    if (!done) {
+                        fflush(stderr);
+                        _exit(3);
+                    }
+                }
             }
         } else {
             static int nwg_max = 0;  // (per instantiation; the same gfx950 target for every device)

@@ -105,8 +105,10 @@ struct frs_ctx {
     // per-frame assignment of the group leaders and the leader frame list
     DevBuf lpc_cand, window_hi, loose_assign, loose_lead;
     int window_hi_bs = 0, window_hi_parts = 0;
-    bool fused = false;   // $FRS_FUSED: k_fused_v6 (analysis + encode in one launch) where it applies
-    DevBuf hand, tile_flag;  // k_fused_v6 hand-off: per-tile parameters + LUT, per-tile epoch flags
+    int fused = 0;        // $FRS_FUSED: 1 k_fused_v6 (analysis + encode in one launch), 2 hybrid (k_analyze_v3 on the first
+                          // $FRS_FUSED_K tiles, default 16 per CU, then k_fused_v6), where they apply
+    int fused_k = 0;
+    DevBuf hand, tile_flag, ana_hand;  // k_fused_v6 hand-off: per-tile parameters + LUT, per-tile flags, frame analyses
     void *tile_flag_zeroed = nullptr;
     uint32_t fuse_epoch = 0;
     int ana_v5 = 0;       // 1: 4 consumer + 4 producer waves per work-group, 2: 6 + 2
