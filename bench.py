@@ -208,19 +208,22 @@ def main():
                                        "peak": VALU_PEAK_GINST_S, "unit": "G wave-instr/s",
                                        "frac": round(rate / VALU_PEAK_GINST_S, 4)}
 
+    progress(f"step {ms_per_step:.3f} ms")
     if args.queries > 0:
+        progress("bbox_extract")
         bx = bbox_extract(ctx, comm, raster, arena, off, mn, mx, H, W, T, row0, counts, args.queries)
         if rank == 0:
             result["bbox_extract"] = bx
     if world == 1 and not args.no_extras:
-        result["batched_decode"] = batched_decode(ctx, arena, off, mn, mx, rows, W, T)
-        result["sentinel2"] = sentinel2(ctx)
-        result["convert_multiband"] = convert_multiband(ctx)
-        result["convert_2band"] = convert_2band(ctx)
-        result["raw_frames"] = raw_frames(ctx)
-        result["convert_level8"] = convert_level8(ctx)
-        result["end_to_end"] = end_to_end(ctx, raster, arena, off, rows, W, T, args)
+        for name, leg in (("batched_decode", lambda: batched_decode(ctx, arena, off, mn, mx, rows, W, T)),
+                          ("sentinel2", lambda: sentinel2(ctx)), ("convert_multiband", lambda: convert_multiband(ctx)),
+                          ("convert_2band", lambda: convert_2band(ctx)), ("raw_frames", lambda: raw_frames(ctx)),
+                          ("convert_level8", lambda: convert_level8(ctx)),
+                          ("end_to_end", lambda: end_to_end(ctx, raster, arena, off, rows, W, T, args))):
+            progress(name)
+            result[name] = leg()
     if rank == 0 and world == 1 and not args.no_cpu:  # (the CPU baseline is an N = 1 figure)
+        progress("cpu_baseline")
         result["cpu_baseline"] = cpu_baseline(ctx, raster, rows, W, T, off, arena, args)
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -229,6 +232,11 @@ def main():
     if comm is not None:
         comm.close()
     ctx.close()
+
+
+def progress(what):
+    """One stderr line per bench leg (a long default run keeps writing while it works)."""
+    print(f"bench.py: {what} ({time.strftime('%H:%M:%S')})", file=sys.stderr, flush=True)
 
 
 def allgather_figures(comm, ag_s, sizes, counts, reps=20):

@@ -2913,7 +2913,8 @@ __device__ inline uint32_t frame_header_bytes(uint32_t v, int srx) {
 
 // Offset of a finished frame (decoupled look-back), inclusive publish, store of its bytes from the wave's
 // bit buffer, and re-zeroing of that buffer.
-__device__ inline void resolve_and_store(const EncodeParams &P, PendingFrame &pf, uint32_t *fbuf, uint8_t *arena,
+// (forced inline: in the larger k_fused_v6 the inliner otherwise emitted real calls with scratch arguments)
+__device__ __forceinline__ void resolve_and_store(const EncodeParams &P, PendingFrame &pf, uint32_t *fbuf, uint8_t *arena,
                                          int64_t arena_cap, int64_t *frame_off, uint64_t *status, int *err, int lane) {
     const int64_t f = pf.f;
     const uint64_t fbytes = pf.fbytes;
@@ -3074,15 +3075,15 @@ __device__ inline uint32_t fixed_lane_sum(const uint32_t *E, bool l0) {
 // from bit 0 of its buffer -- no frame header, no look-back, no CRC -- and stores its words to sub_slots[f * nch +
 // chn] with its bit length in sub_bits; k_mc_assemble joins a frame's subframes behind the frame header.
 template <int DT, bool SUB = false, bool COH = false>
-__device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const EncodeParams &P,
+__device__ __forceinline__ void encode_frame_v3(const typename Elem<DT>::T *raster, const EncodeParams &P,
                                        const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
                                        const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap, int64_t *frame_off,
                                        uint64_t *status, int *err, EncV3Shared &S, int want, int64_t f, int lane,
                                        const int32_t *ftile, PendingFrame &prev, const uint4 *hdr_tab, int hdr_n,
                                        const uint32_t *pslots, const int64_t *pbytes, int chn = 0,
                                        uint32_t *sub_slots = nullptr, int32_t *sub_bits = nullptr,
-                                       const TileHand *hand = nullptr, const uint32_t *flags = nullptr,
-                                       uint32_t epoch = 0, const SubAnalysis *hana = nullptr, int tile_begin = 0) {
+                                       const TileNorm *coh_tn = nullptr, const SubAnalysis *coh_a = nullptr,
+                                       const int32_t *coh_q = nullptr, bool coh_sc1 = false) {
     using T = typename Elem<DT>::T;
     uint32_t *fbuf = S.bits[threadIdx.x >> 6];
     const int t = ftile[f];
@@ -3114,16 +3115,9 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         prev.map = M;
         return;
     }
-    // COH (k_fused_v6): tiles >= tile_begin were analysed in this launch and come through the hand-off; tiles below it
-    // by k_analyze_v3 before the launch (plain loads)
-    const bool hand_t = COH && t >= tile_begin;  // (wave-uniform)
-    TileNorm tn;
-    if (hand_t) {  // (the ticket's tile was polled by wave 0 before the work-group barrier)
-        if (t != want && flags) wait_tile(flags, t, epoch, err);  // (flags = nullptr: all tiles published)
-        tn = sc1_load_lanes(&hand[t].tn);
-    } else {
-        tn = norms[t];
-    }
+    // COH (k_fused_v6): the caller loaded the tile's parameters, the frame's analysis and the lane's coefficient
+    // (from the hand-off or from k_analyze_v3's output): no second load path in here
+    TileNorm tn = COH ? *coh_tn : norms[t];
     // the WG's LDS LUT belongs to tile `want`; a frame of another tile takes the exact division instead
     if (t != want && tn.mode == kNormLut) tn.mode = kNormSlow;
     const int16_t *lut = S.lut;
@@ -3135,8 +3129,7 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
     const int64_t s0 = fk * kMaxBlock;
     constexpr int n = kMaxBlock;
     const int64_t sub = SUB ? f * P.nch + chn : f;
-    const SubAnalysis *asub = hand_t ? ana_hand(const_cast<SubAnalysis *>(hana), sub) : ana + sub;
-    const SubAnalysis A = hand_t ? sc1_load_lanes(asub) : *asub;
+    const SubAnalysis A = COH ? *coh_a : ana[sub];
     const int w = A.wasted;
     const int sbps = 16 - w;
     const T *base = raster + (int64_t)(P.band0 + chn) * P.band_stride + g.r0 * P.row_stride + g.c0;
@@ -3517,9 +3510,10 @@ __device__ inline void encode_frame_v3(const typename Elem<DT>::T *raster, const
         w01 = (i >> 1) == 3 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 3], 0) : w01;
         const uint32_t xi = (i & 1) ? (w01 >> 16) : (w01 & 0xFFFFu);
         // (a lane-indexed load: a select chain over A.q costs registers)
-        const int32_t qi = hand_t ? __hip_atomic_load(const_cast<int32_t *>(&asub->q[i]), __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT)
-                               : asub->q[i];
+        const int32_t qi = !COH ? ana[sub].q[i]
+                           : coh_sc1 ? __hip_atomic_load(const_cast<int32_t *>(coh_q + i), __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)
+                                     : coh_q[i];
         const bool warm = lane < 8 && i < o, coef = type == 3 && lane >= 8 && lane < 16 && i < o;
         if (warm)
             lds_put_bits2(fbuf, M, pos0 + (uint32_t)i * sbps, xi & ((1u << sbps) - 1u), sbps);
@@ -3691,51 +3685,29 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
         if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
 }
 
-// ------------------------------------------------------------------------------ k_fused_v6
-// The analysis and the encoder of a 16-bit mono job in ONE persistent launch.  Separate launches leave the chip
-// idle at the analysis' end: a tile's 64 frames are 64 sequential fp64 sums on one wave (~0.4 ms), 6241 C4 tiles on
-// 3-4 K wave slots take two rounds, and the second is a third full.  Here every work-group first claims tiles from a
-// global counter (stats, parameters, LUT, the k_analyze_v3 sums: phase 1) and, once none is left, joins the encoder
-// (k_encode_v3's ticket loop: phase 2), so the last tiles' sums run beside the first frames' coding.  Frames are coded
-// in stream order and a frame's tile was claimed before any encoder started, so an encoder waits at most for one
-// tile's analysis (flag polled per tile; the hand-off protocol above).  No wave of phase 1 waits on anything.
+// Phase 1 of k_fused_v6: the work-group claims tiles [tile_begin, ntiles) four at a time until none is left; per tile
+// (one per wave) the stats, parameters, LUT and sums of k_analyze_v3, every result handed off (sc1 stores, vmcnt(0),
+// flag, done counter).  Returns the tiles this wave analysed.
 template <int DT>
-__global__ void __launch_bounds__(256, 3) k_fused_v6(const typename Elem<DT>::T *raster, EncodeParams P,
-                                                 const TileGeom *tiles, TileNorm *norms, TileHand *hand,
-                                                 const float *__restrict__ window, SubAnalysis *ana, uint8_t *arena,
-                                                 int64_t arena_cap, int64_t *frame_off, uint64_t *status,
-                                                 int *ticket_ctr, int *err, const int32_t *__restrict__ ftile,
-                                                 const uint4 *__restrict__ hdr_tab, int hdr_n, uint32_t *flags,
-                                                 uint32_t epoch, int *tile_ctr, int ntiles, const int16_t *luts,
-                                                 SubAnalysis *hana, int tile_begin,
-                                                 unsigned long long *dbg = nullptr) {
+__device__ __forceinline__ int fused_analyse_tiles(const typename Elem<DT>::T *raster, const EncodeParams &P,
+                                                const TileGeom *tiles, TileNorm *norms, TileHand *hand,
+                                                const float *__restrict__ window, SubAnalysis *hana, uint32_t *flags,
+                                                uint32_t epoch, int *tile_ctr, int *done_ctr, int ntiles,
+                                                int tile_begin, int16_t *wl, int *s_claim) {
     using T = typename Elem<DT>::T;
-    static_assert(sizeof(T) == 2 && !Elem<DT>::is_float, "16-bit samples");
-    union FusedShared {
-        EncV3Shared enc;
-        int16_t alut[4][kLutCap];  // phase 1: one LUT per wave
-    };
-    __shared__ FusedShared U;
-    __shared__ int s_allpub;  // every tile has been published (the done counter reached ntiles): no more flag polls
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int *done_ctr = tile_ctr + 1;  // tiles published (agent-scope add after each tile's flag)
-    const uint64_t t_start = dbg ? __builtin_amdgcn_s_memrealtime() : 0;  // (dbg: per-WG phase times, 100 MHz)
-    // dbg record of this work-group, updated live (system scope: readable by a host copy while the kernel runs):
-    // [start, end of phase 1, end, tickets, last ticket, last tile, state (1 phase 1, 2 flag wait, 3 encode, 4 done),
-    // tiles analysed]
-    auto dbg_put = [&](int i, unsigned long long v) {
-        if (dbg && threadIdx.x == 0)
-            __hip_atomic_store(dbg + 8 * blockIdx.x + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    };
-    dbg_put(0, t_start);
-    dbg_put(6, 1);
-    int ntiles_done = 0;
-    // ---- phase 1: tiles (k_analyze_v3<DT, false, true> / <DT, true> per tile, results handed off)
+    const int lane = (int)(threadIdx.x & 63), wave = (int)(threadIdx.x >> 6);
+    int done = 0;
     while (true) {
-        int tq = 0;
-        if (lane == 0) tq = tile_begin + atomicAdd(tile_ctr, 1);
-        const int t = __builtin_amdgcn_readfirstlane(tq);
-        if (t >= ntiles) break;
+        // the work-group claims 4 tiles at a time, one per wave: its waves start and end their tiles together, so
+        // none idles at the phase barrier behind a sibling's tile (per-wave claims left ~30 % of the waves waiting
+        // for up to a tile's sums there)
+        __syncthreads();
+        if (threadIdx.x == 0) *s_claim = tile_begin + atomicAdd(tile_ctr, 4);
+        __syncthreads();
+        const int t0 = *s_claim;
+        if (t0 >= ntiles) break;
+        const int t = t0 + wave;
+        if (t >= ntiles) continue;
         const TileGeom g = tiles[t];
         const T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
         TileNorm tn;
@@ -3753,7 +3725,6 @@ __global__ void __launch_bounds__(256, 3) k_fused_v6(const typename Elem<DT>::T 
 #pragma unroll
         for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
         uint32_t or_acc = 0, ft[5];
-        int16_t *wl = U.alut[wave];
         if (tn.mode == kNormLut) {
             const int64_t R = tn.imax - tn.imin;
             uint32_t *hl = reinterpret_cast<uint32_t *>(hand[t].lut);
@@ -3785,16 +3756,62 @@ __global__ void __launch_bounds__(256, 3) k_fused_v6(const typename Elem<DT>::T 
             __hip_atomic_store(flags + (size_t)t * kFlagStride, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_add(done_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        ntiles_done++;
-        if (wave == 0) dbg_put(7, (unsigned long long)ntiles_done);
+        done++;
     }
+    return done;
+}
+
+// ------------------------------------------------------------------------------ k_fused_v6
+// The analysis and the encoder of a 16-bit mono job in ONE persistent launch.  Separate launches leave the chip
+// half idle in the analysis' second round: a tile's 64 frames are 64 sequential fp64 sums on one wave (~0.4 ms), and
+// 6241 C4 tiles on 4096 wave slots take 1.5 rounds.  Here every work-group first claims tiles from a global counter
+// (phase 1, fused_analyse_tiles) and, once none is left, joins the encoder (k_encode_v3's ticket loop: phase 2), so
+// the last tiles' sums run beside the first frames' coding.  Frames are coded in stream order and a frame's tile was
+// claimed before any encoder started, so an encoder waits at most for one tile's analysis (flag polled per tile, the
+// hand-off protocol above; no polls at all once the done counter says every tile is published).  Hybrid
+// (tile_begin > 0): k_analyze_v3 analysed tiles [0, tile_begin) before the launch (one full round at its 4 waves per
+// SIMD); those are read with plain loads, the rest through the hand-off.
+template <int DT, bool PH1 = true>
+__global__ void __launch_bounds__(256, PH1 ? 3 : 1) k_fused_v6(const typename Elem<DT>::T *raster, EncodeParams P,
+                                                 const TileGeom *tiles, TileNorm *norms, TileHand *hand,
+                                                 const float *__restrict__ window, SubAnalysis *ana, uint8_t *arena,
+                                                 int64_t arena_cap, int64_t *frame_off, uint64_t *status,
+                                                 int *ticket_ctr, int *err, const int32_t *__restrict__ ftile,
+                                                 const uint4 *__restrict__ hdr_tab, int hdr_n, uint32_t *flags,
+                                                 uint32_t epoch, int *tile_ctr, int ntiles, const int16_t *luts,
+                                                 SubAnalysis *hana, int tile_begin,
+                                                 unsigned long long *dbg = nullptr) {
+    using T = typename Elem<DT>::T;
+    static_assert(sizeof(T) == 2 && !Elem<DT>::is_float, "16-bit samples");
+    union FusedShared {
+        EncV3Shared enc;
+        int16_t alut[4][kLutCap];  // phase 1: one LUT per wave
+    };
+    __shared__ FusedShared U;
+    __shared__ int s_allpub;  // every tile has been published (the done counter reached its target): no more polls
+    __shared__ int s_claim;   // phase 1: the work-group's claimed tiles
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int *done_ctr = tile_ctr + 1;  // tiles published (agent-scope add after each tile's flag)
+    // dbg record of this work-group, updated live (system scope: readable by a host copy while the kernel runs):
+    // [start, end of phase 1, end, tickets, last ticket, last tile, state (1 phase 1, 2 flag wait, 3 encode, 4 done,
+    // 5 no wait needed), tiles analysed by wave 0]  (s_memrealtime, 100 MHz)
+    auto dbg_put = [&](int i, unsigned long long v) {
+        if (dbg && threadIdx.x == 0)
+            __hip_atomic_store(dbg + 8 * blockIdx.x + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    };
+    dbg_put(0, dbg ? __builtin_amdgcn_s_memrealtime() : 0);
+    dbg_put(6, 1);
+    // ---- phase 1
+    int ndone = 0;
+    if constexpr (PH1)
+        ndone = fused_analyse_tiles<DT>(raster, P, tiles, norms, hand, window, hana, flags, epoch, tile_ctr, done_ctr,
+                                        ntiles, tile_begin, U.alut[wave], &s_claim);
+    if (wave == 0) dbg_put(7, (unsigned long long)ndone);
     if (threadIdx.x == 0) s_allpub = 0;
     __syncthreads();  // the phase-1 LUTs are dead: the LDS becomes the encoder's
-    const uint64_t t_p1 = dbg ? __builtin_amdgcn_s_memrealtime() : 0;
-    dbg_put(1, t_p1);
+    dbg_put(1, dbg ? __builtin_amdgcn_s_memrealtime() : 0);
     dbg_put(6, 3);
-    int ntk = 0;
-    // ---- phase 2: k_encode_v3's loop; tile parameters, LUTs and analyses come through the hand-off
+    // ---- phase 2: k_encode_v3's loop
     EncV3Shared &S = U.enc;
     for (int i = threadIdx.x; i < 2048; i += blockDim.x) (&S.crc8x[0][0])[i] = (&c_crc16x8[0][0])[i];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) S.crc8[i] = c_crc8[i];
@@ -3804,6 +3821,7 @@ __global__ void __launch_bounds__(256, 3) k_fused_v6(const typename Elem<DT>::T 
     if (threadIdx.x == 0) S.lut_tile = -1;
     PendingFrame prev;
     uint32_t *fbuf = S.bits[wave];
+    int ntk = 0;
     while (true) {
         __syncthreads();  // previous ticket's readers of S.ticket / S.lut are done
         if (threadIdx.x == 0) {
@@ -3851,11 +3869,34 @@ __global__ void __launch_bounds__(256, 3) k_fused_v6(const typename Elem<DT>::T 
             if (threadIdx.x == 0) S.lut_tile = want;
         }
         const int64_t f = fbase + wave;
-        if (f < P.nframes)
-            encode_frame_v3<DT, false, true>(raster, P, tiles, norms, nullptr, ana, arena, arena_cap, frame_off,
-                                             status, err, S, want, f, lane, ftile, prev, hdr_tab, hdr_n, nullptr,
-                                             nullptr, 0, nullptr, nullptr, hand, allpub ? nullptr : flags, epoch,
-                                             hana, tile_begin);
+        if (f < P.nframes) {
+            if constexpr (!PH1) {  // every tile analysed before the launch: k_encode_v3's own path
+                encode_frame_v3<DT>(raster, P, tiles, norms, luts, ana, arena, arena_cap, frame_off, status, err, S,
+                                    want, f, lane, ftile, prev, hdr_tab, hdr_n, nullptr, nullptr);
+            } else {
+                // the frame's tile parameters and analysis (encode_frame_v3's COH inputs) and where its LPC
+                // coefficients are read
+                const int t = ftile[f];
+                TileNorm tn;
+                SubAnalysis A;
+                const int32_t *qp;
+                const bool sc1 = t >= tile_begin;
+                if (sc1) {
+                    if (t != want && !allpub) wait_tile(flags, t, epoch, err);
+                    tn = sc1_load_lanes(&hand[t].tn);
+                    const SubAnalysis *ap = ana_hand(hana, f);
+                    A = sc1_load_lanes(ap);
+                    qp = ap->q;
+                } else {
+                    tn = norms[t];
+                    A = ana[f];
+                    qp = ana[f].q;
+                }
+                encode_frame_v3<DT, false, true>(raster, P, tiles, norms, nullptr, ana, arena, arena_cap, frame_off,
+                                                 status, err, S, want, f, lane, ftile, prev, hdr_tab, hdr_n, nullptr,
+                                                 nullptr, 0, nullptr, nullptr, &tn, &A, qp, sc1);
+            }
+        }
     }
     if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
     dbg_put(2, dbg ? __builtin_amdgcn_s_memrealtime() : 0);
@@ -4637,7 +4678,8 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                     dbg = ctx->ana_dbgbuf.as<unsigned long long>();
                 }
                 prof_begin(ctx, "fused", &ev);
-                k_fused_v6<DT><<<(unsigned)grid, 256, 0, st>>>(
+                auto kf = K >= ntiles ? k_fused_v6<DT, false> : k_fused_v6<DT, true>;  // (no tile left: encoder only)
+                kf<<<(unsigned)grid, 256, 0, st>>>(
                     raster, P, dtiles, dnorms, ctx->hand.as<TileHand>(), ctx->window.as<float>(), dana,
                     reinterpret_cast<uint8_t *>(arena_dev), arena_cap, ctx->frame_off.as<int64_t>(), dstatus, ticket,
                     err_flag, ctx->frame_tile.as<int32_t>(), ctx->hdr_tab.as<uint4>(), hdr_n,
