@@ -705,15 +705,24 @@ __global__ void __launch_bounds__(64) k_span_crc_wave(const uint8_t *blob, const
 
 // Span check for batched decodes, one lane per candidate (the wave form above spends a work-group's LDS stage per
 // candidate and runs at ~1.5 waves per SIMD): the lane folds the bytes from its candidate into a CRC-16 with
-// aligned dword loads (slice-by-4 tables in LDS) and compares it at every later candidate start (and the stream
-// end).  Same outputs as k_span_crc_wave.
+// aligned loads and compares it at every later candidate start (and the stream end).  Same outputs as
+// k_span_crc_wave.  The fold is a dependency chain through LDS table lookups; slice-by-16 (16 tables, 8 KB of LDS,
+// derived in the work-group from the slice-by-4 ones) puts only two of a 16-byte step's lookups on that chain
+// instead of two of every 4 bytes' (slice-by-4: the span check was 1.27 ms of the 7.4 ms batched C4 decode).
 __global__ void __launch_bounds__(256) k_span_crc_lane(const uint8_t *blob, const int64_t *soff, int ns,
                                                       const int64_t *cpos, const int *ncand, int cand_cap,
                                                       int64_t max_frame, int64_t *ends, int32_t *nexti) {
-    __shared__ __attribute__((aligned(16))) uint16_t t4[4][256];
+    __shared__ __attribute__((aligned(16))) uint16_t t4[16][256];  // t4[k][x]: byte x followed by k zero bytes
     for (int k = threadIdx.x; k < 128; k += blockDim.x)
         reinterpret_cast<uint4 *>(&t4[0][0])[k] = reinterpret_cast<const uint4 *>(&d_crc16x4[0][0])[k];
     __syncthreads();
+    for (int k = 4; k < 16; k++) {  // t[k][x] = t[k-1][x] advanced by one zero byte
+        for (int x = threadIdx.x; x < 256; x += blockDim.x) {
+            const uint32_t v = t4[k - 1][x];
+            t4[k][x] = (uint16_t)(((v << 8) & 0xFFFFu) ^ t4[0][v >> 8]);
+        }
+        __syncthreads();
+    }
     const int nc = *ncand;
     if (nc > cand_cap) return;
     const int64_t lead = (int64_t)(reinterpret_cast<uintptr_t>(blob) & 15);
@@ -741,32 +750,26 @@ __global__ void __launch_bounds__(256) k_span_crc_lane(const uint8_t *blob, cons
             // whole 128-byte lines, all eight 16-byte loads issued together: a lane streams its own span, and with
             // one 16-byte load per step the ~1500 concurrent streams of a CU evicted each line from L2 between its
             // eight visits (PMC: 7x the span bytes fetched)
-            for (; b + 128 <= stop && ((b + lead) & 127); b += 16) {
-                const uint4 v = *reinterpret_cast<const uint4 *>(abase + b + lead);
-                fold4(v.x);
-                fold4(v.y);
-                fold4(v.z);
-                fold4(v.w);
-            }
+            auto fold16 = [&](const uint4 &v) {  // 16 bytes (little-endian dwords) in order: slice-by-16
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+                uint32_t r = (uint32_t)t4[15][((crc >> 8) ^ (w[0] & 0xFF)) & 0xFF] ^
+                             t4[14][((crc & 0xFF) ^ ((w[0] >> 8) & 0xFF)) & 0xFF];
+                r ^= (uint32_t)t4[13][(w[0] >> 16) & 0xFF] ^ t4[12][w[0] >> 24];
+#pragma unroll
+                for (int q = 1; q < 4; q++)
+                    r ^= (uint32_t)t4[15 - 4 * q][w[q] & 0xFF] ^ t4[14 - 4 * q][(w[q] >> 8) & 0xFF] ^
+                         t4[13 - 4 * q][(w[q] >> 16) & 0xFF] ^ t4[12 - 4 * q][w[q] >> 24];
+                crc = r;
+            };
+            for (; b + 128 <= stop && ((b + lead) & 127); b += 16) fold16(*reinterpret_cast<const uint4 *>(abase + b + lead));
             for (; b + 128 <= stop; b += 128) {
                 uint4 v[8];
 #pragma unroll
                 for (int u = 0; u < 8; u++) v[u] = *reinterpret_cast<const uint4 *>(abase + b + lead + 16 * u);
 #pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    fold4(v[u].x);
-                    fold4(v[u].y);
-                    fold4(v[u].z);
-                    fold4(v[u].w);
-                }
+                for (int u = 0; u < 8; u++) fold16(v[u]);
             }
-            for (; b + 16 <= stop; b += 16) {  // one 16-byte load per four dwords
-                const uint4 v = *reinterpret_cast<const uint4 *>(abase + b + lead);
-                fold4(v.x);
-                fold4(v.y);
-                fold4(v.z);
-                fold4(v.w);
-            }
+            for (; b + 16 <= stop; b += 16) fold16(*reinterpret_cast<const uint4 *>(abase + b + lead));
             for (; b + 4 <= stop; b += 4) fold4(*reinterpret_cast<const uint32_t *>(abase + b + lead));
             for (; b < stop; b++) crc = ((crc << 8) & 0xFFFFu) ^ t4[0][((crc >> 8) ^ blob[b]) & 0xFF];
             if (crc == (((uint32_t)blob[e - 2] << 8) | blob[e - 1])) {
