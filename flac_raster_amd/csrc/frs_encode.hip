@@ -1589,7 +1589,7 @@ __device__ inline uint32_t xpow8(uint64_t m) {  // x^(8m) mod P
 
 constexpr int kFrameWordsV3 = 2176;  // 69632 bits >= worst exact frame (estimate < verbatim)
 constexpr int kXpowBytes = kFrameWordsV3 * 4 + 64;  // multiple of 64 (LDS split tables)
-__constant__ uint16_t c_crc16x8[8][256];           // T_k[v] = CRC-16 of byte v followed by k zero bytes
+__constant__ uint16_t c_crc16x8[16][256];           // T_k[v] = CRC-16 of byte v followed by k zero bytes
 __device__ uint16_t g_xpow_bytes[kXpowBytes];      // x^(8m) mod P for m bytes
 __device__ uint16_t g_xpow_8k[32];                  // x^(8 * 8192 q) mod P
 // x^(8m) mod P for a byte count m: one table read below kXpowBytes, two reads and a multiply below 256 KiB (frames
@@ -2713,7 +2713,7 @@ constexpr int kBufWordsV3 = kFrameWordsV3 + 64;  // + the overflow row of the co
 struct EncV3Shared {
     uint32_t bits[4][kBufWordsV3];
     int16_t lut[kLutCap];
-    uint16_t crc8x[8][256];  // slice-by-8 tables (T_0..T_3 serve the slice-by-4 / byte steps)
+    uint16_t crc8x[16][256];  // slice-by-16 tables (T_0..T_3 serve the slice-by-4 / byte steps)
     uint16_t xlo[64];       // x^(8m) mod P, m = 0..63
     uint16_t xhi[kXpowHi];  // x^(8*64*m) mod P
     uint8_t crc8[256];
@@ -3572,6 +3572,14 @@ __device__ __forceinline__ void encode_frame_v3(const typename Elem<DT>::T *rast
         // latency chain, are halved), then one slice-by-4 step for an odd word
         const uint16_t(*T)[256] = S.crc8x;
         uint32_t i = wb;
+        for (; i + 3 < we; i += 4, colp += 256) {
+            const uint32_t w0 = colp[0], w1 = colp[64], w2 = colp[128], w3 = colp[192];
+            c = (uint32_t)T[15][((c >> 8) ^ (w0 >> 24)) & 0xFF] ^ T[14][((c & 0xFF) ^ (w0 >> 16)) & 0xFF] ^
+                T[13][(w0 >> 8) & 0xFF] ^ T[12][w0 & 0xFF] ^ T[11][w1 >> 24] ^ T[10][(w1 >> 16) & 0xFF] ^
+                T[9][(w1 >> 8) & 0xFF] ^ T[8][w1 & 0xFF] ^ T[7][w2 >> 24] ^ T[6][(w2 >> 16) & 0xFF] ^
+                T[5][(w2 >> 8) & 0xFF] ^ T[4][w2 & 0xFF] ^ T[3][w3 >> 24] ^ T[2][(w3 >> 16) & 0xFF] ^
+                T[1][(w3 >> 8) & 0xFF] ^ T[0][w3 & 0xFF];
+        }
         for (; i + 1 < we; i += 2, colp += 128) {
             const uint32_t w0 = colp[0], w1 = colp[64];
             c = (uint32_t)T[7][((c >> 8) ^ (w0 >> 24)) & 0xFF] ^ T[6][((c & 0xFF) ^ (w0 >> 16)) & 0xFF] ^
@@ -3632,7 +3640,7 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
     // with its own ticket counter; the look-back reaches into the previous launch's (inclusive) statuses
     __shared__ EncV3Shared S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int i = threadIdx.x; i < 2048; i += blockDim.x) (&S.crc8x[0][0])[i] = (&c_crc16x8[0][0])[i];
+    for (int i = threadIdx.x; i < 4096; i += blockDim.x) (&S.crc8x[0][0])[i] = (&c_crc16x8[0][0])[i];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) S.crc8[i] = c_crc8[i];
     for (int i = threadIdx.x; i < 64; i += blockDim.x) S.xlo[i] = g_xpow_bytes[i];
     for (int i = threadIdx.x; i < kXpowHi; i += blockDim.x) S.xhi[i] = g_xpow_bytes[64 * i];
@@ -3813,7 +3821,7 @@ __global__ void __launch_bounds__(256, PH1 ? 3 : 1) k_fused_v6(const typename El
     dbg_put(6, 3);
     // ---- phase 2: k_encode_v3's loop
     EncV3Shared &S = U.enc;
-    for (int i = threadIdx.x; i < 2048; i += blockDim.x) (&S.crc8x[0][0])[i] = (&c_crc16x8[0][0])[i];
+    for (int i = threadIdx.x; i < 4096; i += blockDim.x) (&S.crc8x[0][0])[i] = (&c_crc16x8[0][0])[i];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) S.crc8[i] = c_crc8[i];
     for (int i = threadIdx.x; i < 64; i += blockDim.x) S.xlo[i] = g_xpow_bytes[i];
     for (int i = threadIdx.x; i < kXpowHi; i += blockDim.x) S.xhi[i] = g_xpow_bytes[64 * i];
@@ -4116,10 +4124,10 @@ static int upload_tables(frs_ctx *ctx) {
     FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_crc16), t16, sizeof(t16), 0, hipMemcpyHostToDevice, ctx->stream));
     FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_xpow8), xp, sizeof(xp), 0, hipMemcpyHostToDevice, ctx->stream));
     // slice-by-8 tables: T_k[v] = T_{k-1}[v] advanced by one zero byte
-    static uint16_t t4[8][256];
+    static uint16_t t4[16][256];
     static uint16_t xb[kXpowBytes];
     for (int i = 0; i < 256; i++) t4[0][i] = t16[i];
-    for (int k = 1; k < 8; k++)
+    for (int k = 1; k < 16; k++)
         for (int i = 0; i < 256; i++) {
             const uint16_t c = t4[k - 1][i];
             t4[k][i] = (uint16_t)(((c << 8) & 0xFFFF) ^ t16[c >> 8]);
