@@ -3568,8 +3568,8 @@ __device__ __forceinline__ void encode_frame_v3(const typename Elem<DT>::T *rast
         const uint32_t wb = min(nfw, (uint32_t)lane * M.c), we = min(nfw, wb + M.c);
         uint32_t c = 0;
         const uint32_t *colp = fbuf + lane;
-        // slice-by-8 (two words per step: the table lookups that depend on the running CRC, and so the
-        // latency chain, are halved), then one slice-by-4 step for an odd word
+        // slice-by-16 (four words per step: only two of the step's 16 table lookups depend on the running CRC, so
+        // the latency chain is a quarter of slice-by-4's), then slice-by-8 / slice-by-4 steps for the last 1-3 words
         const uint16_t(*T)[256] = S.crc8x;
         uint32_t i = wb;
         for (; i + 3 < we; i += 4, colp += 256) {
@@ -4123,7 +4123,7 @@ static int upload_tables(frs_ctx *ctx) {
     FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_crc8), t8, sizeof(t8), 0, hipMemcpyHostToDevice, ctx->stream));
     FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_crc16), t16, sizeof(t16), 0, hipMemcpyHostToDevice, ctx->stream));
     FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(c_xpow8), xp, sizeof(xp), 0, hipMemcpyHostToDevice, ctx->stream));
-    // slice-by-8 tables: T_k[v] = T_{k-1}[v] advanced by one zero byte
+    // slice-by-16 tables: T_k[v] = T_{k-1}[v] advanced by one zero byte
     static uint16_t t4[16][256];
     static uint16_t xb[kXpowBytes];
     for (int i = 0; i < 256; i++) t4[0][i] = t16[i];
