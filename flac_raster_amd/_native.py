@@ -161,6 +161,21 @@ def _p(a: np.ndarray):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
+def _is_window_of(raster, desc) -> bool:
+    """True when `raster` is a strided numpy view ([bands][rows][cols] or [rows][cols]) whose element strides are the
+    descriptor's row_stride / band_stride: a window of a larger raster (cli.py:698-699, rasterio Window reads), passed
+    to the C-ABI by its origin pointer without a contiguous copy."""
+    if not isinstance(raster, np.ndarray) or raster.flags.c_contiguous or raster.ndim not in (2, 3):
+        return False
+    es = raster.dtype.itemsize
+    st = raster.strides
+    if st[-1] != es or any(x <= 0 or x % es for x in st):
+        return False
+    if st[-2] // es != desc.row_stride or raster.shape[-1] != desc.width or raster.shape[-2] != desc.height:
+        return False
+    return raster.ndim == 2 or (st[0] // es == desc.band_stride and raster.shape[0] >= desc.band0 + desc.nbands)
+
+
 class DeviceBuffer:
     """A device allocation owned by a Context (freed with it or on close())."""
 
@@ -200,17 +215,26 @@ class HostBuffer:
     into (no device buffer, no D2H copy).  `array` is its uint8 view; freed with close()."""
 
     def __init__(self, ctx: "Context", nbytes: int):
-        self.ctx = ctx
+        # a weak reference: the context caches one HostBuffer (Context._pin), and a strong one would make a cycle that
+        # keeps a dropped context's streams and device buffers alive until the cyclic GC runs
+        self._ctx = weakref.ref(ctx)
+        self.lib = ctx.lib
         self.nbytes = int(nbytes)
         self.ptr = ctx.lib.frs_host_malloc(ctx.handle, self.nbytes)
         if not self.ptr:
             raise FrsError(-2, ctx.last_error())  # FRS_E_HIP
         self.array = np.frombuffer((ctypes.c_uint8 * self.nbytes).from_address(self.ptr), dtype=np.uint8)
 
+    @property
+    def ctx(self):
+        return self._ctx()
+
     def close(self):
         if self.ptr:
             self.array = None
-            self.ctx.lib.frs_host_free(self.ctx.handle, self.ptr)
+            c = self._ctx()
+            # a buffer that outlived its context is freed without one (frs_host_free accepts a null context)
+            self.lib.frs_host_free(c.handle if c is not None and c.handle else None, self.ptr)
             self.ptr = None
 
     def __del__(self):
@@ -320,7 +344,7 @@ class Context:
                           ) -> Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray, int]:
         """Host-pointer encode.  Returns (arena uint8, tile_off int64[n+1], tile_min, tile_max, stream_bps).
         pinned=True: the arena is a view of the context's page-locked buffer (see pinned())."""
-        r = np.ascontiguousarray(raster)
+        r = raster if _is_window_of(raster, desc) else np.ascontiguousarray(raster)
         n = desc.tile_end - desc.tile_begin
         off = np.zeros(n + 1, dtype=np.int64)
         mn = np.zeros(max(n, 1), dtype=np.float64)

@@ -104,13 +104,6 @@ int frs_ctx_create(int device, frs_ctx **out) {
     ctx->force_generic = fg && fg[0] == '1';
     const char *dl = getenv("FRS_DECODE_LANE");
     ctx->decode_lane = dl ? (dl[0] == '1' ? 1 : 0) : -1;
-    if (const char *av = getenv("FRS_ANA_V5")) ctx->ana_v5 = atoi(av);
-    if (const char *ad = getenv("FRS_ANA_DBG")) ctx->ana_dbg = ad[0] == '1';
-    if (const char *fu = getenv("FRS_FUSED")) ctx->fused = atoi(fu);
-    if (const char *fk = getenv("FRS_FUSED_K")) ctx->fused_k = atoi(fk);
-    if (const char *p2 = getenv("FRS_PIPE2")) ctx->pipe2 = p2[0] == '1';
-    const char *es = getenv("FRS_ENC_SPLIT");
-    if (es) ctx->enc_split = std::max(1, std::min(8, atoi(es)));
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return FRS_E_HIP;
@@ -128,17 +121,13 @@ void frs_ctx_destroy(frs_ctx *ctx) {
     hipStreamSynchronize(ctx->stream);
     frs::prof_collect(ctx);
     DevBuf *bufs[] = {&ctx->tiles, &ctx->norms, &ctx->analysis, &ctx->slots, &ctx->frame_bytes, &ctx->frame_off,
-                      &ctx->window, &ctx->tile_sizes, &ctx->luts, &ctx->status, &ctx->frame_tile, &ctx->hdr_tab, &ctx->wave_tab, &ctx->plist, &ctx->ana_ctr, &ctx->ana_dbgbuf, &ctx->hand, &ctx->tile_flag, &ctx->ana_hand, &ctx->lpc_cand, &ctx->window_hi, &ctx->loose_assign, &ctx->loose_lead, &ctx->sub_slots, &ctx->sub_bits, &ctx->mc_bytes, &ctx->raster_stage, &ctx->arena_stage, &ctx->host_pack,
+                      &ctx->window, &ctx->tile_sizes, &ctx->luts, &ctx->status, &ctx->frame_tile, &ctx->hdr_tab, &ctx->wave_tab, &ctx->plist, &ctx->lpc_cand, &ctx->window_hi, &ctx->loose_assign, &ctx->loose_lead, &ctx->sub_slots, &ctx->sub_bits, &ctx->mc_bytes, &ctx->raster_stage, &ctx->arena_stage, &ctx->host_pack,
                       &ctx->dec_cand, &ctx->dec_count, &ctx->dec_pcm, &ctx->dec_soff, &ctx->dec_next, &ctx->dec_status, &ctx->dec_fb, &ctx->dec_sel,
                       &ctx->dec_chass};
     for (DevBuf *b : bufs) b->release();
     ctx->pin.release();
     ctx->ring[0].release();
     ctx->ring[1].release();
-    if (ctx->aux_stream) hipStreamSynchronize(ctx->aux_stream);
-    for (hipEvent_t e : ctx->split_ev)
-        if (e) hipEventDestroy(e);
-    if (ctx->aux_stream) hipStreamDestroy(ctx->aux_stream);
     if (ctx->h2d_stream) hipStreamDestroy(ctx->h2d_stream);
     if (ctx->d2h_stream) hipStreamDestroy(ctx->d2h_stream);
     hipStreamDestroy(ctx->stream);

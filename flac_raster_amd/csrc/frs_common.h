@@ -78,7 +78,6 @@ struct EncodeParams {
     int32_t ncand;        // LPC candidates per coded signal from k_analyze_lpc_hi (subdivide_tukey levels), 0 = the
                           // single tukey(0.5) candidate of the SubAnalysis
     int32_t loose_frames; // loose mid/side (levels 1 / 4 on two channels): frames per evaluation, 0 = exhaustive
-    int32_t dbg;          // $FRS_ANA_DBG: diagnostics printf of the fused kernel
 };
 
 // libFLAC compression-level table (docs/sonos-pyflac.txt:6926-6934): mid/side, loose mid/side, max LPC order, max

@@ -1495,25 +1495,7 @@ __device__ inline void lds_publish(volatile int32_t *p, int32_t v) {
 }
 __device__ inline int32_t lds_poll(volatile int32_t *p) { return *p; }
 
-// NB = 2: the producer's Rice decode split between a resolver (wave 0) and NB builder waves (2, 3).  Windows sit at fixed
-// strides of kPipeStride bits from the partition's first code, so a window's jump tables do not depend on where the
-// previous window's chain ended: the builders fill a ring of kPipeSlots table sets ahead of the resolver (up to the
-// window it requested), and the resolver only walks each window's chain from its entry (six dependent LDS reads per
-// 64 codes) and decodes the values.  Window tables are tagged (partition generation, window) and the ring is reused
-// only for windows the resolver has left behind (requests reach at most kPipeSlots - 1 windows ahead); every wait is
-// on LDS state of the work-group and bounded.
-constexpr int kPipeStride = 896, kPipeSlots = 4, kPipeAhead = kPipeSlots - 1;
-struct PipeCtl {
-    int32_t gen;       // partition generation of the builders' windows (-1: none yet)
-    uint32_t p0;       // stage bit of the generation's first code (window n starts at p0 + n kPipeStride)
-    int32_t kp;        // its Rice parameter
-    int32_t req;       // windows 0..req of the generation may be built
-    int32_t done;      // builders exit
-    int32_t tag[kPipeSlots];  // (gen << 16) | window of the tables in each slot
-};
-
-template <int NB = 0>
-__global__ void __launch_bounds__(64 * (2 + NB)) k_decode_frames_pipe(const uint8_t *blob, const int64_t *soff, int ns,
+__global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob, const int64_t *soff, int ns,
                                                            const int64_t *poff, const int64_t *cpos,
                                                            const int64_t *ends, const int64_t *fbase,
                                                            const int64_t *frame_cand, int64_t nframes, int channels,
@@ -1532,8 +1514,6 @@ __global__ void __launch_bounds__(64 * (2 + NB)) k_decode_frames_pipe(const uint
         int32_t fb[kDecResMax];
     };
     __shared__ __attribute__((aligned(16))) PipeU pu;
-    __shared__ __attribute__((aligned(16))) uint16_t jtr[NB ? kPipeSlots : 1][NB ? 6 : 1][NB ? kJumpN : 1];
-    __shared__ PipeCtl ctl;
     uint32_t *xout = pu.p.xout;
     uint16_t(*jt)[kJumpN] = pu.p.jt;
     const int64_t fi = blockIdx.x;
@@ -1553,17 +1533,6 @@ __global__ void __launch_bounds__(64 * (2 + NB)) k_decode_frames_pipe(const uint
         info.progress = 0;
         info.finished = 0;
         info.valid = 0;
-        ctl.gen = -1;
-        ctl.req = -1;
-        ctl.done = 0;
-    }
-    if constexpr (NB > 0) {
-        if (threadIdx.x < kPipeSlots) ctl.tag[threadIdx.x] = -1;
-        // table entries past a window's candidates are fixed points (every slot, every level)
-        for (int e = threadIdx.x; e < kPipeSlots * 6 * 128; e += blockDim.x) {
-            const int c = kRiceWinBits + (e & 127);
-            jtr[e / (6 * 128)][(e / 128) % 6][c] = (uint16_t)c;
-        }
     }
     __syncthreads();
     const int64_t nsamp = poff[s + 1] - poff[s];
@@ -1592,7 +1561,6 @@ __global__ void __launch_bounds__(64 * (2 + NB)) k_decode_frames_pipe(const uint
                 info.valid = valid;
                 lds_publish(&vi->finished, 1);
                 if (st) lds_publish(&vi->state, st);
-                if (NB) lds_publish(&ctl.done, 1);  // (the builders exit)
             }
         };
         if (!staged) {
@@ -1721,109 +1689,6 @@ __global__ void __launch_bounds__(64 * (2 + NB)) k_decode_frames_pipe(const uint
             jt[k][kRiceWinBits + lane] = (uint16_t)(kRiceWinBits + lane);
             jt[k][kRiceWinBits + 64 + lane] = (uint16_t)(kRiceWinBits + 64 + lane);
         }
-        if constexpr (NB > 0) {
-            // ---- resolver: partition by partition; inside one, windows at fixed strides from its first code whose
-            //      jump tables the builders fill ahead; the chain is walked from each window's entry
-            volatile PipeCtl *vc = &ctl;
-            uint32_t H = P;  // stage bit of the next partition's parameter field
-            for (int p = 0; p < (1 << po) && !bad; p++) {
-                br.seek(H);
-                const int kp = (int)br.bits(pb);
-                int left = psz - (p == 0 ? o : 0);
-                uint32_t E = br.pos();
-                if (kp == esc) {  // escaped partition: fixed-width residuals, no builders
-                    const int nb = (int)br.bits(5);
-                    for (int j = 0; j < left; j++, i++) {
-                        const int32_t r = nb ? br.sbits(nb) : 0;
-                        if (lane == 0) resbuf[i] = r;
-                    }
-                    H = br.pos();
-                    publish();
-                    continue;
-                }
-                const uint32_t P0 = E;
-                if (lane == 0) {
-                    vc->p0 = P0;
-                    vc->kp = kp;
-                    vc->req = kPipeAhead;
-                    lds_publish(&vc->gen, p);
-                }
-                while (left > 0 && !bad) {
-                    if (E > lim) {
-                        bad = true;
-                        break;
-                    }
-                    const int n = (int)((E - P0) / (uint32_t)kPipeStride);
-                    const uint32_t Sn = P0 + (uint32_t)n * (uint32_t)kPipeStride;
-                    if (lane == 0 && n + kPipeAhead > vc->req) vc->req = n + kPipeAhead;
-                    const int slot = n % kPipeSlots, want = (p << 16) | n;
-                    for (long spin = 0; vc->tag[slot] != want; spin++) {
-                        if (spin > (1l << 24)) {  // (never: a builder always reaches a requested window)
-                            bad = true;
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                    if (bad) break;
-                    __asm__ volatile("" ::: "memory");  // table reads stay behind the tag
-                    const uint16_t(*T)[kJumpN] = jtr[slot];
-                    int e = (int)(E - Sn);
-                    while (left > 0 && e < kPipeStride) {
-                        const int cap = left < 64 ? left : 64;
-                        int posv = e;
-#pragma unroll
-                        for (int k = 0; k < 6; k++) {
-                            const int nx = T[k][posv];
-                            posv = ((lane >> k) & 1) ? nx : posv;
-                        }
-                        const int nxt = T[0][posv];
-                        const uint64_t chain = __ballot(posv < kPipeStride && nxt != posv && lane < cap);
-                        const int cnt = __builtin_popcountll(chain);
-                        int cur;
-                        bool lng = false;
-                        if (cnt < cap) {  // stopped at a long code inside the window, or left it
-                            cur = __builtin_amdgcn_readlane(posv, cnt);
-                            lng = cur < kPipeStride;
-                        } else {
-                            cur = __builtin_amdgcn_readlane(nxt, cnt - 1);
-                        }
-                        {
-                            const uint32_t bc = Sn + (uint32_t)posv, wc = min(bc >> 5, (uint32_t)(we - wb + 2));
-                            const uint32_t x0 = stage[wc], x1 = stage[wc + 1], x2 = stage[wc + 2], sft = bc & 31u;
-                            const uint32_t hi = sft ? __builtin_amdgcn_alignbit(x0, x1, 32u - sft) : x0;
-                            const uint32_t lo = sft ? __builtin_amdgcn_alignbit(x1, x2, 32u - sft) : x1;
-                            const uint64_t win = ((uint64_t)hi << 32) | lo;
-                            const int z = win ? __builtin_clzll(win) : 64;
-                            const uint32_t low = kp ? (uint32_t)((win << (z + 1)) >> (64 - kp)) : 0u;
-                            const uint32_t u = ((uint32_t)z << kp) | low;
-                            if (lane < cnt) resbuf[i + lane] = (int32_t)((u >> 1) ^ (uint32_t)(-(int32_t)(u & 1)));
-                        }
-                        const int i0 = i;
-                        i += cnt;
-                        left -= cnt;
-                        e = cur;
-                        if (lng) {  // a long unary run: one code through the scalar reader
-                            br.seek(Sn + (uint32_t)cur);
-                            uint32_t q;
-                            if (!br.unary(q, lim)) {
-                                bad = true;
-                                break;
-                            }
-                            const uint32_t uu = (q << kp) | br.bits(kp);
-                            if (lane == 0) resbuf[i] = (int32_t)((uu >> 1) ^ (uint32_t)(-(int32_t)(uu & 1)));
-                            i++;
-                            left--;
-                            e = (int)(br.pos() - Sn);
-                        }
-                        if ((i0 >> 6) != (i >> 6) || left == 0) publish();
-                    }
-                    E = Sn + (uint32_t)e;
-                }
-                H = E;
-            }
-            if (lane == 0) lds_publish(&vc->done, 1);
-            P = H;
-        } else
         for (int p = 0; p < (1 << po) && !bad; p++) {
             br.seek(P);
             const int kp = (int)br.bits(pb);
@@ -1946,75 +1811,6 @@ __global__ void __launch_bounds__(64 * (2 + NB)) k_decode_frames_pipe(const uint
             lds_publish(&vi->finished, 1);
         }
         return;
-    }
-    if constexpr (NB > 0) {
-        if (wave >= 2) {
-            // ================= builders: jump tables of the windows the resolver requested, b, b + NB, ...
-            const int b = wave - 2;
-            volatile PipeCtl *vc = &ctl;
-            int my_gen = -1, n = b, k1 = 1;
-            uint32_t P0 = 0;
-            const uint32_t wlim = (uint32_t)(we - wb + 2 * kRiceWinQ);  // last stage word a window may read
-            for (long spin = 0; spin < (1l << 24);) {
-                if (vc->done) return;
-                const int g = vc->gen;
-                if (g < 0) {
-                    __builtin_amdgcn_s_sleep(1);
-                    spin++;
-                    continue;
-                }
-                if (g != my_gen) {
-                    my_gen = g;
-                    n = b;
-                    P0 = vc->p0;
-                    k1 = vc->kp + 1;
-                }
-                if (n > vc->req) {
-                    __builtin_amdgcn_s_sleep(1);
-                    spin++;
-                    continue;
-                }
-                spin = 0;
-                const int slot = n % kPipeSlots;
-                uint16_t(*T)[kJumpN] = jtr[slot];
-                const uint32_t Sn = P0 + (uint32_t)n * (uint32_t)kPipeStride;
-                const uint32_t bb = Sn + (uint32_t)(kRiceWinQ * lane), wi = min(bb >> 5, wlim), sh = bb & 31u;
-                const uint64_t wA = ((uint64_t)stage[wi] << 32) | stage[wi + 1];
-                const uint64_t wB = ((uint64_t)stage[wi + 2] << 32) | stage[wi + 3];
-                int jq[kRiceWinQ];
-#pragma unroll
-                for (int t = 0; t < kRiceWinQ; t++) {
-                    const uint32_t s2 = sh + (uint32_t)t;
-                    const uint64_t win = s2 ? (wA << s2) | (wB >> (64u - s2)) : wA;
-                    const int tot = (win ? __builtin_clzll(win) : 64) + k1;
-                    const int c = kRiceWinQ * lane + t;
-                    jq[t] = (c < kPipeStride && tot <= 64) ? c + tot : c;  // past the stride: fixed points
-                }
-                auto store_run = [&](uint16_t *row) {
-#pragma unroll
-                    for (int v = 0; v < kRiceWinQ / 8; v++) {
-                        uint4 u;
-                        u.x = (uint32_t)jq[8 * v] | ((uint32_t)jq[8 * v + 1] << 16);
-                        u.y = (uint32_t)jq[8 * v + 2] | ((uint32_t)jq[8 * v + 3] << 16);
-                        u.z = (uint32_t)jq[8 * v + 4] | ((uint32_t)jq[8 * v + 5] << 16);
-                        u.w = (uint32_t)jq[8 * v + 6] | ((uint32_t)jq[8 * v + 7] << 16);
-                        reinterpret_cast<uint4 *>(row + kRiceWinQ * lane)[v] = u;
-                    }
-                };
-                store_run(T[0]);
-#pragma unroll
-                for (int k = 0; k < 5; k++) {
-#pragma unroll
-                    for (int q = 0; q < kRiceWinQ; q++) jq[q] = T[k][jq[q]];
-                    store_run(T[k + 1]);
-                }
-                __builtin_amdgcn_s_waitcnt(0xC07F);
-                __builtin_amdgcn_wave_barrier();
-                if (lane == 0) vc->tag[slot] = (g << 16) | n;
-                n += NB;
-            }
-            return;
-        }
     }
     // ================= consumer (wave 1): LPC / FIXED restore behind the producer
     int st;
@@ -2912,19 +2708,11 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         k_decode_frames_wave_list<<<(unsigned)std::min<int64_t>(frames, 4 * (int64_t)ctx->num_cus), 64, 0, st>>>(
             blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, dchain, channels, bps, pcm_dev, blocksize, nvalid,
             dout, fbl, fbc);
-    } else if (pipe)
-    {
-        // $FRS_PIPE2: the Rice decode split between a resolver and two table-building waves (k_decode_frames_pipe<2>)
-        if (ctx->pipe2)
-            k_decode_frames_pipe<2><<<(unsigned)frames, 256, 0, st>>>(blob_dev, dsoff, nstreams, dpoff, cpos, ends,
-                                                                      dfbase, dchain, frames, channels, bps, pcm_dev,
-                                                                      blocksize, nvalid, dout);
-        else
-            k_decode_frames_pipe<0><<<(unsigned)frames, 128, 0, st>>>(blob_dev, dsoff, nstreams, dpoff, cpos, ends,
-                                                                      dfbase, dchain, frames, channels, bps, pcm_dev,
-                                                                      blocksize, nvalid, dout);
-    }
-    else
+    } else if (pipe) {
+        k_decode_frames_pipe<<<(unsigned)frames, 128, 0, st>>>(blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase,
+                                                               dchain, frames, channels, bps, pcm_dev, blocksize, nvalid,
+                                                               dout);
+    } else
         k_decode_frames_wave<<<(unsigned)frames, 64, 0, st>>>(blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase,
                                                               dchain, frames, channels, bps, pcm_dev, blocksize, nvalid,
                                                               dout);

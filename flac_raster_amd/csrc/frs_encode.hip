@@ -809,8 +809,10 @@ __global__ void __launch_bounds__(128) k_analyze_lpc_hi(const typename Elem<DT>:
             k++;
             if (b >= 3) {
                 if (!skip) {
+                    // libFLAC 1.4.3 apply_apodization_: lags 0 .. max_order - 1 are root - partial, lag max_order keeps
+                    // the partial window's value (its loop and autoc_root memcpy stop below max_order)
 #pragma unroll
-                    for (int l = 0; l <= kMaxLpcHi; l++) ac[l] = root[l] - ac[l];
+                    for (int l = 0; l < kMaxLpcHi; l++) ac[l] = l < max_order ? root[l] - ac[l] : ac[l];
                     lpc_candidate<kMaxLpcHi>(ac, max_order, n, sbps, P, c);
                     out[k] = c;
                 }
@@ -2340,177 +2342,6 @@ __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *
     out[f * P.nch + chn] = analysis_finish(acc, or_acc, n, P, ft);
 }
 
-// ------------------------------------------------------------------------------ k_analyze_v5
-// Role-split analysis inside one work-group (16-bit mono streams, one wave per tile, 16-B aligned rows): the same
-// per-tile work as k_analyze_v3<DT, false, true>, but the HBM-bound min/max pass leaves the slots of the fp64-bound
-// autocorrelation.  In v3 every wave read its tile for min/max before its sums (C4: 437 us of stats against 402 us of
-// sums per wave, ~2000 of the 4096 slots in a stats pass at any moment, a 330 us start-up burst with the VALU idle).
-// A work-group here is 8 waves: waves 4..7 ("producers") claim tiles from a global counter, compute each tile's
-// min/max and normalisation, write its parameters and LUT to HBM for the encoder and its LUT into an LDS slot, and
-// post the slot; waves 0..3 ("consumers") take the posted slots in order and run ana_autoc on them.  Every wait is
-// on LDS state of the same work-group, so no wave ever waits on another work-group (no cross-WG progress assumption,
-// no epochs).  Ring protocol (kV5Slots slots, item i in slot i % kV5Slots, items numbered by two LDS counters):
-//   producer of item i: waits until slot.seq == i - kV5Slots has been consumed (done == i - kV5Slots + 1 ... i.e. the
-//   slot's `free` tag equals i), fills it, then publishes seq = i (release);
-//   consumer of item i: waits for seq == i (acquire), works, then sets free = i + kV5Slots (release).
-// A producer whose global claim is past the last tile posts an end marker (tile -1) and exits: four producers post
-// exactly four markers, one for each consumer.  A slow-class tile (fast / exact division) is not posted (its
-// parameters go to HBM; k_analyze_v3<DT, true> analyses it) and the producer claims another tile for the same item.
-constexpr int kV5Slots = 8;
-struct V5Slot {
-    TileNorm tn;
-    int tile;  // -1: end marker
-    int seq;   // item number posted in this slot (-1: none yet)
-    int free;  // item number the slot may take next
-    int pad;
-};
-// NC consumer and NP producer waves per work-group (NC a multiple of NP: each producer posts NC / NP end markers);
-// dbg (optional, $FRS_ANA_DBG): wave-cycle totals [consumer wait, consumer sums, items, producer stats, producer slot
-// wait, items].
-template <int DT, int NC = 4, int NP = 4, bool DBG = false>
-__global__ void __launch_bounds__(64 * (NC + NP), 4) k_analyze_v5(const typename Elem<DT>::T *raster, EncodeParams P,
-                                                      const TileGeom *tiles, TileNorm *norms, int16_t *luts,
-                                                      const float *__restrict__ window, SubAnalysis *out, int ntiles,
-                                                      int *tile_ctr, int *err, unsigned long long *dbg = nullptr) {
-    static_assert(NC % NP == 0 && NC + NP <= kV5Slots, "end markers / slots");
-    static_assert(sizeof(typename Elem<DT>::T) == 2 && !Elem<DT>::is_float, "16-bit samples");
-    __shared__ int16_t slut[kV5Slots][kLutCap];
-    __shared__ V5Slot slot[kV5Slots];
-    __shared__ int ctr[2];  // items taken by producers / by consumers
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (threadIdx.x < kV5Slots) {
-        slot[threadIdx.x].seq = -1;
-        slot[threadIdx.x].free = threadIdx.x;
-    }
-    if (threadIdx.x < 2) ctr[threadIdx.x] = 0;
-    __syncthreads();
-    auto lds_wait = [&](const int *addr, int want) {  // spin on an LDS word of this work-group until it equals want
-        for (long spin = 0;; spin++) {
-            int v = 0;
-            if (lane == 0) v = __hip_atomic_load(addr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (__builtin_amdgcn_readfirstlane(v) == want) return true;
-            if (spin > (1l << 26)) {  // (never: every posted item is consumed, every slot is freed in order)
-                if (lane == 0) atomicOr(err, 64);
-                return false;
-            }
-            if (spin < 64) __builtin_amdgcn_s_sleep(1);
-            else __builtin_amdgcn_s_sleep(8);
-        }
-    };
-    auto take = [&](int k) {
-        int i = 0;
-        if (lane == 0) i = atomicAdd(&ctr[k], 1);
-        return __builtin_amdgcn_readfirstlane(i);
-    };
-    uint64_t tw = 0, tb = 0, nit = 0;  // (dbg) wait cycles, busy cycles, items
-    auto dbg_flush = [&](int base) {
-        if (DBG && lane == 0) {
-            atomicAdd(&dbg[base], (unsigned long long)tw);
-            atomicAdd(&dbg[base + 1], (unsigned long long)tb);
-            atomicAdd(&dbg[base + 2], (unsigned long long)nit);
-        }
-    };
-    if (wave >= NC) {
-        // ---- producer
-        int ends_left = NC / NP;  // end markers this producer posts once the tiles are out
-        while (true) {
-            const int i = take(0);
-            uint64_t t0 = DBG ? __builtin_amdgcn_s_memtime() : 0;
-            V5Slot &sl = slot[i % kV5Slots];
-            int t;
-            TileNorm tn;
-            while (true) {  // the next tile the consumers analyse here (slow-class tiles only get their parameters)
-                int tq = 0;
-                if (lane == 0) tq = atomicAdd(tile_ctr, 1);
-                t = __builtin_amdgcn_readfirstlane(tq);
-                if (t >= ntiles) break;
-                const TileGeom g = tiles[t];
-                const typename Elem<DT>::T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
-                wave_tile_minmax<DT>(base, P.row_stride, g, lane, tn.imin, tn.imax);
-                tile_norm_finalize<DT>(tn, P.norm_mode, P.scale_bits);
-                if (lane == 0) norms[t] = tn;
-                const int nfull = g.nframes - (g.partial ? 1 : 0);
-                if ((tn.mode == kNormLut || tn.mode == kNormZero) && nfull > 0) break;
-            }
-            uint64_t t1 = DBG ? __builtin_amdgcn_s_memtime() : 0;
-            tb += t1 - t0;
-            if (!lds_wait(&sl.free, i)) return;  // the slot's previous item has been consumed
-            if (DBG) {
-                const uint64_t t2 = __builtin_amdgcn_s_memtime();
-                tw += t2 - t1;
-                t1 = t2;
-            }
-            if (t < ntiles && tn.mode == kNormLut) {
-                int16_t *glut = luts + (int64_t)t * kLutCap;
-                int16_t *wl = slut[i % kV5Slots];
-                const int64_t R = tn.imax - tn.imin;
-                for (int64_t d = lane; d <= R; d += 64) {
-                    const int16_t e = lut_entry<DT>(tn, d);
-                    wl[d] = e;
-                    glut[d] = e;
-                }
-            }
-            if (lane == 0) {
-                sl.tn = tn;
-                sl.tile = t < ntiles ? t : -1;
-            }
-            __builtin_amdgcn_s_waitcnt(0xC07F);  // the slot's LUT and parameters have landed in LDS
-            if (lane == 0) __hip_atomic_store(&sl.seq, i, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (DBG) {
-                tb += __builtin_amdgcn_s_memtime() - t1;
-                nit++;
-            }
-            if (t >= ntiles && --ends_left == 0) {  // end markers posted
-                dbg_flush(3);
-                return;
-            }
-        }
-    }
-    // ---- consumer
-    while (true) {
-        const int i = take(1);
-        V5Slot &sl = slot[i % kV5Slots];
-        const uint64_t t0 = DBG ? __builtin_amdgcn_s_memtime() : 0;
-        if (!lds_wait(&sl.seq, i)) return;
-        const uint64_t t1 = DBG ? __builtin_amdgcn_s_memtime() : 0;
-        tw += t1 - t0;
-        const int t = sl.tile;
-        if (t < 0) {
-            dbg_flush(0);
-            return;
-        }
-        const TileNorm tn = sl.tn;
-        const TileGeom g = tiles[t];
-        const typename Elem<DT>::T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
-        const int nfull = g.nframes - (g.partial ? 1 : 0);
-        const bool live = lane < nfull;
-        const int64_t fk = live ? lane : nfull - 1;  // dead lanes re-read the tile's last full frame
-        const int64_t f = g.frame_base + fk;
-        const int64_t s0 = fk * P.blocksize;
-        const int64_t tile_px = (int64_t)g.h * g.w;
-        const int n = live ? (int)min((int64_t)P.blocksize, tile_px - s0) : 0;
-        constexpr int kChunk = 64;
-        const int vec = (g.w % kChunk) == 0 ? P.vec_ok : 0;
-        double acc[kMaxLpc + 1];
-#pragma unroll
-        for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
-        uint32_t or_acc = 0, ft[5];
-        const int16_t *wl = slut[i % kV5Slots];
-        const int16_t *glut = luts + (int64_t)t * kLutCap;
-        if (tn.mode == kNormLut)
-            ana_autoc<DT, kAnaKindLds, kChunk>(base, P, g, s0, tn, wl, glut, window, vec, acc, or_acc, ft);
-        else
-            ana_autoc<DT, kAnaKindZero, kChunk>(base, P, g, s0, tn, wl, glut, window, vec, acc, or_acc, ft);
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's reads of the slot are done
-        if (lane == 0) __hip_atomic_store(&sl.free, i + kV5Slots, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (live) out[f] = analysis_finish(acc, or_acc, n, P, ft);
-        if (DBG) {
-            tb += __builtin_amdgcn_s_memtime() - t1;
-            nit++;
-        }
-    }
-}
-
 // ---- wave helpers (64 lanes)
 __device__ inline uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
@@ -2808,75 +2639,6 @@ __device__ inline void lut_gather_pairs(const uint32_t *w, const int16_t *lut, i
 
 __device__ inline uint32_t zigzag(int32_t r) { return ((uint32_t)r << 1) ^ (uint32_t)(r >> 31); }
 
-// ---- hand-off between the work-groups of one launch (k_fused_v6): the analysis wave stores a tile's parameters,
-// LUT and frame analyses with sc1 stores (relaxed agent-scope atomics), waits for them (vmcnt(0)) and sets the
-// tile's flag to the launch's epoch with an sc1 store; every read of those bytes on the encoder side is an sc1 load
-// behind a matched sc1 poll of the flag (MI355X_MICROARCH.md, inter-workgroup visibility: the sc1 form, no L1 copy).
-struct TileHand {
-    TileNorm tn;
-    uint8_t pad[128 - sizeof(TileNorm)];  // the LUT starts on a line of its own
-    int16_t lut[kLutCap];
-};
-static_assert(sizeof(TileNorm) % 4 == 0 && sizeof(SubAnalysis) % 4 == 0 && sizeof(TileNorm) <= 128, "sc1 units");
-// a frame's analysis in the hand-off: one per 128-B line (frames of two tiles never share a line)
-constexpr int kAnaHandStride = 128;
-static_assert(sizeof(SubAnalysis) <= kAnaHandStride, "analysis line");
-__device__ inline SubAnalysis *ana_hand(SubAnalysis *base, int64_t f) {
-    return reinterpret_cast<SubAnalysis *>(reinterpret_cast<char *>(base) + f * kAnaHandStride);
-}
-template <typename S> using Sc1Unit = std::conditional_t<sizeof(S) % 8 == 0, uint64_t, uint32_t>;
-template <typename S> __device__ inline void sc1_store(S *dst, const S &v) {
-    using U = Sc1Unit<S>;
-    const U *src = reinterpret_cast<const U *>(&v);
-    U *d = reinterpret_cast<U *>(dst);
-#pragma unroll
-    for (int i = 0; i < (int)(sizeof(S) / sizeof(U)); i++)
-        __hip_atomic_store(d + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <typename S> __device__ inline S sc1_load(const S *src) {
-    using U = Sc1Unit<S>;
-    S v;
-    U *d = reinterpret_cast<U *>(&v);
-    U *q = reinterpret_cast<U *>(const_cast<S *>(src));
-#pragma unroll
-    for (int i = 0; i < (int)(sizeof(S) / sizeof(U)); i++)
-        d[i] = __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return v;
-}
-// a wave-uniform struct with ONE vector load: lane i reads dword i, then v_readlane per dword (SGPRs)
-template <typename S> __device__ inline S sc1_load_lanes(const S *src) {
-    constexpr int n = (int)(sizeof(S) / 4);
-    static_assert(sizeof(S) % 4 == 0 && n <= 64, "dwords");
-    uint32_t *q = reinterpret_cast<uint32_t *>(const_cast<S *>(src));
-    const int lane = (int)(threadIdx.x & 63);
-    const uint32_t mine = __hip_atomic_load(q + (lane < n ? lane : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    S v;
-    uint32_t *d = reinterpret_cast<uint32_t *>(&v);
-#pragma unroll
-    for (int i = 0; i < n; i++) d[i] = (uint32_t)__builtin_amdgcn_readlane((int)mine, i);
-    return v;
-}
-// (wave-uniform) poll a tile's flag until it holds this launch's epoch; the analysis of every tile is claimed by a
-// running wave before any encoder work-group starts, so the wait is bounded by one tile's analysis.  Flags sit one
-// per 128-B line (kFlagStride) and pollers back off to ~3 us: a small job's dozens of encoder work-groups polling a
-// few flags on one line flooded that line's memory channel and stalled the analysis waves' own loads behind them.
-constexpr int kFlagStride = 32;
-__device__ inline void wait_tile(const uint32_t *flags, int tile, uint32_t epoch, int *err) {
-    uint32_t *flag = const_cast<uint32_t *>(flags) + (size_t)tile * kFlagStride;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();  // 100 MHz
-    for (int spin = 0;; spin++) {
-        const uint32_t v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__builtin_amdgcn_readfirstlane(v) == epoch) return;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s (a tile's analysis takes ~1 ms)
-            if ((threadIdx.x & 63) == 0) atomicOr(err, 32);
-            return;
-        }
-        if (spin < 8) __builtin_amdgcn_s_sleep(8);
-        else if (spin < 32) __builtin_amdgcn_s_sleep(32);
-        else __builtin_amdgcn_s_sleep(127);
-    }
-}
-
 struct PendingFrame {  // a frame whose bytes sit in the wave's bit buffer, offset not yet resolved
     int64_t f = -1;
     uint64_t fbytes = 0;
@@ -2913,7 +2675,7 @@ __device__ inline uint32_t frame_header_bytes(uint32_t v, int srx) {
 
 // Offset of a finished frame (decoupled look-back), inclusive publish, store of its bytes from the wave's
 // bit buffer, and re-zeroing of that buffer.
-// (forced inline: in the larger k_fused_v6 the inliner otherwise emitted real calls with scratch arguments)
+// (forced inline: the inliner otherwise emitted real calls with scratch arguments)
 __device__ __forceinline__ void resolve_and_store(const EncodeParams &P, PendingFrame &pf, uint32_t *fbuf, uint8_t *arena,
                                          int64_t arena_cap, int64_t *frame_off, uint64_t *status, int *err, int lane) {
     const int64_t f = pf.f;
@@ -3074,21 +2836,19 @@ __device__ inline uint32_t fixed_lane_sum(const uint32_t *E, bool l0) {
 // SUB = true (multi-channel streams, >= 3 independent channels): the wave codes ONE subframe (channel chn of frame f)
 // from bit 0 of its buffer -- no frame header, no look-back, no CRC -- and stores its words to sub_slots[f * nch +
 // chn] with its bit length in sub_bits; k_mc_assemble joins a frame's subframes behind the frame header.
-template <int DT, bool SUB = false, bool COH = false>
+template <int DT, bool SUB = false>
 __device__ __forceinline__ void encode_frame_v3(const typename Elem<DT>::T *raster, const EncodeParams &P,
                                        const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
                                        const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap, int64_t *frame_off,
                                        uint64_t *status, int *err, EncV3Shared &S, int want, int64_t f, int lane,
                                        const int32_t *ftile, PendingFrame &prev, const uint4 *hdr_tab, int hdr_n,
                                        const uint32_t *pslots, const int64_t *pbytes, int chn = 0,
-                                       uint32_t *sub_slots = nullptr, int32_t *sub_bits = nullptr,
-                                       const TileNorm *coh_tn = nullptr, const SubAnalysis *coh_a = nullptr,
-                                       const int32_t *coh_q = nullptr, bool coh_sc1 = false) {
+                                       uint32_t *sub_slots = nullptr, int32_t *sub_bits = nullptr) {
     using T = typename Elem<DT>::T;
     uint32_t *fbuf = S.bits[threadIdx.x >> 6];
     const int t = ftile[f];
     const TileGeom g = tiles[t];
-    if (!SUB && !COH && g.partial && f - g.frame_base == g.nframes - 1) {
+    if (!SUB && g.partial && f - g.frame_base == g.nframes - 1) {
         // (wave-uniform) the tile's partial last frame: already coded and sealed by the generic kernels, so it
         // only joins the look-back chain -- publish its size, finish the previous frame, and stage its bytes in
         // the bit buffer for resolve_and_store like a frame coded here
@@ -3115,9 +2875,7 @@ __device__ __forceinline__ void encode_frame_v3(const typename Elem<DT>::T *rast
         prev.map = M;
         return;
     }
-    // COH (k_fused_v6): the caller loaded the tile's parameters, the frame's analysis and the lane's coefficient
-    // (from the hand-off or from k_analyze_v3's output): no second load path in here
-    TileNorm tn = COH ? *coh_tn : norms[t];
+    TileNorm tn = norms[t];
     // the WG's LDS LUT belongs to tile `want`; a frame of another tile takes the exact division instead
     if (t != want && tn.mode == kNormLut) tn.mode = kNormSlow;
     const int16_t *lut = S.lut;
@@ -3129,7 +2887,7 @@ __device__ __forceinline__ void encode_frame_v3(const typename Elem<DT>::T *rast
     const int64_t s0 = fk * kMaxBlock;
     constexpr int n = kMaxBlock;
     const int64_t sub = SUB ? f * P.nch + chn : f;
-    const SubAnalysis A = COH ? *coh_a : ana[sub];
+    const SubAnalysis A = ana[sub];
     const int w = A.wasted;
     const int sbps = 16 - w;
     const T *base = raster + (int64_t)(P.band0 + chn) * P.band_stride + g.r0 * P.row_stride + g.c0;
@@ -3510,10 +3268,7 @@ __device__ __forceinline__ void encode_frame_v3(const typename Elem<DT>::T *rast
         w01 = (i >> 1) == 3 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 3], 0) : w01;
         const uint32_t xi = (i & 1) ? (w01 >> 16) : (w01 & 0xFFFFu);
         // (a lane-indexed load: a select chain over A.q costs registers)
-        const int32_t qi = !COH ? ana[sub].q[i]
-                           : coh_sc1 ? __hip_atomic_load(const_cast<int32_t *>(coh_q + i), __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT)
-                                     : coh_q[i];
+        const int32_t qi = ana[sub].q[i];
         const bool warm = lane < 8 && i < o, coef = type == 3 && lane >= 8 && lane < 16 && i < o;
         if (warm)
             lds_put_bits2(fbuf, M, pos0 + (uint32_t)i * sbps, xi & ((1u << sbps) - 1u), sbps);
@@ -3635,9 +3390,7 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
                                                   const int32_t *__restrict__ ftile, const uint4 *__restrict__ hdr_tab,
                                                   int hdr_n, const uint32_t *__restrict__ pslots,
                                                   const int64_t *__restrict__ pbytes, uint32_t *sub_slots = nullptr,
-                                                  int32_t *sub_bits = nullptr, int64_t ubeg = 0, int64_t uend = -1) {
-    // units [ubeg, uend) of the job (uend < 0: to the end): a split job encodes its tile ranges in turn, each launch
-    // with its own ticket counter; the look-back reaches into the previous launch's (inclusive) statuses
+                                                  int32_t *sub_bits = nullptr) {
     __shared__ EncV3Shared S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int i = threadIdx.x; i < 4096; i += blockDim.x) (&S.crc8x[0][0])[i] = (&c_crc16x8[0][0])[i];
@@ -3650,15 +3403,15 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
     uint32_t *fbuf = S.bits[wave];
     while (true) {
         __syncthreads();  // previous ticket's readers of S.ticket / S.lut are done
-        const int64_t nunits = uend < 0 ? (SUB ? P.nframes * P.nch : P.nframes) : uend;
+        const int64_t nunits = SUB ? P.nframes * P.nch : P.nframes;
         if (threadIdx.x == 0) {
             const int tk = atomicAdd(ticket_ctr, 1);
             S.ticket = tk;
-            const int64_t u0 = ubeg + (int64_t)tk * 4;
+            const int64_t u0 = (int64_t)tk * 4;
             S.want = (u0 < nunits) ? ftile[SUB ? u0 / P.nch : u0] : -1;
         }
         __syncthreads();
-        const int64_t fbase = ubeg + (int64_t)S.ticket * 4;
+        const int64_t fbase = (int64_t)S.ticket * 4;
         if (fbase >= nunits) break;
         const int want = S.want;
         if (want != S.lut_tile) {  // WG-uniform
@@ -3691,224 +3444,6 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
     }
     if constexpr (!SUB)
         if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
-}
-
-// Phase 1 of k_fused_v6: the work-group claims tiles [tile_begin, ntiles) four at a time until none is left; per tile
-// (one per wave) the stats, parameters, LUT and sums of k_analyze_v3, every result handed off (sc1 stores, vmcnt(0),
-// flag, done counter).  Returns the tiles this wave analysed.
-template <int DT>
-__device__ __forceinline__ int fused_analyse_tiles(const typename Elem<DT>::T *raster, const EncodeParams &P,
-                                                const TileGeom *tiles, TileNorm *norms, TileHand *hand,
-                                                const float *__restrict__ window, SubAnalysis *hana, uint32_t *flags,
-                                                uint32_t epoch, int *tile_ctr, int *done_ctr, int ntiles,
-                                                int tile_begin, int16_t *wl, int *s_claim) {
-    using T = typename Elem<DT>::T;
-    const int lane = (int)(threadIdx.x & 63), wave = (int)(threadIdx.x >> 6);
-    int done = 0;
-    while (true) {
-        // the work-group claims 4 tiles at a time, one per wave: its waves start and end their tiles together, so
-        // none idles at the phase barrier behind a sibling's tile (per-wave claims left ~30 % of the waves waiting
-        // for up to a tile's sums there)
-        __syncthreads();
-        if (threadIdx.x == 0) *s_claim = tile_begin + atomicAdd(tile_ctr, 4);
-        __syncthreads();
-        const int t0 = *s_claim;
-        if (t0 >= ntiles) break;
-        const int t = t0 + wave;
-        if (t >= ntiles) continue;
-        const TileGeom g = tiles[t];
-        const T *base = raster + (int64_t)P.band0 * P.band_stride + g.r0 * P.row_stride + g.c0;
-        TileNorm tn;
-        wave_tile_minmax<DT>(base, P.row_stride, g, lane, tn.imin, tn.imax);
-        tile_norm_finalize<DT>(tn, P.norm_mode, P.scale_bits);
-        if (lane == 0) {
-            norms[t] = tn;  // (for the host's min/max, after the launch)
-            sc1_store(&hand[t].tn, tn);
-        }
-        const int nfull = g.nframes;  // (no partial frames on this path)
-        const bool live = lane < nfull;
-        const int64_t fk = live ? lane : nfull - 1;  // dead lanes re-read the tile's last frame
-        const int64_t s0 = fk * P.blocksize;
-        double acc[kMaxLpc + 1];
-#pragma unroll
-        for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
-        uint32_t or_acc = 0, ft[5];
-        if (tn.mode == kNormLut) {
-            const int64_t R = tn.imax - tn.imin;
-            uint32_t *hl = reinterpret_cast<uint32_t *>(hand[t].lut);
-            for (int64_t d2 = lane; 2 * d2 <= R; d2 += 64) {  // entry pairs: 4-byte sc1 stores
-                const int16_t e0 = lut_entry<DT>(tn, 2 * d2);
-                const int16_t e1 = 2 * d2 + 1 <= R ? lut_entry<DT>(tn, 2 * d2 + 1) : (int16_t)0;
-                wl[2 * d2] = e0;
-                wl[2 * d2 + 1] = e1;
-                __hip_atomic_store(hl + d2, (uint32_t)(uint16_t)e0 | ((uint32_t)(uint16_t)e1 << 16), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            }
-            __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's LUT stores have landed in LDS
-            __builtin_amdgcn_wave_barrier();
-            ana_autoc<DT, kAnaKindLds, 64>(base, P, g, s0, tn, wl, nullptr, window, (g.w % 64) == 0 ? P.vec_ok : 0,
-                                           acc, or_acc, ft);
-        } else if (tn.mode == kNormZero) {
-            ana_autoc<DT, kAnaKindZero, 64>(base, P, g, s0, tn, wl, nullptr, window, (g.w % 64) == 0 ? P.vec_ok : 0,
-                                            acc, or_acc, ft);
-        } else if (tn.mode == kNormFastDiv) {
-            ana_autoc<DT, kAnaKindFastDiv, 16>(base, P, g, s0, tn, nullptr, nullptr, window,
-                                               (g.w % 16) == 0 ? P.vec_ok : 0, acc, or_acc, ft);
-        } else {
-            ana_autoc<DT, kAnaKindGeneric, 16>(base, P, g, s0, tn, nullptr, nullptr, window,
-                                               (g.w % 16) == 0 ? P.vec_ok : 0, acc, or_acc, ft);
-        }
-        if (live) sc1_store(ana_hand(hana, g.frame_base + fk), analysis_finish(acc, or_acc, P.blocksize, P, ft));
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every handed-off byte of this tile has been written
-        if (lane == 0) {
-            __hip_atomic_store(flags + (size_t)t * kFlagStride, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(done_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        done++;
-    }
-    return done;
-}
-
-// ------------------------------------------------------------------------------ k_fused_v6
-// The analysis and the encoder of a 16-bit mono job in ONE persistent launch.  Separate launches leave the chip
-// half idle in the analysis' second round: a tile's 64 frames are 64 sequential fp64 sums on one wave (~0.4 ms), and
-// 6241 C4 tiles on 4096 wave slots take 1.5 rounds.  Here every work-group first claims tiles from a global counter
-// (phase 1, fused_analyse_tiles) and, once none is left, joins the encoder (k_encode_v3's ticket loop: phase 2), so
-// the last tiles' sums run beside the first frames' coding.  Frames are coded in stream order and a frame's tile was
-// claimed before any encoder started, so an encoder waits at most for one tile's analysis (flag polled per tile, the
-// hand-off protocol above; no polls at all once the done counter says every tile is published).  Hybrid
-// (tile_begin > 0): k_analyze_v3 analysed tiles [0, tile_begin) before the launch (one full round at its 4 waves per
-// SIMD); those are read with plain loads, the rest through the hand-off.
-template <int DT, bool PH1 = true>
-__global__ void __launch_bounds__(256, PH1 ? 3 : 1) k_fused_v6(const typename Elem<DT>::T *raster, EncodeParams P,
-                                                 const TileGeom *tiles, TileNorm *norms, TileHand *hand,
-                                                 const float *__restrict__ window, SubAnalysis *ana, uint8_t *arena,
-                                                 int64_t arena_cap, int64_t *frame_off, uint64_t *status,
-                                                 int *ticket_ctr, int *err, const int32_t *__restrict__ ftile,
-                                                 const uint4 *__restrict__ hdr_tab, int hdr_n, uint32_t *flags,
-                                                 uint32_t epoch, int *tile_ctr, int ntiles, const int16_t *luts,
-                                                 SubAnalysis *hana, int tile_begin,
-                                                 unsigned long long *dbg = nullptr) {
-    using T = typename Elem<DT>::T;
-    static_assert(sizeof(T) == 2 && !Elem<DT>::is_float, "16-bit samples");
-    union FusedShared {
-        EncV3Shared enc;
-        int16_t alut[4][kLutCap];  // phase 1: one LUT per wave
-    };
-    __shared__ FusedShared U;
-    __shared__ int s_allpub;  // every tile has been published (the done counter reached its target): no more polls
-    __shared__ int s_claim;   // phase 1: the work-group's claimed tiles
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int *done_ctr = tile_ctr + 1;  // tiles published (agent-scope add after each tile's flag)
-    // dbg record of this work-group, updated live (system scope: readable by a host copy while the kernel runs):
-    // [start, end of phase 1, end, tickets, last ticket, last tile, state (1 phase 1, 2 flag wait, 3 encode, 4 done,
-    // 5 no wait needed), tiles analysed by wave 0]  (s_memrealtime, 100 MHz)
-    auto dbg_put = [&](int i, unsigned long long v) {
-        if (dbg && threadIdx.x == 0)
-            __hip_atomic_store(dbg + 8 * blockIdx.x + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    };
-    dbg_put(0, dbg ? __builtin_amdgcn_s_memrealtime() : 0);
-    dbg_put(6, 1);
-    // ---- phase 1
-    int ndone = 0;
-    if constexpr (PH1)
-        ndone = fused_analyse_tiles<DT>(raster, P, tiles, norms, hand, window, hana, flags, epoch, tile_ctr, done_ctr,
-                                        ntiles, tile_begin, U.alut[wave], &s_claim);
-    if (wave == 0) dbg_put(7, (unsigned long long)ndone);
-    if (threadIdx.x == 0) s_allpub = 0;
-    __syncthreads();  // the phase-1 LUTs are dead: the LDS becomes the encoder's
-    dbg_put(1, dbg ? __builtin_amdgcn_s_memrealtime() : 0);
-    dbg_put(6, 3);
-    // ---- phase 2: k_encode_v3's loop
-    EncV3Shared &S = U.enc;
-    for (int i = threadIdx.x; i < 4096; i += blockDim.x) (&S.crc8x[0][0])[i] = (&c_crc16x8[0][0])[i];
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) S.crc8[i] = c_crc8[i];
-    for (int i = threadIdx.x; i < 64; i += blockDim.x) S.xlo[i] = g_xpow_bytes[i];
-    for (int i = threadIdx.x; i < kXpowHi; i += blockDim.x) S.xhi[i] = g_xpow_bytes[64 * i];
-    for (int i = threadIdx.x; i < 4 * kBufWordsV3; i += blockDim.x) (&S.bits[0][0])[i] = 0;
-    if (threadIdx.x == 0) S.lut_tile = -1;
-    PendingFrame prev;
-    uint32_t *fbuf = S.bits[wave];
-    int ntk = 0;
-    while (true) {
-        __syncthreads();  // previous ticket's readers of S.ticket / S.lut are done
-        if (threadIdx.x == 0) {
-            const int tk = atomicAdd(ticket_ctr, 1);
-            // (independent of the ticket: both requests in flight together)
-            if (!s_allpub)
-                s_allpub = __hip_atomic_load(done_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ntiles - tile_begin;
-            S.ticket = tk;
-            const int64_t u0 = (int64_t)tk * 4;
-            S.want = (u0 < P.nframes) ? ftile[u0] : -1;
-        }
-        __syncthreads();
-        const int64_t fbase = (int64_t)S.ticket * 4;
-        if (fbase >= P.nframes) break;
-        ntk++;
-        const int want = S.want;
-        const bool allpub = s_allpub;
-        dbg_put(3, (unsigned long long)ntk);
-        dbg_put(4, (unsigned long long)S.ticket);
-        dbg_put(5, (unsigned long long)want);
-        if (want != S.lut_tile) {  // WG-uniform
-            const bool hand_w = want >= tile_begin;
-            dbg_put(6, allpub ? 5 : 2);
-            if (wave == 0 && !allpub && hand_w) wait_tile(flags, want, epoch, err);
-            dbg_put(6, 3);
-            __syncthreads();  // the other waves read the tile's bytes behind wave 0's matched poll
-            if (hand_w) {
-                const TileNorm tw = sc1_load_lanes(&hand[want].tn);
-                if (tw.mode == kNormLut) {
-                    const int64_t R = min(tw.imax - tw.imin, (int64_t)kLutCap - 1);  // (a LUT tile's range is below)
-                    uint32_t *hl = reinterpret_cast<uint32_t *>(hand[want].lut);
-                    uint32_t *sl = reinterpret_cast<uint32_t *>(S.lut);
-                    for (int64_t d2 = threadIdx.x; 2 * d2 <= R; d2 += blockDim.x)
-                        sl[d2] = __hip_atomic_load(hl + d2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            } else {  // analysed by k_analyze_v3 before this launch
-                const TileNorm tw = norms[want];
-                if (tw.mode == kNormLut) {
-                    const int64_t R = min(tw.imax - tw.imin, (int64_t)kLutCap - 1);
-                    const int16_t *src = luts + (int64_t)want * kLutCap;
-                    for (int64_t d = threadIdx.x; d <= R; d += blockDim.x) S.lut[d] = src[d];
-                }
-            }
-            __syncthreads();
-            if (threadIdx.x == 0) S.lut_tile = want;
-        }
-        const int64_t f = fbase + wave;
-        if (f < P.nframes) {
-            if constexpr (!PH1) {  // every tile analysed before the launch: k_encode_v3's own path
-                encode_frame_v3<DT>(raster, P, tiles, norms, luts, ana, arena, arena_cap, frame_off, status, err, S,
-                                    want, f, lane, ftile, prev, hdr_tab, hdr_n, nullptr, nullptr);
-            } else {
-                // the frame's tile parameters and analysis (encode_frame_v3's COH inputs) and where its LPC
-                // coefficients are read
-                const int t = ftile[f];
-                TileNorm tn;
-                SubAnalysis A;
-                const int32_t *qp;
-                const bool sc1 = t >= tile_begin;
-                if (sc1) {
-                    if (t != want && !allpub) wait_tile(flags, t, epoch, err);
-                    tn = sc1_load_lanes(&hand[t].tn);
-                    const SubAnalysis *ap = ana_hand(hana, f);
-                    A = sc1_load_lanes(ap);
-                    qp = ap->q;
-                } else {
-                    tn = norms[t];
-                    A = ana[f];
-                    qp = ana[f].q;
-                }
-                encode_frame_v3<DT, false, true>(raster, P, tiles, norms, nullptr, ana, arena, arena_cap, frame_off,
-                                                 status, err, S, want, f, lane, ftile, prev, hdr_tab, hdr_n, nullptr,
-                                                 nullptr, 0, nullptr, nullptr, &tn, &A, qp, sc1);
-            }
-        }
-    }
-    if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
-    dbg_put(2, dbg ? __builtin_amdgcn_s_memrealtime() : 0);
-    dbg_put(6, 4);
 }
 
 // ---------------------------------------------------------------- multi-channel streams (>= 3 channels, 16-bit)
@@ -4271,7 +3806,6 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     P.ncand = lv.parts > 1 ? apod_windows(lv.parts) : 0;
     // loose mid/side (stream_encoder.c init): an evaluation every (uint32_t)(sample_rate * 0.4 / blocksize + 0.5) frames
     P.loose_frames = 0;
-    P.dbg = ctx->ana_dbg ? 1 : 0;
     if (P.nch == 2 && lv.mid_side && lv.loose) {
         P.loose_frames = (int32_t)(uint32_t)((double)d->sample_rate * 0.4 / (double)d->blocksize + 0.5);
         if (P.loose_frames == 0) P.loose_frames = 1;
@@ -4399,9 +3933,6 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         FRS_HIP(ctx->frame_tile.ensure(sizeof(int32_t) * nframes));
         if (!(dev_tiles && ctx->geo_ptrs[3] == ctx->frame_tile.ptr))
             k_frame_tile<<<ntiles, 64, 0, st>>>(dtiles, ntiles, ctx->frame_tile.as<int32_t>());
-        int nsplit = 1;
-        bool fused = false;
-        int split_t[9] = {0};  // first wave (= tile, when split) of each range
         {
             // wave table: (tile, first frame) per wave, up to 64 frames of one tile each
             int nwaves = ctx->geo_nwaves;
@@ -4414,76 +3945,20 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                 FRS_HIP(ctx->wave_tab.ensure(sizeof(int2) * nwaves));
                 FRS_HIP(hipMemcpyAsync(ctx->wave_tab.ptr, wt, sizeof(int2) * nwaves, hipMemcpyHostToDevice, st));
             }
-            // split (fused stats, one wave per tile, mono, no partial frames): the wave table's ranges [w_k, w_k+1)
-            // are whole tiles; range k is analysed on the aux stream and encoded on `st` once its event fired
-            nsplit = (fuse_stats && !mc && P.nch == 1 && npartial == 0 && nwaves >= 32 * ctx->enc_split)
-                         ? ctx->enc_split : 1;
-            // one launch for analysis + encode (k_fused_v6): 16-bit mono, fused stats, no partial frames
-            fused = ctx->fused && fuse_stats && !mc && P.nch == 1 && npartial == 0 && nsplit == 1;
-            hipStream_t ast = st;
-            if (nsplit > 1) {
-                if (!ctx->aux_stream) FRS_HIP(hipStreamCreateWithFlags(&ctx->aux_stream, hipStreamNonBlocking));
-                for (int k = 0; k <= nsplit; k++)
-                    if (!ctx->split_ev[k]) FRS_HIP(hipEventCreateWithFlags(&ctx->split_ev[k], hipEventDisableTiming));
-                ast = ctx->aux_stream;
-                FRS_HIP(hipEventRecord(ctx->split_ev[nsplit], st));  // the uploads and setup kernels above
-                FRS_HIP(hipStreamWaitEvent(ast, ctx->split_ev[nsplit], 0));
+            prof_begin(ctx, "analyze", &ev);
+            const unsigned wgrid = (unsigned)((nwaves + 3) / 4);
+            const int2 *wtab = ctx->wave_tab.as<int2>();
+            if (fuse_stats) {
+                if constexpr (sizeof(T) == 2)
+                    k_analyze_v3<DT, false, true><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
+                                                                         ctx->window.as<float>(), dana, wtab, nwaves);
+            } else {
+                k_analyze_v3<DT, false><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
+                                                                ctx->window.as<float>(), dana, wtab, nwaves);
             }
-            if (!fused) prof_begin(ctx, "analyze", &ev, ast);
-            for (int k = 0; k < nsplit && !fused; k++) {
-                const int w0 = (int)((int64_t)nwaves * k / nsplit), w1 = (int)((int64_t)nwaves * (k + 1) / nsplit);
-                split_t[k] = w0;
-                const int nw = w1 - w0;
-                const unsigned wgrid = (unsigned)((nw + 3) / 4);
-                const int2 *wtk = ctx->wave_tab.as<int2>() + w0;
-                if (fuse_stats && ctx->ana_v5 && nsplit == 1 && P.nch == 1) {
-                    if constexpr (sizeof(T) == 2) {
-                        // role-split analysis: producers (tile stats + LUT) and consumers (sums) in each work-group
-                        FRS_HIP(ctx->ana_ctr.ensure(64));
-                        FRS_HIP(hipMemsetAsync(ctx->ana_ctr.ptr, 0, sizeof(int), ast));
-                        unsigned long long *dbg = nullptr;
-                        if (ctx->ana_dbg) {
-                            FRS_HIP(ctx->ana_dbgbuf.ensure(64));
-                            FRS_HIP(hipMemsetAsync(ctx->ana_dbgbuf.ptr, 0, 64, ast));
-                            dbg = ctx->ana_dbgbuf.as<unsigned long long>();
-                        }
-                        const int64_t g5 = std::min<int64_t>(2 * (int64_t)ctx->num_cus, ((int64_t)ntiles + 3) / 4);
-                        auto v5 = [&](auto kern) {
-                            kern<<<(unsigned)g5, 512, 0, ast>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
-                                                               ctx->window.as<float>(), dana, ntiles,
-                                                               ctx->ana_ctr.as<int>(), err_flag, dbg);
-                        };
-                        if (ctx->ana_v5 == 2) {
-                            if (dbg) v5(k_analyze_v5<DT, 6, 2, true>);
-                            else v5(k_analyze_v5<DT, 6, 2>);
-                        } else {
-                            if (dbg) v5(k_analyze_v5<DT, 4, 4, true>);
-                            else v5(k_analyze_v5<DT, 4, 4>);
-                        }
-                        if (dbg) {
-                            unsigned long long h[8];
-                            FRS_HIP(hipMemcpyAsync(h, dbg, 64, hipMemcpyDeviceToHost, ast));
-                            FRS_HIP(hipStreamSynchronize(ast));
-                            fprintf(stderr, "ana_v5 dbg: cons wait %.3g busy %.3g items %llu | prod busy %.3g wait %.3g "
-                                            "items %llu (wave-cycles)\n", (double)h[0], (double)h[1], h[2], (double)h[3],
-                                    (double)h[4], h[5]);
-                        }
-                    }
-                } else if (fuse_stats) {
-                    if constexpr (sizeof(T) == 2)
-                        k_analyze_v3<DT, false, true><<<wgrid, 256, 0, ast>>>(raster, P, dtiles, dnorms,
-                                                                              ctx->luts.as<int16_t>(),
-                                                                              ctx->window.as<float>(), dana, wtk, nw);
-                } else {
-                    k_analyze_v3<DT, false><<<wgrid, 256, 0, ast>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
-                                                                    ctx->window.as<float>(), dana, wtk, nw);
-                }
-                k_analyze_v3<DT, true><<<wgrid, 256, 0, ast>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
-                                                               ctx->window.as<float>(), dana, wtk, nw);
-                if (nsplit > 1) FRS_HIP(hipEventRecord(ctx->split_ev[k], ast));
-            }
-            split_t[nsplit] = nwaves;
-            if (!fused) prof_end(ctx, "analyze", ev, ast);
+            k_analyze_v3<DT, true><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
+                                                           ctx->window.as<float>(), dana, wtab, nwaves);
+            prof_end(ctx, "analyze", ev);
             if (!geo_hit) {  // the geometry's device copies are (being) uploaded on this stream: cache them
                 ctx->geo_tiles = tiles;
                 ctx->geo_plist.assign(hplist, hplist + npartial);
@@ -4643,101 +4118,17 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                 ctx->hdr_tab_sr = d->sample_rate;
             }
         }
-        if (fused) {
-            if constexpr (sizeof(T) == 2) {
-                FRS_HIP(ctx->hand.ensure(sizeof(TileHand) * (size_t)ntiles));
-                FRS_HIP(ctx->ana_hand.ensure((size_t)kAnaHandStride * nframes));  // frame analyses, one per line
-                // hybrid (FRS_FUSED=2): k_analyze_v3 takes the first K tiles (one full round of its 4 waves per SIMD),
-                // the fused launch analyses the rest while its early work-groups already encode
-                int K = 0;
-                if (ctx->fused == 2) {
-                    K = ctx->fused_k > 0 ? ctx->fused_k : 16 * ctx->num_cus;
-                    K = std::min(K, ntiles);
-                    prof_begin(ctx, "analyze", &ev);
-                    const unsigned wg = (unsigned)((K + 3) / 4);
-                    k_analyze_v3<DT, false, true><<<wg, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
-                                                                     ctx->window.as<float>(), dana,
-                                                                     ctx->wave_tab.as<int2>(), K);
-                    k_analyze_v3<DT, true><<<wg, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
-                                                              ctx->window.as<float>(), dana, ctx->wave_tab.as<int2>(), K);
-                    prof_end(ctx, "analyze", ev);
-                }
-                FRS_HIP(ctx->tile_flag.ensure(sizeof(uint32_t) * kFlagStride * (size_t)ntiles));
-                FRS_HIP(ctx->ana_ctr.ensure(64));
-                // flags hold the epoch of the launch that published them.  The epoch is advanced on EVERY launch
-                // (never inside a short-circuited condition: the round-3 k_analyze_v4 kept epoch 0 on its first call,
-                // which matched its zeroed flags), a new allocation is zeroed, and a wrap to 0 zeroes and restarts at 1
-                const bool fresh_flags = ctx->tile_flag.ptr != ctx->tile_flag_zeroed;
-                ++ctx->fuse_epoch;
-                if (fresh_flags || ctx->fuse_epoch == 0) {
-                    FRS_HIP(hipMemsetAsync(ctx->tile_flag.ptr, 0, ctx->tile_flag.bytes, st));
-                    ctx->tile_flag_zeroed = ctx->tile_flag.ptr;
-                    if (ctx->fuse_epoch == 0) ctx->fuse_epoch = 1;
-                }
-                FRS_HIP(hipMemsetAsync(ctx->ana_ctr.ptr, 0, 2 * sizeof(int), st));  // tile counter, done counter
-                static int nwg_f = 0;
-                if (nwg_f == 0) FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nwg_f, k_fused_v6<DT>, 256, 0));
-                const int64_t grid = std::min<int64_t>((int64_t)std::max(1, nwg_f) * ctx->num_cus, (nframes + 3) / 4);
-                unsigned long long *dbg = nullptr;
-                if (ctx->ana_dbg) {
-                    FRS_HIP(ctx->ana_dbgbuf.ensure(64 * (size_t)grid));
-                    FRS_HIP(hipMemsetAsync(ctx->ana_dbgbuf.ptr, 0, 64 * (size_t)grid, st));
-                    FRS_HIP(hipStreamSynchronize(st));
-                    dbg = ctx->ana_dbgbuf.as<unsigned long long>();
-                }
-                prof_begin(ctx, "fused", &ev);
-                auto kf = K >= ntiles ? k_fused_v6<DT, false> : k_fused_v6<DT, true>;  // (no tile left: encoder only)
-                kf<<<(unsigned)grid, 256, 0, st>>>(
-                    raster, P, dtiles, dnorms, ctx->hand.as<TileHand>(), ctx->window.as<float>(), dana,
-                    reinterpret_cast<uint8_t *>(arena_dev), arena_cap, ctx->frame_off.as<int64_t>(), dstatus, ticket,
-                    err_flag, ctx->frame_tile.as<int32_t>(), ctx->hdr_tab.as<uint4>(), hdr_n,
-                    ctx->tile_flag.as<uint32_t>(), ctx->fuse_epoch, ctx->ana_ctr.as<int>(), ntiles,
-                    ctx->luts.as<int16_t>(), ctx->ana_hand.as<SubAnalysis>(), K, dbg);
-                prof_end(ctx, "fused", ev);
-                if (dbg) {  // the work-groups' records; a launch still running after 10 s is reported and the process ends
-                    bool done = false;
-                    for (int i = 0; i < 1000 && !done; i++) {
-                        done = hipStreamQuery(st) == hipSuccess;
-                        if (!done) usleep(10000);
-                    }
-                    std::vector<unsigned long long> h(8 * (size_t)grid);
-                    int herr = 0;
-                    hipStream_t ds = st;
-                    if (!done) FRS_HIP(hipStreamCreateWithFlags(&ds, hipStreamNonBlocking));
-                    FRS_HIP(hipMemcpyAsync(h.data(), dbg, 64 * (size_t)grid, hipMemcpyDeviceToHost, ds));
-                    FRS_HIP(hipMemcpyAsync(&herr, err_flag, sizeof(int), hipMemcpyDeviceToHost, ds));
-                    FRS_HIP(hipStreamSynchronize(ds));
-                    for (int64_t b = 0; b < grid; b++)
-                        fprintf(stderr, "frs-wg %lld %llu %llu %llu %llu %llu %llu %llu %llu\n", (long long)b, h[8 * b],
-                                h[8 * b + 1], h[8 * b + 2], h[8 * b + 3], h[8 * b + 4], h[8 * b + 5], h[8 * b + 6],
-                                h[8 * b + 7]);
-                    fprintf(stderr, "frs-fused done=%d err=%d ntiles=%d nframes=%lld grid=%lld epoch=%u\n", (int)done, herr,
-                            (int)ntiles, (long long)nframes, (long long)grid, ctx->fuse_epoch);
-                    if (!done) {
-                        fflush(stderr);
-                        _exit(3);
-                    }
-                }
-            }
-        } else {
+        {
             static int nwg_max = 0;  // (per instantiation; the same gfx950 target for every device)
             if (nwg_max == 0) FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nwg_max, k_encode_v3<DT>, 256, 0));
-            for (int k = 0; k < nsplit; k++) {
-                // frames of range k: its tiles' frames (the whole job when not split)
-                const int64_t f0 = nsplit > 1 ? tiles[split_t[k]].frame_base : 0;
-                const int64_t f1 = nsplit > 1 && k + 1 < nsplit ? tiles[split_t[k + 1]].frame_base : nframes;
-                if (nsplit > 1) FRS_HIP(hipStreamWaitEvent(st, ctx->split_ev[k], 0));
-                if (k == 0) prof_begin(ctx, "encode", &ev);
-                int64_t grid = (int64_t)std::max(1, nwg_max) * ctx->num_cus;
-                grid = std::min<int64_t>(grid, (f1 - f0 + 3) / 4);
-                k_encode_v3<DT><<<(unsigned)grid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(), dana,
-                                                                reinterpret_cast<uint8_t *>(arena_dev), arena_cap,
-                                                                ctx->frame_off.as<int64_t>(), dstatus, ticket + k,
-                                                                err_flag, ctx->frame_tile.as<int32_t>(),
-                                                                ctx->hdr_tab.as<uint4>(), hdr_n,
-                                                                ctx->slots.as<uint32_t>(), dpbytes, nullptr, nullptr,
-                                                                f0, f1);
-            }
+            prof_begin(ctx, "encode", &ev);
+            int64_t grid = (int64_t)std::max(1, nwg_max) * ctx->num_cus;
+            grid = std::min<int64_t>(grid, (nframes + 3) / 4);
+            k_encode_v3<DT><<<(unsigned)grid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(), dana,
+                                                            reinterpret_cast<uint8_t *>(arena_dev), arena_cap,
+                                                            ctx->frame_off.as<int64_t>(), dstatus, ticket, err_flag,
+                                                            ctx->frame_tile.as<int32_t>(), ctx->hdr_tab.as<uint4>(), hdr_n,
+                                                            ctx->slots.as<uint32_t>(), dpbytes);
             prof_end(ctx, "encode", ev);
         }
         FRS_HIP(ctx->host_pack.ensure(res_bytes));
@@ -4904,7 +4295,6 @@ template <int DT>
 static int run_encode_any(frs_ctx *ctx, const frs_encode_desc *d, const void *raster_dev, void *arena_dev,
                           int64_t arena_cap, int64_t *tile_off, double *tile_min, double *tile_max) {
     int rc = run_encode<DT>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max, true);
-    if (rc == kFastDeclined && ctx->ana_dbg) fprintf(stderr, "frs: %s\n", ctx->err.c_str());
     if (rc == kFastDeclined) rc = run_encode<DT>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max, false);
     return rc;
 }

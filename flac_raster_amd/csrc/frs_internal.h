@@ -97,27 +97,10 @@ struct frs_ctx {
     int64_t geo_nframes = 0;
     int geo_nwaves = 0;
     void *geo_ptrs[4] = {nullptr, nullptr, nullptr, nullptr};  // tiles, wave_tab, plist, frame_tile as uploaded
-    // fast encode path split into enc_split tile ranges ($FRS_ENC_SPLIT, 1..8): range k's analysis runs on aux_stream
-    // while range k - 1 is encoded on `stream` (the analysis' min/max bursts and last-round tail overlap the encoder)
-    // role-split analysis (k_analyze_v5: stats producers and sums consumers inside each work-group); $FRS_ANA_V5
-    DevBuf ana_ctr;       // its global tile counter
     // subdivide_tukey levels (6..8): LPC candidates per coded signal, the tukey(0.5 / parts) window; loose mid/side:
     // per-frame assignment of the group leaders and the leader frame list
     DevBuf lpc_cand, window_hi, loose_assign, loose_lead;
     int window_hi_bs = 0, window_hi_parts = 0;
-    int fused = 0;        // $FRS_FUSED: 1 k_fused_v6 (analysis + encode in one launch), 2 hybrid (k_analyze_v3 on the first
-                          // $FRS_FUSED_K tiles, default 16 per CU, then k_fused_v6), where they apply
-    int fused_k = 0;
-    DevBuf hand, tile_flag, ana_hand;  // k_fused_v6 hand-off: per-tile parameters + LUT, per-tile flags, frame analyses
-    void *tile_flag_zeroed = nullptr;
-    uint32_t fuse_epoch = 0;
-    int ana_v5 = 0;       // 1: 4 consumer + 4 producer waves per work-group, 2: 6 + 2
-    bool ana_dbg = false; // $FRS_ANA_DBG: k_analyze_v5 wave-cycle totals to stderr
-    DevBuf ana_dbgbuf;
-    bool pipe2 = false;   // $FRS_PIPE2: the pipelined decoder's Rice decode by a resolver + two builder waves
-    int enc_split = 1;  // (2-4 measured slower on C4: both kernels are issue-bound, so sharing the CUs gains nothing)
-    hipStream_t aux_stream = nullptr;
-    hipEvent_t split_ev[9] = {};
 };
 
 #define FRS_HIP(call)                                                                  \

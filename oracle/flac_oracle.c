@@ -492,7 +492,9 @@ static void decide_subframe(int64_t *x, int n, int bps, int extra, int cfg_block
                 window_partial(x, window, scratch_d, n, n / b / 2, (c / 2 * n) / b);
                 autocorrelation(scratch_d, n / b, max_order + 1, autoc);
             } else {
-                for (int i = 0; i <= max_order; i++) autoc[i] = autoc_root[i] - autoc[i];
+                /* libFLAC 1.4.3 apply_apodization_ (stream_encoder.c): the punch-out subtracts (and autoc_root holds,
+                 * by its memcpy) lags 0 .. max_order - 1 only; lag max_order keeps the partial window's value */
+                for (int i = 0; i < max_order; i++) autoc[i] = autoc_root[i] - autoc[i];
             }
             more = next_subdivide(parts, &b, &c);
         }

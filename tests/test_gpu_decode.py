@@ -48,7 +48,6 @@ def _bands():
 
 
 DECODERS = {"pipe": {"FRS_DECODE_LANE": "0"},      # two-wave pipelined decoder (latency; C5 queries)
-            "pipe2": {"FRS_DECODE_LANE": "0", "FRS_PIPE2": "1"},  # its Rice decode by a resolver + 2 table builders
             "lane": {"FRS_DECODE_LANE": "1"},      # lane-per-frame decoder (throughput; batched decodes)
             "wave": {"FRS_FORCE_GENERIC": "1"}}    # one-lane wave decoder (any layout)
 

@@ -114,8 +114,9 @@ def test_loose_mid_side_schedule():
         for k in range(1, len(ca)):
             if k % 4:
                 assert ca[k] == ca[k - 1], (lv, k)
-    # the exhaustive search (levels 2 / 5) may pick left-side / right-side on the same signal
-    assert set(np.unique(O.frame_assignments(O.encode_frames(x, 16, 44100, level=5), 2, 16, n))) - {1, 10} or True
+    # the exhaustive search (level 5) on the same signal picks left-side (8) on some frames, which loose mid/side never
+    # considers
+    assert 8 in set(np.unique(O.frame_assignments(O.encode_frames(x, 16, 44100, level=5), 2, 16, n)))
 
 
 def test_product_level_gate():
