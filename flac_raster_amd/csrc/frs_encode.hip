@@ -2439,6 +2439,15 @@ __device__ inline uint32_t dpp_wave_or_u32(uint32_t v) {
     v |= bfly_partner<32>(v);
     return uni(v);
 }
+__device__ inline uint32_t dpp_wave_max_u32(uint32_t v) {
+    v = max(v, bfly_partner<1>(v));
+    v = max(v, bfly_partner<2>(v));
+    v = max(v, bfly_partner<4>(v));
+    v = max(v, bfly_partner<8>(v));
+    v = max(v, bfly_partner<16>(v));
+    v = max(v, bfly_partner<32>(v));
+    return uni(v);
+}
 __device__ inline uint32_t dpp_wave_xor_u32(uint32_t v) {
     v ^= bfly_partner<1>(v);
     v ^= bfly_partner<2>(v);
@@ -2833,148 +2842,12 @@ __device__ inline uint32_t fixed_lane_sum(const uint32_t *E, bool l0) {
     return s;
 }
 
-// SUB = true (multi-channel streams, >= 3 independent channels): the wave codes ONE subframe (channel chn of frame f)
-// from bit 0 of its buffer -- no frame header, no look-back, no CRC -- and stores its words to sub_slots[f * nch +
-// chn] with its bit length in sub_bits; k_mc_assemble joins a frame's subframes behind the frame header.
-template <int DT, bool SUB = false>
-__device__ __forceinline__ void encode_frame_v3(const typename Elem<DT>::T *raster, const EncodeParams &P,
-                                       const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
-                                       const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap, int64_t *frame_off,
-                                       uint64_t *status, int *err, EncV3Shared &S, int want, int64_t f, int lane,
-                                       const int32_t *ftile, PendingFrame &prev, const uint4 *hdr_tab, int hdr_n,
-                                       const uint32_t *pslots, const int64_t *pbytes, int chn = 0,
-                                       uint32_t *sub_slots = nullptr, int32_t *sub_bits = nullptr) {
-    using T = typename Elem<DT>::T;
-    uint32_t *fbuf = S.bits[threadIdx.x >> 6];
-    const int t = ftile[f];
-    const TileGeom g = tiles[t];
-    if (!SUB && g.partial && f - g.frame_base == g.nframes - 1) {
-        // (wave-uniform) the tile's partial last frame: already coded and sealed by the generic kernels, so it
-        // only joins the look-back chain -- publish its size, finish the previous frame, and stage its bytes in
-        // the bit buffer for resolve_and_store like a frame coded here
-        const int64_t si = g.partial - 1;
-        const uint64_t nb = (uint64_t)pbytes[si];
-        const uint32_t words = (uint32_t)((nb + 3) >> 2);
-        const bool ok = words + 2 <= (uint32_t)kFrameWordsV3;
-        if (!ok && lane == 0) atomicOr(err, 2);
-        const uint64_t fbytes = ok ? nb : 0;
-        const FbMap M = fb_map(words + 1);
-        if (lane == 0)
-            __hip_atomic_store(&status[f], (f == 0 ? kFlagIncl : kFlagAgg) | fbytes, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
-        if (ok) {
-            const uint32_t *src = pslots + (size_t)si * P.slot_words;
-            for (uint32_t w = (uint32_t)lane; w < words; w += 64) fbuf[M(w)] = __builtin_bswap32(src[w]);
-        }
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_wave_barrier();
-        prev.f = f;
-        prev.fbytes = fbytes;
-        prev.ok = ok;
-        prev.map = M;
-        return;
-    }
-    TileNorm tn = norms[t];
-    // the WG's LDS LUT belongs to tile `want`; a frame of another tile takes the exact division instead
-    if (t != want && tn.mode == kNormLut) tn.mode = kNormSlow;
-    const int16_t *lut = S.lut;
-    // issue priority: phase A (up to the size publish) and the previous frame's look-back + store gate the successors'
-    // look-backs, phase B (packing, CRC) gates nobody until the next frame -- the SIMD's arbiter prefers the former
-    // (encode 3.81 -> 3.65 ms on C4)
-    __builtin_amdgcn_s_setprio(2);
-    const int64_t fk = f - g.frame_base;
-    const int64_t s0 = fk * kMaxBlock;
+// libFLAC's set_partitioned_rice_ (stream_encoder.c) for the fixed and LPC candidates of a 4096-sample frame: orders
+// 5..0, group sums merged by lane shuffles (the 32-bit form when every lane sum is below 2^24)
+__device__ __forceinline__ void rice_candidates(uint32_t sf, uint32_t sl, int of, int ol, bool cand_fixed,
+                                                bool cand_lpc, int lane, uint32_t &rb_f, int &po_f, int &k_f,
+                                                uint32_t &rb_l, int &po_l, int &k_l) {
     constexpr int n = kMaxBlock;
-    const int64_t sub = SUB ? f * P.nch + chn : f;
-    const SubAnalysis A = ana[sub];
-    const int w = A.wasted;
-    const int sbps = 16 - w;
-    const T *base = raster + (int64_t)(P.band0 + chn) * P.band_stride + g.r0 * P.row_stride + g.c0;
-
-    // ---- this lane's 64 samples, normalised and shifted, packed as int16 pairs E[4 + m] = (x[2m], x[2m+1]);
-    //      E[0..3] = the previous lane's last 8 samples (zeros on lane 0)
-    uint32_t E[36];
-    {
-        Chunk64<DT> ch;
-        const uint32_t sl0 = (uint32_t)s0 + 64u * (uint32_t)lane;  // tile pixels < 2^31
-        const uint32_t row = udiv_inv(sl0, (uint32_t)g.w, 1.0 / (double)g.w);
-        ch.load(base, P.row_stride, g.w, row, (int)(sl0 - row * (uint32_t)g.w), (g.w % 64) == 0 ? P.vec_ok : 0, 64);
-        if (sizeof(T) == 2 && tn.mode == kNormLut && w == 0) {  // (wave-uniform) the common case
-            lut_gather_pairs(ch.w, lut, (int32_t)tn.imin, E + 4);
-        } else {
-            int32_t lo = 0;
-            norm_chunk<DT>(ch, tn, lut, [&](int j, int32_t x) {
-                if (j & 1) E[4 + (j >> 1)] = pack2(lo, x >> w);
-                else lo = x >> w;
-            });
-        }
-    }
-#pragma unroll
-    for (int m = 0; m < 4; m++) E[m] = dpp_wave_shr1(E[32 + m]);
-    reg_fence(E);  // keeps the load/normalise phase from overlapping the totals pass (VGPR peak)
-    auto X = [&](int j) -> int32_t {
-        const uint32_t v = E[4 + (j >> 1)];
-        return (j & 1) ? ((int32_t)v >> 16) : (int32_t)(int16_t)(v & 0xFFFFu);
-    };
-    const bool l0 = lane == 0;
-
-    // ---- fixed predictor: the order guess and its totals come from the analysis (fixed.c over samples 4..n-1);
-    //      here only the fixed candidate's lane partition sum of |e_guess(i)| is formed, below, when it is a
-    //      candidate at all
-    const int guess = A.fixed_order;
-    const uint32_t tg = A.fixed_tg;
-    const double dn = (double)(n - 4);
-    const float fb1 = (float)(A.fixed_t1 > 0 ? log(M_LN2 * (double)A.fixed_t1 / dn) / M_LN2 : 0.0);
-    const float fbg = (float)(tg > 0 ? log(M_LN2 * (double)tg / dn) / M_LN2 : 0.0);
-    // constant test (all samples equal) only where libFLAC reaches it: fixed bits[1] == 0
-    bool constant = false;
-    if (fb1 == 0.0f) {
-        reg_fence(E);
-        const uint32_t x0 = uni(E[4] & 0xFFFFu);
-        const uint32_t xx = x0 | (x0 << 16);  // both halves of a packed pair equal to sample 0
-        uint32_t diff = 0;
-#pragma unroll
-        for (int m = 4; m < 36; m++) diff |= E[m] ^ xx;
-        constant = dpp_wave_or_u32(diff) == 0;
-    }
-    const bool cand_fixed = !constant && !(fbg >= (float)sbps);
-    const bool cand_lpc = !constant && (A.flags & kFlagLpcOk);
-    const int of = guess, ol = A.lpc_order, lshift = A.lpc_shift;
-    uint32_t sf = 0;  // the lane's sum of |e_of(i)| (lane 0 from i = of)
-    if (cand_fixed) {
-        switch (of) {  // wave-uniform
-        case 0: sf = fixed_lane_sum<0>(E, l0); break;
-        case 1: sf = fixed_lane_sum<1>(E, l0); break;
-        case 2: sf = fixed_lane_sum<2>(E, l0); break;
-        case 3: sf = fixed_lane_sum<3>(E, l0); break;
-        default: sf = fixed_lane_sum<4>(E, l0); break;
-        }
-    }
-
-    uint32_t CL[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) CL[k] = pack2(A.q[2 * k + 1], A.q[2 * k]);
-    // ---- this lane's LPC |r| sum (residuals are recomputed by the later passes: cheaper than 64 live VGPRs)
-    uint32_t sl = 0;
-    if (cand_lpc) {
-#pragma unroll
-        for (int m = 0; m < 32; m++) {
-            if (m % 4 == 0 && m) asm volatile("" : "+v"(sl));
-            int32_t re, ro;
-            residual_pair(E, CL, lshift, m, re, ro);
-            const uint32_t ae = (uint32_t)abs(re), ao = (uint32_t)abs(ro);
-            if (2 * m < kMaxLpc) {
-                sl += (l0 && 2 * m < ol) ? 0u : ae;
-                sl += (l0 && 2 * m + 1 < ol) ? 0u : ao;
-            } else {
-                sl += ae + ao;
-            }
-        }
-    }
-    reg_fence(E);
-    // ---- set_partitioned_rice_ (stream_encoder.c): orders 5..0, group sums merged by lane shuffles;
-    //      n = 4096 so max order is 5 for every predictor order <= 8
     auto rice64 = [&](uint32_t lane_sum, int order, uint32_t &best_bits, int &best_po, int &my_k) {
         best_bits = 0;
         best_po = 0;
@@ -3096,8 +2969,8 @@ __device__ __forceinline__ void encode_frame_v3(const typename Elem<DT>::T *rast
             rice64(lane_sum, order, best_bits, best_po, my_k);
         }
     };
-    uint32_t rb_f = 0, rb_l = 0;
-    int po_f = 0, po_l = 0, k_f = 0, k_l = 0;
+    rb_f = rb_l = 0;
+    po_f = po_l = k_f = k_l = 0;
     if (cand_fixed && cand_lpc && __ballot(sf >= (1u << 24) || sl >= (1u << 24)) == 0) {
         uint32_t bb[2];
         int bp[2], bk[2];
@@ -3110,7 +2983,212 @@ __device__ __forceinline__ void encode_frame_v3(const typename Elem<DT>::T *rast
         if (cand_fixed) rice(sf, of, rb_f, po_f, k_f);
         if (cand_lpc) rice(sl, ol, rb_l, po_l, k_l);
     }
-    // ---- choose (process_subframe_: VERBATIM, then CONSTANT | FIXED, LPC; strict <)
+}
+
+// ------------------------------------------------------------------------------ k_encode_v4 (lane-private segments)
+// The v3 encoder needs every code's frame position before it packs (the look-back publishes sizes early), so it
+// walks the residuals three times: |r| sums for the Rice search, exact code lengths, packing.  v4 packs each lane's
+// 64 codes into a PRIVATE column of the wave's buffer (lane L's word i at i * 64 + L, the partition's 4-bit Rice
+// parameter first when the lane starts a partition), so the code-length pass disappears: a lane's length is its
+// write position at the end.  The frame is then assembled in place in a linear layout (word w at w): every lane
+// reads its column into registers, the buffer is zeroed, and the lane ORs its segment in at its bit offset (one
+// v_alignbit per word; words shared with a neighbour lane are OR-ed by both).  Header, warm-up and coefficient
+// fields are OR-ed at their fixed positions, the CRC-16 is summed per lane over word ranges, and only then does the
+// wave look back for its frame's byte offset and store the frame (one buffer per wave: the store is not deferred to
+// the next frame, which leaves the assembly and CRC as the look-back's slack).  A lane whose segment outgrows its
+// column (> kPrivBits, e.g. a residual spike in an otherwise smooth frame) makes the whole wave repack from its
+// registers at the now known offsets (the v3 writer on the linear layout).
+constexpr int kPrivRows = 34;                    // column rows holding a lane's codes; row 34 takes the last lo words
+constexpr uint32_t kPrivBits = kPrivRows * 32;   // 1088 bits = 17 bits per sample
+static_assert(kBufWordsV3 >= (kPrivRows + 1) * 64, "private rows + the spill row");
+static_assert(kBufWordsV3 % 4 == 0, "b128 zeroing");
+
+// zero the wave's whole buffer (kBufWordsV3 words) with 16-byte stores
+__device__ inline void zero_wave_buf(uint32_t *buf, int lane) {
+    uint4 *b4 = reinterpret_cast<uint4 *>(buf);
+#pragma unroll
+    for (int i = 0; i < (kBufWordsV3 / 4 + 63) / 64; i++) {
+        const int c = lane + 64 * i;
+        if (i < kBufWordsV3 / 256 || c < kBufWordsV3 / 4) b4[c] = make_uint4(0u, 0u, 0u, 0u);
+    }
+}
+
+// CRC-16 of body bytes [0, body) of a frame in the column layout M: lane L takes column L (words L C .. L C + C - 1,
+// so at each step the lanes read one row: consecutive banks) by slice-by-16, the lane holding the last whole word adds
+// the tail bytes, and the lanes' values are combined with x^(8m) factors (m = bytes after the lane's range)
+__device__ __forceinline__ uint32_t crc16_cols(const uint32_t *fbuf, const FbMap &M, uint32_t body, const EncV3Shared &S,
+                                               int lane) {
+    const uint32_t nfw = body >> 2, tail = body & 3;
+    const uint32_t wb = min(nfw, (uint32_t)lane * M.c), we = min(nfw, wb + M.c);
+    uint32_t c = 0;
+    const uint32_t *colp = fbuf + lane;
+    const uint16_t(*T)[256] = S.crc8x;
+    uint32_t i = wb;
+    for (; i + 3 < we; i += 4, colp += 256) {
+        const uint32_t w0 = colp[0], w1 = colp[64], w2 = colp[128], w3 = colp[192];
+        c = (uint32_t)T[15][((c >> 8) ^ (w0 >> 24)) & 0xFF] ^ T[14][((c & 0xFF) ^ (w0 >> 16)) & 0xFF] ^
+            T[13][(w0 >> 8) & 0xFF] ^ T[12][w0 & 0xFF] ^ T[11][w1 >> 24] ^ T[10][(w1 >> 16) & 0xFF] ^
+            T[9][(w1 >> 8) & 0xFF] ^ T[8][w1 & 0xFF] ^ T[7][w2 >> 24] ^ T[6][(w2 >> 16) & 0xFF] ^
+            T[5][(w2 >> 8) & 0xFF] ^ T[4][w2 & 0xFF] ^ T[3][w3 >> 24] ^ T[2][(w3 >> 16) & 0xFF] ^
+            T[1][(w3 >> 8) & 0xFF] ^ T[0][w3 & 0xFF];
+    }
+    for (; i + 1 < we; i += 2, colp += 128) {
+        const uint32_t w0 = colp[0], w1 = colp[64];
+        c = (uint32_t)T[7][((c >> 8) ^ (w0 >> 24)) & 0xFF] ^ T[6][((c & 0xFF) ^ (w0 >> 16)) & 0xFF] ^
+            T[5][(w0 >> 8) & 0xFF] ^ T[4][w0 & 0xFF] ^ T[3][w1 >> 24] ^ T[2][(w1 >> 16) & 0xFF] ^
+            T[1][(w1 >> 8) & 0xFF] ^ T[0][w1 & 0xFF];
+    }
+    if (i < we) {
+        const uint32_t word = *colp;
+        c = (uint32_t)T[3][((c >> 8) ^ (word >> 24)) & 0xFF] ^ T[2][((c & 0xFF) ^ (word >> 16)) & 0xFF] ^
+            T[1][(word >> 8) & 0xFF] ^ T[0][word & 0xFF];
+    }
+    uint32_t end = we * 4;
+    if (lane == (int)M.col(nfw - 1)) {
+        const uint32_t word = fbuf[M(nfw)];
+        for (uint32_t b = 0; b < tail; b++) {
+            const uint32_t byte = (word >> (24 - 8 * b)) & 0xFF;
+            c = ((c << 8) & 0xFFFFu) ^ S.crc8x[0][((c >> 8) ^ byte) & 0xFF];
+        }
+        end += tail;
+    }
+    const uint32_t m = body - end;
+    return dpp_wave_xor_u32(gf_mulmod(gf_mulmod(c, S.xlo[m & 63]), S.xhi[m >> 6]));
+}
+
+template <int DT, bool SUB = false>
+__device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *raster, const EncodeParams &P,
+                                                const TileGeom *tiles, const TileNorm *norms,
+                                                const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap,
+                                                int64_t *frame_off, uint64_t *status, int *err, EncV3Shared &S,
+                                                int want, int64_t f, int lane, const int32_t *ftile,
+                                                PendingFrame &prev, const uint4 *hdr_tab, int hdr_n,
+                                                const uint32_t *pslots, const int64_t *pbytes, int chn = 0,
+                                                uint32_t *sub_slots = nullptr, int32_t *sub_bits = nullptr) {
+    using T = typename Elem<DT>::T;
+    uint32_t *fbuf = S.bits[threadIdx.x >> 6];  // holds the pending frame `prev` (or zero) on entry
+    const int t = ftile[f];
+    const TileGeom g = tiles[t];
+    const bool l0 = lane == 0;
+    if (!SUB && g.partial && f - g.frame_base == g.nframes - 1) {
+        // (wave-uniform) the tile's partial last frame: already coded and sealed by the generic kernels; it only joins
+        // the look-back chain
+        const int64_t si = g.partial - 1;
+        const uint64_t nb = (uint64_t)pbytes[si];
+        const uint32_t words = (uint32_t)((nb + 3) >> 2);
+        const bool ok = words + 2 <= (uint32_t)kFrameWordsV3;
+        if (!ok && l0) atomicOr(err, 2);
+        const uint64_t fbytes = ok ? nb : 0;
+        const FbMap M = fb_map(words + 1);
+        __builtin_amdgcn_s_setprio(2);
+        if (l0)
+            __hip_atomic_store(&status[f], (f == 0 ? kFlagIncl : kFlagAgg) | fbytes, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
+        if (ok) {
+            const uint32_t *src = pslots + (size_t)si * P.slot_words;
+            for (uint32_t w = (uint32_t)lane; w < words; w += 64) fbuf[M(w)] = __builtin_bswap32(src[w]);
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_s_setprio(0);
+        prev.f = f, prev.fbytes = fbytes, prev.ok = ok, prev.map = M;
+        return;
+    }
+    TileNorm tn = norms[t];
+    // the WG's LDS LUT belongs to tile `want`; a frame of another tile takes the exact division instead
+    if (t != want && tn.mode == kNormLut) tn.mode = kNormSlow;
+    const int16_t *lut = S.lut;
+    // issue priority: the work up to the size publish gates the successors' look-backs
+    __builtin_amdgcn_s_setprio(2);
+    const int64_t fk = f - g.frame_base;
+    const int64_t s0 = fk * kMaxBlock;
+    constexpr int n = kMaxBlock;
+    const int64_t sub = SUB ? f * P.nch + chn : f;
+    const SubAnalysis A = ana[sub];
+    const int w = A.wasted;
+    const int sbps = 16 - w;
+    const T *base = raster + (int64_t)(P.band0 + chn) * P.band_stride + g.r0 * P.row_stride + g.c0;
+
+    // ---- this lane's 64 samples, normalised and shifted, packed as int16 pairs E[4 + m] = (x[2m], x[2m+1]);
+    //      E[0..3] = the previous lane's last 8 samples (zeros on lane 0)
+    auto load_E = [&](uint32_t *E) {
+        Chunk64<DT> ch;
+        const uint32_t sl0 = (uint32_t)s0 + 64u * (uint32_t)lane;  // tile pixels < 2^31
+        const uint32_t row = udiv_inv(sl0, (uint32_t)g.w, 1.0 / (double)g.w);
+        ch.load(base, P.row_stride, g.w, row, (int)(sl0 - row * (uint32_t)g.w), (g.w % 64) == 0 ? P.vec_ok : 0, 64);
+        if (sizeof(T) == 2 && tn.mode == kNormLut && w == 0) {  // (wave-uniform) the common case
+            lut_gather_pairs(ch.w, lut, (int32_t)tn.imin, E + 4);
+        } else {
+            int32_t lo = 0;
+            norm_chunk<DT>(ch, tn, lut, [&](int j, int32_t x) {
+                if (j & 1) E[4 + (j >> 1)] = pack2(lo, x >> w);
+                else lo = x >> w;
+            });
+        }
+#pragma unroll
+        for (int m = 0; m < 4; m++) E[m] = dpp_wave_shr1(E[32 + m]);
+        reg_fence(E);
+    };
+    uint32_t E[36];
+    load_E(E);
+    auto X = [&](int j) -> int32_t {
+        const uint32_t v = E[4 + (j >> 1)];
+        return (j & 1) ? ((int32_t)v >> 16) : (int32_t)(int16_t)(v & 0xFFFFu);
+    };
+
+    // ---- candidates (as v3): fixed order guess + totals from the analysis, the fixed and LPC lane |r| sums
+    const int guess = A.fixed_order;
+    const uint32_t tg = A.fixed_tg;
+    const double dn = (double)(n - 4);
+    const float fb1 = (float)(A.fixed_t1 > 0 ? log(M_LN2 * (double)A.fixed_t1 / dn) / M_LN2 : 0.0);
+    const float fbg = (float)(tg > 0 ? log(M_LN2 * (double)tg / dn) / M_LN2 : 0.0);
+    bool constant = false;
+    if (fb1 == 0.0f) {
+        reg_fence(E);
+        const uint32_t x0 = uni(E[4] & 0xFFFFu);
+        const uint32_t xx = x0 | (x0 << 16);
+        uint32_t diff = 0;
+#pragma unroll
+        for (int m = 4; m < 36; m++) diff |= E[m] ^ xx;
+        constant = dpp_wave_or_u32(diff) == 0;
+    }
+    const bool cand_fixed = !constant && !(fbg >= (float)sbps);
+    const bool cand_lpc = !constant && (A.flags & kFlagLpcOk);
+    const int of = guess, ol = A.lpc_order, lshift = A.lpc_shift;
+    uint32_t sf = 0;
+    if (cand_fixed) {
+        switch (of) {  // wave-uniform
+        case 0: sf = fixed_lane_sum<0>(E, l0); break;
+        case 1: sf = fixed_lane_sum<1>(E, l0); break;
+        case 2: sf = fixed_lane_sum<2>(E, l0); break;
+        case 3: sf = fixed_lane_sum<3>(E, l0); break;
+        default: sf = fixed_lane_sum<4>(E, l0); break;
+        }
+    }
+    uint32_t CL[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) CL[k] = pack2(A.q[2 * k + 1], A.q[2 * k]);
+    uint32_t sl = 0;
+    if (cand_lpc) {
+#pragma unroll
+        for (int m = 0; m < 32; m++) {
+            if (m % 4 == 0 && m) asm volatile("" : "+v"(sl));
+            int32_t re, ro;
+            residual_pair(E, CL, lshift, m, re, ro);
+            const uint32_t ae = (uint32_t)abs(re), ao = (uint32_t)abs(ro);
+            if (2 * m < kMaxLpc) {
+                sl += (l0 && 2 * m < ol) ? 0u : ae;
+                sl += (l0 && 2 * m + 1 < ol) ? 0u : ao;
+            } else {
+                sl += ae + ao;
+            }
+        }
+    }
+    reg_fence(E);
+    uint32_t rb_f = 0, rb_l = 0;
+    int po_f = 0, po_l = 0, k_f = 0, k_l = 0;
+    rice_candidates(sf, sl, of, ol, cand_fixed, cand_lpc, lane, rb_f, po_f, k_f, rb_l, po_l, k_l);
     uint32_t best = (uint32_t)(1 + 6 + 1 + w + n * sbps);
     int type = 1;
     if (constant) {
@@ -3128,10 +3206,19 @@ __device__ __forceinline__ void encode_frame_v3(const typename Elem<DT>::T *rast
             if (est != 0 && est < best) { best = est; type = 3; }
         }
     }
-    // ---- phase A: sizes only (no writes to the bit buffer, which still holds the previous frame)
+    // lane i (< 8) of lane 0's warm-up sample i, lane 0's sample 0 (CONSTANT): taken now, the registers die below
+    uint32_t xi;
+    {
+        const int i = lane & 7;
+        uint32_t w01 = (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 0], 0);
+        w01 = (i >> 1) == 1 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 1], 0) : w01;
+        w01 = (i >> 1) == 2 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 2], 0) : w01;
+        w01 = (i >> 1) == 3 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 3], 0) : w01;
+        xi = (i & 1) ? (w01 >> 16) : (w01 & 0xFFFFu);
+    }
+    // ---- field positions
     int src, srx;
     sample_rate_code(P.sample_rate, src, srx);
-    // frame header bytes: host table by frame number within the stream (words MSB-first; .w = length)
     const bool tab = !SUB && fk < hdr_n;
     uint4 hrow = make_uint4(0, 0, 0, 0);
     if (tab) hrow = hdr_tab[fk];
@@ -3142,8 +3229,10 @@ __device__ __forceinline__ void encode_frame_v3(const typename Elem<DT>::T *rast
     uint32_t end_bits;
     bool ok = true;
     uint32_t C[4];
-    int shift = lshift, k = 0, lanes_per = 64, p = 0, o = 0, po = 0;
-    uint32_t run = 0;
+    int shift = lshift, k = 0, lanes_per = 64, o = 0, po = 0;
+    uint32_t run = 0;      // lane-private write position (bits)
+    uint32_t seglen = 0;   // the lane's segment length (bits)
+    bool over = false;     // (wave-uniform) a lane outgrew its column: repack at known offsets
     if (type == 0) {
         end_bits = pos + (uint32_t)sbps;
     } else if (type == 1) {
@@ -3153,7 +3242,6 @@ __device__ __forceinline__ void encode_frame_v3(const typename Elem<DT>::T *rast
         po = type == 2 ? po_f : po_l;
         k = type == 2 ? k_f : k_l;
         lanes_per = 64 >> po;
-        p = lane / lanes_per;
         if (type == 2) {
             int32_t qf[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             if (of == 1) qf[0] = 1;
@@ -3169,123 +3257,20 @@ __device__ __forceinline__ void encode_frame_v3(const typename Elem<DT>::T *rast
         }
         pos += (uint32_t)o * sbps;
         if (type == 3) pos += 9 + (uint32_t)o * A.lpc_prec;
-        pos += 6;
-        // exact code lengths (masked warm-up samples: len 0)
-        uint32_t lens = 0;
-#pragma unroll
-        for (int m = 0; m < 32; m++) {
-            if (m % 4 == 0 && m) asm volatile("" : "+v"(lens));
-            int32_t re, ro;
-            residual_pair(E, C, shift, m, re, ro);
-            uint32_t le = zigzag(re) >> k, lo = zigzag(ro) >> k;
-            if (2 * m < kMaxLpc) {
-                if (l0 && 2 * m < o) le = 0;
-                if (l0 && 2 * m + 1 < o) lo = 0;
-            }
-            lens += le + lo;
-        }
-        lens += (uint32_t)(64 - (l0 ? o : 0)) * (1u + (uint32_t)k);  // unary stop bit + k low bits per code
-        reg_fence(E);
-        const uint32_t incl = dpp_incl_scan_u32(lens);
-        const uint64_t excl = incl - lens;
-        const uint64_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        const uint64_t fin = (uint64_t)pos + 4ull * (uint64_t)(1 << po) + total;
-        end_bits = (uint32_t)fin;
-        if (fin + 64 > (uint64_t)kFrameWordsV3 * 32) ok = false;
-        run = pos + 4u * (uint32_t)(p + 1) + (uint32_t)excl;
+        pos += 6;  // RICE method + partition order; the partitions' parameters sit in their first lanes' segments
     }
-    if (!ok) {
-        if (l0) atomicOr(err, 2);
-        end_bits = 0;
-    }
-    const uint32_t body = (end_bits + 7) >> 3;  // bytes before the CRC-16 footer
-    const uint64_t fbytes = ok ? (uint64_t)body + 2 : 0;
-    const FbMap M = fb_map(((end_bits + 23) >> 5) + 2);  // words written: body, CRC-16 (byte aligned), one spare
-    if (!SUB && l0) {  // publish our aggregate
-        const uint64_t v = (f == 0 ? kFlagIncl : kFlagAgg) | fbytes;
-        __hip_atomic_store(&status[f], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // ---- the previous frame of this wave: its predecessors have had a whole phase A to publish, so the
-    //      look-back rarely waits; store it and free the bit buffer
+    // ---- the previous frame of this wave: its successors have had this frame's loads, sums and Rice search to
+    //      publish, so the look-back rarely waits; store it and free the buffer (zero after this)
     if constexpr (!SUB)
         if (prev.f >= 0) resolve_and_store(P, prev, fbuf, arena, arena_cap, frame_off, status, err, lane);
-    __builtin_amdgcn_s_setprio(0);
-    reg_fence(E);
-    // ---- phase B: every bit of this frame into the (zeroed) buffer, then the CRC-16
-    if (l0 && tab) {
-        // 13 header bytes at most; the 4th word's low byte holds the length (byte 15: never a header byte)
-        fbuf[M(0)] = hrow.x;
-        fbuf[M(1)] = hrow.y;
-        fbuf[M(2)] = hrow.z;
-        fbuf[M(3)] = hrow.w & 0xFFFFFF00u;
-    }
-    if (l0) {
-        uint32_t hbits = 0, c8 = 0;
-        auto put8 = [&](uint32_t b) {
-            lds_put_bits2(fbuf, M, hbits, b, 8);
-            c8 = S.crc8[c8 ^ b];
-            hbits += 8;
-        };
-        const int sr = P.sample_rate;
-        if (!SUB && !tab) {
-        put8(0xFF);
-        put8(0xF8);
-        put8((uint32_t)((12 << 4) | src));  // block size code 12 = 4096
-        put8((uint32_t)(4 << 1));           // mono, 16 bits
-        const uint32_t v = (uint32_t)fk;    // UTF-8 coded frame number
-        if (v < 0x80) put8(v);
-        else if (v < 0x800) { put8(0xC0 | (v >> 6)); put8(0x80 | (v & 0x3F)); }
-        else if (v < 0x10000) { put8(0xE0 | (v >> 12)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
-        else if (v < 0x200000) { put8(0xF0 | (v >> 18)); put8(0x80 | ((v >> 12) & 0x3F)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
-        else if (v < 0x4000000) { put8(0xF8 | (v >> 24)); put8(0x80 | ((v >> 18) & 0x3F)); put8(0x80 | ((v >> 12) & 0x3F)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
-        else { put8(0xFC | (v >> 30)); put8(0x80 | ((v >> 24) & 0x3F)); put8(0x80 | ((v >> 18) & 0x3F)); put8(0x80 | ((v >> 12) & 0x3F)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
-        if (srx == 12) put8((uint32_t)(sr / 1000));
-        else if (srx == 13) { put8((uint32_t)(sr >> 8) & 0xFF); put8((uint32_t)sr & 0xFF); }
-        else if (srx == 14) { put8((uint32_t)((sr / 10) >> 8) & 0xFF); put8((uint32_t)(sr / 10) & 0xFF); }
-        put8(c8);  // CRC-8 (the table lookup of the last call is unused)
-        }
-        const int typecode = type == 0 ? 0 : type == 1 ? 1 : type == 2 ? 8 + of : 32 + ol - 1;
-        lds_put_bits2(fbuf, M, hdr_bits, (uint32_t)(typecode << 1) | (w ? 1u : 0u), 8);
-        if (w) lds_put_bits2(fbuf, M, hdr_bits + 8 + (uint32_t)(w - 1), 1, 1);
-        if (type == 0) lds_put_bits2(fbuf, M, pos0, (uint32_t)X(0) & ((1u << sbps) - 1u), sbps);
-        if (type >= 2) {
-            uint32_t q = pos0 + (uint32_t)o * sbps;
-            if (type == 3) {
-                lds_put_bits2(fbuf, M, q, (uint32_t)(A.lpc_prec - 1), 4);
-                lds_put_bits2(fbuf, M, q + 4, (uint32_t)lshift & 31u, 5);
-                q += 9 + (uint32_t)o * A.lpc_prec;
-            }
-            lds_put_bits2(fbuf, M, q, (uint32_t)po, 6);  // RICE (00) + partition order (4 bits)
-        }
-    }
     if (type >= 2) {
-        // warm-up samples and quantised coefficients in parallel: lane i < o writes lane 0's sample i, lane 8 + i
-        // (LPC) coefficient i
-        const int i = lane & 7;
-        uint32_t w01 = (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 0], 0);
-        w01 = (i >> 1) == 1 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 1], 0) : w01;
-        w01 = (i >> 1) == 2 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 2], 0) : w01;
-        w01 = (i >> 1) == 3 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 3], 0) : w01;
-        const uint32_t xi = (i & 1) ? (w01 >> 16) : (w01 & 0xFFFFu);
-        // (a lane-indexed load: a select chain over A.q costs registers)
-        const int32_t qi = ana[sub].q[i];
-        const bool warm = lane < 8 && i < o, coef = type == 3 && lane >= 8 && lane < 16 && i < o;
-        if (warm)
-            lds_put_bits2(fbuf, M, pos0 + (uint32_t)i * sbps, xi & ((1u << sbps) - 1u), sbps);
-        if (coef)
-            lds_put_bits2(fbuf, M, pos0 + (uint32_t)o * sbps + 9 + (uint32_t)i * A.lpc_prec,
-                          (uint32_t)qi & ((1u << A.lpc_prec) - 1u), A.lpc_prec);
-    }
-    if (type >= 2 && ok && (lane & (lanes_per - 1)) == 0) lds_put_bits2(fbuf, M, run - 4u, (uint32_t)k, 4);
-    const int nk4 = -4 * (int)M.k;
-    if (type == 1) {
-        const uint32_t p0 = pos + (uint32_t)(64 * lane) * (uint32_t)sbps;
-        const uint32_t shl = 32u - (uint32_t)sbps;
-#pragma unroll
-        for (int j = 0; j < 64; j++) lds_put_left(fbuf, M, nk4, p0 + (uint32_t)j * sbps, (uint32_t)X(j) << shl);
-    } else if (type >= 2 && ok) {
-        // code = stop bit + k low bits, left-aligned: u << (31 - k) keeps u's low k bits below bit 31 (higher bits
-        // shift out, bit k lands on bit 31) and the stop bit is forced on
+        // ---- private packing: the lane's codes into its column (hi word at row p >> 5, lo word one row below;
+        //      rows clamped so an overflowing lane stays inside the buffer -- its frame is repacked below)
+        uint32_t *pcol = fbuf + lane;
+        if ((lane & (lanes_per - 1)) == 0) {
+            run = 4;
+            pcol[0] = (uint32_t)k << 28;
+        }
         const uint32_t sh = 31u - (uint32_t)k, oneL = 0x80000000u;
 #pragma unroll
         for (int m = 0; m < 32; m++) {
@@ -3302,62 +3287,185 @@ __device__ __forceinline__ void encode_frame_v3(const typename Elem<DT>::T *rast
                     codeL = 0;
                     adv = 0;
                 }
-                lds_put_left(fbuf, M, nk4, run + q, codeL);
+                const uint32_t p = run + q;
+                uint32_t *a = pcol + (min(p >> 5, (uint32_t)(kPrivRows - 1)) << 6);
+                atomicOr(a, __builtin_amdgcn_alignbit(0u, codeL, p));
+                atomicOr(a + 64, __builtin_amdgcn_alignbit(codeL, 0u, p));
                 run += adv;
             }
         }
+        over = __ballot(run > kPrivBits) != 0;
+        const uint32_t incl = dpp_incl_scan_u32(run);
+        const uint64_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        const uint64_t fin = (uint64_t)pos + total;
+        end_bits = (uint32_t)fin;
+        if (fin + 64 > (uint64_t)kFrameWordsV3 * 32) ok = false;
+        seglen = run;
+        run = incl - run;  // from here: the lane's exclusive offset within the residual section
+    }
+    if (!ok) {
+        if (l0) atomicOr(err, 2);
+        end_bits = 0;
+    }
+    const uint32_t body = (end_bits + 7) >> 3;  // bytes before the CRC-16 footer
+    const uint64_t fbytes = ok ? (uint64_t)body + 2 : 0;
+    if (!SUB && l0) {  // publish our aggregate
+        const uint64_t v = (f == 0 ? kFlagIncl : kFlagAgg) | fbytes;
+        __hip_atomic_store(&status[f], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __builtin_amdgcn_s_setprio(0);
+    // ---- assembly into the v3 frame layout (word w at row w mod C, column w / C: the store and CRC read rows, the
+    //      lanes' columns fall in distinct banks)
+    const FbMap M = fb_map(((end_bits + 23) >> 5) + 2);  // words written: body, CRC-16 (byte aligned), one spare
+    const int nk4 = -4 * (int)M.k;
+    bool fold = false;  // (wave-uniform) the v3 writer ran: its overflow row needs folding
+    // OR a lane's segment (registers Pv: MSB-first words from segment bit 0) in at frame bit `off`, `nwl` words: word
+    // i at column c0 row r0 + i while that is inside the column, then column c0 + 1 from row 0 (two base addresses,
+    // the row step is the ds offset); a lane spanning three columns (a frame far smaller than its largest segment)
+    // maps every word exactly
+    auto assemble = [&](const uint32_t *Pv, uint32_t off, uint32_t nwl) {
+        const uint32_t r = off & 31u, w0 = off >> 5;
+        const uint32_t c0 = M.col(w0), r0 = w0 - c0 * M.c, split = M.c - r0;
+        uint32_t *A = fbuf + (r0 << 6) + c0;
+        uint32_t *B = A + 1 - (int)(M.c << 6);
+        const uint32_t nmax = dpp_wave_max_u32(nwl);
+        if (__ballot(nwl > split + M.c) == 0) {
+            // words past the lane's last are zeros (its column is zero past its length): no per-lane predicate, and
+            // every address stays inside the wave's buffer (row <= 33 of column c0 + 1 <= 64)
+#pragma unroll
+            for (int i = 0; i <= kPrivRows; i++) {
+                if (i % 8 == 0 && (uint32_t)i >= nmax) break;  // (wave-uniform, every 8 words)
+                atomicOr(((uint32_t)i < split ? A : B) + 64 * i,
+                         __builtin_amdgcn_alignbit(i ? Pv[i - 1] : 0u, Pv[i], r));
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i <= kPrivRows; i++)
+                if ((uint32_t)i < nwl) atomicOr(fbuf + M(w0 + (uint32_t)i), __builtin_amdgcn_alignbit(i ? Pv[i - 1] : 0u, Pv[i], r));
+        }
+    };
+    if (type >= 2) {
+        uint32_t Pv[kPrivRows + 1];
+        const uint32_t *pcol = fbuf + lane;
+#pragma unroll
+        for (int i = 0; i <= kPrivRows; i++) Pv[i] = pcol[i << 6];
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // every lane's column is in registers before the zeroing
+        __builtin_amdgcn_wave_barrier();
+        zero_wave_buf(fbuf, lane);
+        if (ok && !over) {
+            const uint32_t off = pos + run;
+            assemble(Pv, off, ((off & 31u) + seglen + 31) >> 5);
+        } else if (ok) {
+            // a lane outgrew its column: the v3 writer at the known offsets, from the samples loaded again (rare: the
+            // registers of the first load are free for the assembly)
+            load_E(E);
+            uint32_t rp = pos + run;
+            if ((lane & (lanes_per - 1)) == 0) {
+                lds_put_bits2(fbuf, M, rp, (uint32_t)k, 4);
+                rp += 4;
+            }
+            const uint32_t sh = 31u - (uint32_t)k, oneL = 0x80000000u;
+#pragma unroll
+            for (int m = 0; m < 32; m++) {
+                int32_t re, ro;
+                residual_pair(E, C, shift, m, re, ro);
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int j = 2 * m + h;
+                    const uint32_t u = zigzag(h ? ro : re);
+                    uint32_t q = u >> k, codeL = (u << sh) | oneL, adv = q + 1 + (uint32_t)k;
+                    if (j < kMaxLpc && l0 && j < o) {
+                        q = 0;
+                        codeL = 0;
+                        adv = 0;
+                    }
+                    lds_put_left(fbuf, M, nk4, rp + q, codeL);
+                    rp += adv;
+                }
+            }
+            fold = true;
+        }
+    } else if (type == 1) {
+        if (w == 0) {
+            // 16-bit VERBATIM: the lane's 64 samples are its 32 packed pairs (halves swapped to MSB-first order)
+            uint32_t Pv[kPrivRows + 1];
+#pragma unroll
+            for (int m = 0; m < 32; m++) Pv[m] = __builtin_amdgcn_alignbit(E[4 + m], E[4 + m], 16);
+#pragma unroll
+            for (int m = 32; m <= kPrivRows; m++) Pv[m] = 0;
+            const uint32_t off = pos + 1024u * (uint32_t)lane;
+            assemble(Pv, off, ((off & 31u) + 1024u + 31) >> 5);
+        } else {
+            const uint32_t p0 = pos + (uint32_t)(64 * lane) * (uint32_t)sbps;
+            const uint32_t shl = 32u - (uint32_t)sbps;
+#pragma unroll
+            for (int j = 0; j < 64; j++) lds_put_left(fbuf, M, nk4, p0 + (uint32_t)j * sbps, (uint32_t)X(j) << shl);
+            fold = true;
+        }
+    }
+    // ---- header, subframe header, warm-up, coefficients, partition order (fixed positions below pos)
+    if (l0) {
+        if (tab) {
+            // 13 header bytes at most; the 4th word's low byte holds the length (byte 15: never a header byte)
+            atomicOr(fbuf + M(0), hrow.x);
+            atomicOr(fbuf + M(1), hrow.y);
+            atomicOr(fbuf + M(2), hrow.z);
+            atomicOr(fbuf + M(3), hrow.w & 0xFFFFFF00u);
+        } else if (!SUB) {
+            uint32_t hbits = 0, c8 = 0;
+            auto put8 = [&](uint32_t b) {
+                lds_put_bits2(fbuf, M, hbits, b, 8);
+                c8 = S.crc8[c8 ^ b];
+                hbits += 8;
+            };
+            const int sr = P.sample_rate;
+            put8(0xFF);
+            put8(0xF8);
+            put8((uint32_t)((12 << 4) | src));  // block size code 12 = 4096
+            put8((uint32_t)(4 << 1));           // mono, 16 bits
+            const uint32_t v = (uint32_t)fk;    // UTF-8 coded frame number
+            if (v < 0x80) put8(v);
+            else if (v < 0x800) { put8(0xC0 | (v >> 6)); put8(0x80 | (v & 0x3F)); }
+            else if (v < 0x10000) { put8(0xE0 | (v >> 12)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
+            else if (v < 0x200000) { put8(0xF0 | (v >> 18)); put8(0x80 | ((v >> 12) & 0x3F)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
+            else if (v < 0x4000000) { put8(0xF8 | (v >> 24)); put8(0x80 | ((v >> 18) & 0x3F)); put8(0x80 | ((v >> 12) & 0x3F)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
+            else { put8(0xFC | (v >> 30)); put8(0x80 | ((v >> 24) & 0x3F)); put8(0x80 | ((v >> 18) & 0x3F)); put8(0x80 | ((v >> 12) & 0x3F)); put8(0x80 | ((v >> 6) & 0x3F)); put8(0x80 | (v & 0x3F)); }
+            if (srx == 12) put8((uint32_t)(sr / 1000));
+            else if (srx == 13) { put8((uint32_t)(sr >> 8) & 0xFF); put8((uint32_t)sr & 0xFF); }
+            else if (srx == 14) { put8((uint32_t)((sr / 10) >> 8) & 0xFF); put8((uint32_t)(sr / 10) & 0xFF); }
+            put8(c8);  // CRC-8
+        }
+        const int typecode = type == 0 ? 0 : type == 1 ? 1 : type == 2 ? 8 + of : 32 + ol - 1;
+        lds_put_bits2(fbuf, M, hdr_bits, (uint32_t)(typecode << 1) | (w ? 1u : 0u), 8);
+        if (w) lds_put_bits2(fbuf, M, hdr_bits + 8 + (uint32_t)(w - 1), 1, 1);
+        if (type == 0) lds_put_bits2(fbuf, M, pos0, xi & ((1u << sbps) - 1u), sbps);  // (lane 0: its sample 0)
+        if (type >= 2) {
+            uint32_t qq = pos0 + (uint32_t)o * sbps;
+            if (type == 3) {
+                lds_put_bits2(fbuf, M, qq, (uint32_t)(A.lpc_prec - 1), 4);
+                lds_put_bits2(fbuf, M, qq + 4, (uint32_t)lshift & 31u, 5);
+                qq += 9 + (uint32_t)o * A.lpc_prec;
+            }
+            lds_put_bits2(fbuf, M, qq, (uint32_t)po, 6);  // RICE (00) + partition order (4 bits)
+        }
+    }
+    if (type >= 2) {
+        // warm-up samples and quantised coefficients in parallel: lane i < o writes lane 0's sample i, lane 8 + i
+        // (LPC) coefficient i
+        const int i = lane & 7;
+        const int32_t qi = ana[sub].q[i];  // (a lane-indexed load: a select chain over A.q costs registers)
+        const bool warm = lane < 8 && i < o, coef = type == 3 && lane >= 8 && lane < 16 && i < o;
+        if (warm) lds_put_bits2(fbuf, M, pos0 + (uint32_t)i * sbps, xi & ((1u << sbps) - 1u), sbps);
+        if (coef)
+            lds_put_bits2(fbuf, M, pos0 + (uint32_t)o * sbps + 9 + (uint32_t)i * A.lpc_prec,
+                          (uint32_t)qi & ((1u << A.lpc_prec) - 1u), A.lpc_prec);
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS atomics have landed
     __builtin_amdgcn_wave_barrier();
-    if (type == 1 || (type >= 2 && ok)) {  // (wave-uniform) codes were written: overflow rows home
+    if (fold) {  // (wave-uniform) the v3 writer's overflow row home
         fb_fold(fbuf, M, lane);
         __builtin_amdgcn_s_waitcnt(0xC07F);
         __builtin_amdgcn_wave_barrier();
-    }
-    uint32_t crc = 0;
-    if (!SUB && ok) {
-        // slice-by-4 over 32-bit words, one contiguous word range per lane, combined with x^(8m) factors
-        const uint32_t nfw = body >> 2, tail = body & 3;
-        // lane L takes column L of the buffer (words L C .. L C + C - 1), so at each step the lanes read one row:
-        // consecutive banks
-        const uint32_t wb = min(nfw, (uint32_t)lane * M.c), we = min(nfw, wb + M.c);
-        uint32_t c = 0;
-        const uint32_t *colp = fbuf + lane;
-        // slice-by-16 (four words per step: only two of the step's 16 table lookups depend on the running CRC, so
-        // the latency chain is a quarter of slice-by-4's), then slice-by-8 / slice-by-4 steps for the last 1-3 words
-        const uint16_t(*T)[256] = S.crc8x;
-        uint32_t i = wb;
-        for (; i + 3 < we; i += 4, colp += 256) {
-            const uint32_t w0 = colp[0], w1 = colp[64], w2 = colp[128], w3 = colp[192];
-            c = (uint32_t)T[15][((c >> 8) ^ (w0 >> 24)) & 0xFF] ^ T[14][((c & 0xFF) ^ (w0 >> 16)) & 0xFF] ^
-                T[13][(w0 >> 8) & 0xFF] ^ T[12][w0 & 0xFF] ^ T[11][w1 >> 24] ^ T[10][(w1 >> 16) & 0xFF] ^
-                T[9][(w1 >> 8) & 0xFF] ^ T[8][w1 & 0xFF] ^ T[7][w2 >> 24] ^ T[6][(w2 >> 16) & 0xFF] ^
-                T[5][(w2 >> 8) & 0xFF] ^ T[4][w2 & 0xFF] ^ T[3][w3 >> 24] ^ T[2][(w3 >> 16) & 0xFF] ^
-                T[1][(w3 >> 8) & 0xFF] ^ T[0][w3 & 0xFF];
-        }
-        for (; i + 1 < we; i += 2, colp += 128) {
-            const uint32_t w0 = colp[0], w1 = colp[64];
-            c = (uint32_t)T[7][((c >> 8) ^ (w0 >> 24)) & 0xFF] ^ T[6][((c & 0xFF) ^ (w0 >> 16)) & 0xFF] ^
-                T[5][(w0 >> 8) & 0xFF] ^ T[4][w0 & 0xFF] ^ T[3][w1 >> 24] ^ T[2][(w1 >> 16) & 0xFF] ^
-                T[1][(w1 >> 8) & 0xFF] ^ T[0][w1 & 0xFF];
-        }
-        if (i < we) {
-            const uint32_t word = *colp;
-            c = (uint32_t)T[3][((c >> 8) ^ (word >> 24)) & 0xFF] ^ T[2][((c & 0xFF) ^ (word >> 16)) & 0xFF] ^
-                T[1][(word >> 8) & 0xFF] ^ T[0][word & 0xFF];
-        }
-        uint32_t end = we * 4;
-        if (lane == (int)M.col(nfw - 1)) {
-            const uint32_t word = fbuf[M(nfw)];
-            for (uint32_t b = 0; b < tail; b++) {
-                const uint32_t byte = (word >> (24 - 8 * b)) & 0xFF;
-                c = ((c << 8) & 0xFFFFu) ^ S.crc8x[0][((c >> 8) ^ byte) & 0xFF];
-            }
-            end += tail;
-        }
-        const uint32_t m = body - end;
-        crc = dpp_wave_xor_u32(gf_mulmod(gf_mulmod(c, S.xlo[m & 63]), S.xhi[m >> 6]));
-        if (l0) lds_put_bits2(fbuf, M, body << 3, crc, 16);
     }
     if constexpr (SUB) {
         // the subframe's words (bits past end_bits are zeros) to its slot, then re-zero the buffer
@@ -3367,23 +3475,23 @@ __device__ __forceinline__ void encode_frame_v3(const typename Elem<DT>::T *rast
             for (uint32_t wi = (uint32_t)lane; wi < nw; wi += 64) dst[wi] = fbuf[M(wi)];
             for (uint32_t i = 0; i < M.c; i++) fbuf[(i << 6) | (uint32_t)lane] = 0;
         } else {
-            for (uint32_t i = (uint32_t)lane; i < (uint32_t)kBufWordsV3; i += 64) fbuf[i] = 0;
+            zero_wave_buf(fbuf, lane);
         }
         if (l0) sub_bits[sub] = ok ? (int32_t)end_bits : -1;
         (void)fbytes;
-        (void)crc;
         return;
     }
-    prev.f = f;
-    prev.fbytes = fbytes;
-    prev.ok = ok;
-    prev.map = M;
+    if (ok) {
+        const uint32_t crc = crc16_cols(fbuf, M, body, S, lane);
+        if (l0) lds_put_bits2(fbuf, M, body << 3, crc, 16);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_wave_barrier();
+    }
+    prev.f = f, prev.fbytes = fbytes, prev.ok = ok, prev.map = M;
 }
 
-// SUB = true: the units are the subframes (frame, channel) of a multi-channel job (encode_frame_v3<DT, true>); the
-// tile's partial last frame is coded whole by the generic kernels and skipped here.
 template <int DT, bool SUB = false>
-__global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *raster, EncodeParams P,
+__global__ void __launch_bounds__(256, sizeof(typename Elem<DT>::T) <= 2 ? 3 : 1) k_encode_v4(const typename Elem<DT>::T *raster, EncodeParams P,
                                                   const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
                                                   const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap,
                                                   int64_t *frame_off, uint64_t *status, int *ticket_ctr, int *err,
@@ -3391,7 +3499,7 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
                                                   int hdr_n, const uint32_t *__restrict__ pslots,
                                                   const int64_t *__restrict__ pbytes, uint32_t *sub_slots = nullptr,
                                                   int32_t *sub_bits = nullptr) {
-    __shared__ EncV3Shared S;
+    __shared__ __attribute__((aligned(16))) EncV3Shared S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int i = threadIdx.x; i < 4096; i += blockDim.x) (&S.crc8x[0][0])[i] = (&c_crc16x8[0][0])[i];
     for (int i = threadIdx.x; i < 256; i += blockDim.x) S.crc8[i] = c_crc8[i];
@@ -3417,7 +3525,7 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
         if (want != S.lut_tile) {  // WG-uniform
             const TileNorm tw = norms[want];
             if (tw.mode == kNormLut) {
-                const int64_t R = min(tw.imax - tw.imin, (int64_t)kLutCap - 1);  // (a LUT tile's range is below that)
+                const int64_t R = min(tw.imax - tw.imin, (int64_t)kLutCap - 1);
                 const int16_t *src = luts + (int64_t)want * kLutCap;
                 for (int64_t d = threadIdx.x; d <= R; d += blockDim.x) S.lut[d] = src[d];
             }
@@ -3431,15 +3539,15 @@ __global__ void __launch_bounds__(256) k_encode_v3(const typename Elem<DT>::T *r
                 const int chn = (int)(v - f * P.nch);
                 const TileGeom g = tiles[ftile[f]];
                 if (!(g.partial && f - g.frame_base == g.nframes - 1))
-                    encode_frame_v3<DT, true>(raster, P, tiles, norms, luts, ana, arena, arena_cap, frame_off, status,
-                                              err, S, want, f, lane, ftile, prev, hdr_tab, hdr_n, pslots, pbytes, chn,
+                    encode_frame_v4<DT, true>(raster, P, tiles, norms, ana, arena, arena_cap, frame_off, status, err, S,
+                                              want, f, lane, ftile, prev, hdr_tab, hdr_n, pslots, pbytes, chn,
                                               sub_slots, sub_bits);
             }
         } else {
             const int64_t f = fbase + wave;
             if (f < nunits)
-                encode_frame_v3<DT>(raster, P, tiles, norms, luts, ana, arena, arena_cap, frame_off, status, err, S,
-                                    want, f, lane, ftile, prev, hdr_tab, hdr_n, pslots, pbytes);
+                encode_frame_v4<DT>(raster, P, tiles, norms, ana, arena, arena_cap, frame_off, status, err, S, want, f,
+                                    lane, ftile, prev, hdr_tab, hdr_n, pslots, pbytes);
         }
     }
     if constexpr (!SUB)
@@ -4005,10 +4113,10 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
             prof_begin(ctx, "encode", &ev);
             {
                 static int nwg_max = 0;  // (per instantiation; the same gfx950 target for every device)
-                if (nwg_max == 0) FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nwg_max, k_encode_v3<DT, true>, 256, 0));
+                if (nwg_max == 0) FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nwg_max, k_encode_v4<DT, true>, 256, 0));
                 int64_t grid = (int64_t)std::max(1, nwg_max) * ctx->num_cus;
                 grid = std::min<int64_t>(grid, (nsub + 3) / 4);
-                k_encode_v3<DT, true><<<(unsigned)grid, 256, 0, st>>>(
+                k_encode_v4<DT, true><<<(unsigned)grid, 256, 0, st>>>(
                     raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(), dana, reinterpret_cast<uint8_t *>(arena_dev),
                     arena_cap, ctx->frame_off.as<int64_t>(), dstatus, ticket, err_flag, ctx->frame_tile.as<int32_t>(),
                     ctx->hdr_tab.as<uint4>(), 0, ctx->slots.as<uint32_t>(), dpbytes, dsub, dsbits);
@@ -4120,15 +4228,15 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         }
         {
             static int nwg_max = 0;  // (per instantiation; the same gfx950 target for every device)
-            if (nwg_max == 0) FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nwg_max, k_encode_v3<DT>, 256, 0));
+            if (nwg_max == 0) FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nwg_max, k_encode_v4<DT>, 256, 0));
             prof_begin(ctx, "encode", &ev);
             int64_t grid = (int64_t)std::max(1, nwg_max) * ctx->num_cus;
             grid = std::min<int64_t>(grid, (nframes + 3) / 4);
-            k_encode_v3<DT><<<(unsigned)grid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(), dana,
+            k_encode_v4<DT><<<(unsigned)grid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(), dana,
                                                             reinterpret_cast<uint8_t *>(arena_dev), arena_cap,
                                                             ctx->frame_off.as<int64_t>(), dstatus, ticket, err_flag,
-                                                            ctx->frame_tile.as<int32_t>(), ctx->hdr_tab.as<uint4>(), hdr_n,
-                                                            ctx->slots.as<uint32_t>(), dpbytes);
+                                                            ctx->frame_tile.as<int32_t>(), ctx->hdr_tab.as<uint4>(),
+                                                            hdr_n, ctx->slots.as<uint32_t>(), dpbytes);
             prof_end(ctx, "encode", ev);
         }
         FRS_HIP(ctx->host_pack.ensure(res_bytes));
@@ -4302,6 +4410,9 @@ static int run_encode_any(frs_ctx *ctx, const frs_encode_desc *d, const void *ra
 int encode_job(frs_ctx *ctx, const frs_encode_desc *d, const void *raster_dev, void *arena_dev, int64_t arena_cap,
                int64_t *tile_off, double *tile_min, double *tile_max, int32_t *stream_bps) {
     if (stream_bps) *stream_bps = stream_bps_of(d);
+#ifdef FRS_PROBE_I16  // (register probes: tools/kernel_regs.py --probe compiles the int16 kernels only)
+    return run_encode_any<FRS_DT_I16>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
+#else
     switch (d->dtype) {
     case FRS_DT_U8: return run_encode_any<FRS_DT_U8>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
     case FRS_DT_U16: return run_encode_any<FRS_DT_U16>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
@@ -4312,6 +4423,7 @@ int encode_job(frs_ctx *ctx, const frs_encode_desc *d, const void *raster_dev, v
     case FRS_DT_F64: return run_encode_any<FRS_DT_F64>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
     default: ctx->err = "bad dtype"; return FRS_E_ARG;
     }
+#endif
 }
 
 }  // namespace frs

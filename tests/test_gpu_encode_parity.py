@@ -266,3 +266,27 @@ def test_many_small_tiles_match_oracle():
             assert list(off) == list(o_off)
             assert arena.tobytes() == o_arena.tobytes()
             assert list(mn) == list(o_mn) and list(mx) == list(o_mx)
+
+
+@pytest.mark.parametrize("kind", ["spikes", "burst", "steps16"])
+def test_lane_segment_overflow_matches_oracle(gpu_ctx, kind):
+    """The fast encoder packs each lane's 64 Rice codes into a private LDS column of 1088 bits; a lane whose codes
+    outgrow it (a residual spike in a smooth frame: one code of thousands of unary bits) makes the wave repack the
+    frame at its known offsets, and a lane whose segment is far longer than the frame's per-lane average spans
+    three columns of the frame layout.  Frames of every kind must still be the oracle's bytes."""
+    rng = np.random.default_rng(77)
+    H = W = 512
+    y, x = np.meshgrid(np.linspace(0, 6, H), np.linspace(0, 6, W), indexing="ij")
+    band = (2000 + 900 * np.sin(x) * np.cos(y)).astype(np.int16)
+    if kind == "spikes":      # isolated +-30000 samples: single huge codes
+        band.flat[rng.choice(band.size, 60, replace=False)] = rng.choice([-30000, 30000], 60).astype(np.int16)
+    elif kind == "burst":     # a 64-sample run of noise inside smooth frames: one lane's segment ~16 bits/sample
+        for f in range(0, band.size // 4096, 3):
+            s = f * 4096 + 64 * int(rng.integers(1, 63))
+            band.flat[s:s + 64] = rng.integers(-32000, 32000, 64).astype(np.int16)
+    else:                     # steps of exactly 16-bit residual magnitude on alternate lanes
+        band.flat[::128] += 16000
+    arena, off, mn, mx, bps = _gpu_tiles(gpu_ctx, band, 256)
+    o_arena, o_off, o_mn, o_mx = O.encode_tiles(band, 256, threads=8)
+    assert list(off) == list(o_off)
+    assert arena.tobytes() == o_arena.tobytes()
