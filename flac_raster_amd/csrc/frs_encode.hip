@@ -2154,10 +2154,8 @@ __device__ inline void ana_autoc(const typename Elem<DT>::T *base, const EncodeP
     double prev[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) prev[j] = 0.0;
-    // fixed-predictor totals (fixed.c FLAC__fixed_compute_best_predictor: sum of |e_k(i)| over samples 4..n-1) on the
-    // unshifted samples; the first four samples' terms are subtracted at the end (snapshot after sample 3)
-    uint32_t x1 = 0x80000000u, e1p = 0x80000000u, e2p = 0x80000000u, e3p = 0x80000000u;  // biased zeros
-    uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0, s0t = 0, s1t = 0, s2t = 0, s3t = 0, s4t = 0;
+    // (the fixed-predictor totals of fixed.c are the encoder's: encode_frame_v4 forms them lane-parallel from the
+    // samples it has loaded anyway, which takes ~12 integer ops per sample out of this fp64-bound pass)
     for (int c = 0; c < kMaxBlock / kAnaChunk; c++) {
         const int i0 = c * kAnaChunk;
         Ch ch;
@@ -2175,25 +2173,6 @@ __device__ inline void ana_autoc(const typename Elem<DT>::T *base, const EncodeP
                 const int32_t x = ana_norm<DT, KIND>(ch.get(8 * b + j), tn, slut, glut);
                 or_acc |= (uint32_t)x;
                 cur[j] = (double)((float)x * swin[i0 + 8 * b + j]);  // lpc.c window_data: float product
-                // sign-flipped differences (y = e ^ 2^31): |e_{k+1}| = v_sad_u32(y_k(i), y_k(i-1)) in one op
-                const uint32_t y0 = (uint32_t)x ^ 0x80000000u;
-                const uint32_t y1 = (y0 - x1) ^ 0x80000000u, y2 = (y1 - e1p) ^ 0x80000000u, y3 = (y2 - e2p) ^ 0x80000000u;
-                t0 = ana_sad(y0, 0x80000000u, t0);
-                t1 = ana_sad(y0, x1, t1);
-                t2 = ana_sad(y1, e1p, t2);
-                t3 = ana_sad(y2, e2p, t3);
-                t4 = ana_sad(y3, e3p, t4);
-                x1 = y0;
-                e1p = y1;
-                e2p = y2;
-                e3p = y3;
-                if (b == 0 && j == 3 && c == 0) {
-                    s0t = t0;
-                    s1t = t1;
-                    s2t = t2;
-                    s3t = t3;
-                    s4t = t4;
-                }
             }
 #pragma unroll
             for (int j = 0; j < 8; j++) {
@@ -2204,11 +2183,8 @@ __device__ inline void ana_autoc(const typename Elem<DT>::T *base, const EncodeP
             for (int j = 0; j < 8; j++) prev[j] = cur[j];
         }
     }
-    ft[0] = t0 - s0t;
-    ft[1] = t1 - s1t;
-    ft[2] = t2 - s2t;
-    ft[3] = t3 - s3t;
-    ft[4] = t4 - s4t;
+#pragma unroll
+    for (int k = 0; k < 5; k++) ft[k] = 0;  // (unused: the encoder forms the fixed totals)
 }
 
 // min/max of a whole tile by one wave (16-bit samples, 16-B aligned rows): 16-B loads, kStatsLoads in flight per lane,
@@ -2807,39 +2783,50 @@ __device__ __forceinline__ void resolve_and_store(const EncodeParams &P, Pending
     pf.f = -1;
 }
 
-// Sum of |e_K(j)| (order-K fixed residual) over a lane's 64 samples, packed as int16 pairs E[4 + m] = (x[2m],
-// x[2m+1]) with E[2..3] = the previous lane's last four samples; lane 0 starts at j = K (the warm-up).  Differences
-// are carried sign-flipped (y = e ^ 2^31) so |e_{k+1}| = v_sad_u32(y_k(i), y_k(i-1)) in one op.
-template <int K>
-__device__ inline uint32_t fixed_lane_sum(const uint32_t *E, bool l0) {
+// fixed.c FLAC__fixed_compute_best_predictor, lane-parallel: this lane's sums of |e_k(i)|, k = 0..4, over its 64 samples
+// (packed pairs E[4 + m], E[2..3] = the previous lane's last four samples), lane 0 from sample 4 (tk); and lane 0's
+// terms at k <= i < 4 (hk: with tk, the fixed candidate's Rice sum from its warm-up on).  Differences are carried
+// sign-flipped (y = e ^ 2^31) so |e_{k+1}| = v_sad_u32(y_k(i), y_k(i-1)) in one op.
+__device__ inline void fixed_lane_totals(const uint32_t *E, bool l0, uint32_t *tk, uint32_t *hk) {
     constexpr uint32_t M = 0x80000000u;
     const int32_t h1 = (int32_t)E[3] >> 16, h2 = (int16_t)(E[3] & 0xFFFFu);
     const int32_t h3 = (int32_t)E[2] >> 16, h4 = (int16_t)(E[2] & 0xFFFFu);
     uint32_t p0 = (uint32_t)h1 ^ M, p1 = (uint32_t)(h1 - h2) ^ M, p2 = (uint32_t)((h1 - h2) - (h2 - h3)) ^ M;
     uint32_t p3 = (uint32_t)(((h1 - h2) - (h2 - h3)) - ((h2 - h3) - (h3 - h4))) ^ M;
-    uint32_t s = 0;
+    uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+#pragma unroll
+    for (int k = 0; k < 5; k++) hk[k] = 0;
 #pragma unroll
     for (int j = 0; j < 64; j++) {
         const uint32_t v = E[4 + (j >> 1)];
         const int32_t x = (j & 1) ? ((int32_t)v >> 16) : (int32_t)(int16_t)(v & 0xFFFFu);
         const uint32_t y0 = (uint32_t)x ^ M;
-        uint32_t y1 = 0, y2 = 0, y3 = 0, a, b;
-        if constexpr (K >= 2) y1 = (y0 - p0) ^ M;
-        if constexpr (K >= 3) y2 = (y1 - p1) ^ M;
-        if constexpr (K >= 4) y3 = (y2 - p2) ^ M;
-        if constexpr (K == 0) { a = y0; b = M; }
-        else if constexpr (K == 1) { a = y0; b = p0; }
-        else if constexpr (K == 2) { a = y1; b = p1; }
-        else if constexpr (K == 3) { a = y2; b = p2; }
-        else { a = y3; b = p3; }
-        if (j < K) s = l0 ? s : sad_u32(a, b, s);
-        else s = sad_u32(a, b, s);
+        const uint32_t y1 = (y0 - p0) ^ M, y2 = (y1 - p1) ^ M, y3 = (y2 - p2) ^ M;
+        if (j < 4) {  // lane 0: not in the totals; its order-k terms from i = k are the Rice sum's
+            hk[0] = sad_u32(y0, M, hk[0]);
+            if (j >= 1) hk[1] = sad_u32(y0, p0, hk[1]);
+            if (j >= 2) hk[2] = sad_u32(y1, p1, hk[2]);
+            if (j >= 3) hk[3] = sad_u32(y2, p2, hk[3]);
+            if (!l0) {
+                t0 = sad_u32(y0, M, t0);
+                t1 = sad_u32(y0, p0, t1);
+                t2 = sad_u32(y1, p1, t2);
+                t3 = sad_u32(y2, p2, t3);
+                t4 = sad_u32(y3, p3, t4);
+            }
+        } else {
+            t0 = sad_u32(y0, M, t0);
+            t1 = sad_u32(y0, p0, t1);
+            t2 = sad_u32(y1, p1, t2);
+            t3 = sad_u32(y2, p2, t3);
+            t4 = sad_u32(y3, p3, t4);
+        }
         p0 = y0;
-        if constexpr (K >= 2) p1 = y1;
-        if constexpr (K >= 3) p2 = y2;
-        if constexpr (K >= 4) p3 = y3;
+        p1 = y1;
+        p2 = y2;
+        p3 = y3;
     }
-    return s;
+    tk[0] = t0, tk[1] = t1, tk[2] = t2, tk[3] = t3, tk[4] = t4;
 }
 
 // libFLAC's set_partitioned_rice_ (stream_encoder.c) for the fixed and LPC candidates of a 4096-sample frame: orders
@@ -3137,11 +3124,20 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
         return (j & 1) ? ((int32_t)v >> 16) : (int32_t)(int16_t)(v & 0xFFFFu);
     };
 
-    // ---- candidates (as v3): fixed order guess + totals from the analysis, the fixed and LPC lane |r| sums
-    const int guess = A.fixed_order;
-    const uint32_t tg = A.fixed_tg;
+    // ---- candidates: the fixed order guess from the totals (fixed.c: first minimum under <=), its lane sum; the LPC
+    //      lane |r| sum
+    uint32_t tk[5], hk[5], Tt[5];
+    fixed_lane_totals(E, l0, tk, hk);
+    dpp_wave_sum_multi<5>(tk, Tt);
+    int guess;
+    if (Tt[0] <= min(min(Tt[1], Tt[2]), min(Tt[3], Tt[4]))) guess = 0;
+    else if (Tt[1] <= min(min(Tt[2], Tt[3]), Tt[4])) guess = 1;
+    else if (Tt[2] <= min(Tt[3], Tt[4])) guess = 2;
+    else if (Tt[3] <= Tt[4]) guess = 3;
+    else guess = 4;
+    const uint32_t tg = guess == 0 ? Tt[0] : guess == 1 ? Tt[1] : guess == 2 ? Tt[2] : guess == 3 ? Tt[3] : Tt[4];
     const double dn = (double)(n - 4);
-    const float fb1 = (float)(A.fixed_t1 > 0 ? log(M_LN2 * (double)A.fixed_t1 / dn) / M_LN2 : 0.0);
+    const float fb1 = (float)(Tt[1] > 0 ? log(M_LN2 * (double)Tt[1] / dn) / M_LN2 : 0.0);
     const float fbg = (float)(tg > 0 ? log(M_LN2 * (double)tg / dn) / M_LN2 : 0.0);
     bool constant = false;
     if (fb1 == 0.0f) {
@@ -3156,16 +3152,9 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
     const bool cand_fixed = !constant && !(fbg >= (float)sbps);
     const bool cand_lpc = !constant && (A.flags & kFlagLpcOk);
     const int of = guess, ol = A.lpc_order, lshift = A.lpc_shift;
-    uint32_t sf = 0;
-    if (cand_fixed) {
-        switch (of) {  // wave-uniform
-        case 0: sf = fixed_lane_sum<0>(E, l0); break;
-        case 1: sf = fixed_lane_sum<1>(E, l0); break;
-        case 2: sf = fixed_lane_sum<2>(E, l0); break;
-        case 3: sf = fixed_lane_sum<3>(E, l0); break;
-        default: sf = fixed_lane_sum<4>(E, l0); break;
-        }
-    }
+    // the fixed candidate's lane sum of |e_of(i)|, lane 0 from i = of (the totals start at 4: lane 0 adds its i < 4)
+    uint32_t sf = of == 0 ? tk[0] + (l0 ? hk[0] : 0u) : of == 1 ? tk[1] + (l0 ? hk[1] : 0u)
+                : of == 2 ? tk[2] + (l0 ? hk[2] : 0u) : of == 3 ? tk[3] + (l0 ? hk[3] : 0u) : tk[4];
     uint32_t CL[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) CL[k] = pack2(A.q[2 * k + 1], A.q[2 * k]);
