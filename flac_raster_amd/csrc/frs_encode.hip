@@ -3165,13 +3165,11 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
             if (m % 4 == 0 && m) asm volatile("" : "+v"(sl));
             int32_t re, ro;
             residual_pair(E, CL, lshift, m, re, ro);
-            const uint32_t ae = (uint32_t)abs(re), ao = (uint32_t)abs(ro);
-            if (2 * m < kMaxLpc) {
-                sl += (l0 && 2 * m < ol) ? 0u : ae;
-                sl += (l0 && 2 * m + 1 < ol) ? 0u : ao;
-            } else {
-                sl += ae + ao;
-            }
+            // |r| + sl in one v_sad_u32 on the sign-flipped residual
+            const uint32_t se = sad_u32((uint32_t)re ^ 0x80000000u, 0x80000000u, sl);
+            sl = (2 * m < kMaxLpc && l0 && 2 * m < ol) ? sl : se;
+            const uint32_t so = sad_u32((uint32_t)ro ^ 0x80000000u, 0x80000000u, sl);
+            sl = (2 * m + 1 < kMaxLpc && l0 && 2 * m + 1 < ol) ? sl : so;
         }
     }
     reg_fence(E);
@@ -3260,7 +3258,7 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
             run = 4;
             pcol[0] = (uint32_t)k << 28;
         }
-        const uint32_t sh = 31u - (uint32_t)k, oneL = 0x80000000u;
+        const uint32_t sh = 31u - (uint32_t)k, oneL = 0x80000000u, k1 = 1u + (uint32_t)k;
 #pragma unroll
         for (int m = 0; m < 32; m++) {
             if (m % 4 == 0 && m) asm volatile("" : "+v"(run));
@@ -3270,17 +3268,17 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
             for (int h = 0; h < 2; h++) {
                 const int j = 2 * m + h;
                 const uint32_t u = zigzag(h ? ro : re);
-                uint32_t q = u >> k, codeL = (u << sh) | oneL, adv = q + 1 + (uint32_t)k;
-                if (j < kMaxLpc && l0 && j < o) {
-                    q = 0;
+                uint32_t codeL = (u << sh) | oneL;
+                uint32_t p = run + (u >> k);  // the code's stop bit (its unary zeros are the buffer's)
+                const bool warm = j < kMaxLpc && l0 && j < o;  // (lane 0's warm-up samples: no code)
+                if (warm) {
                     codeL = 0;
-                    adv = 0;
+                    p = run;
                 }
-                const uint32_t p = run + q;
                 uint32_t *a = pcol + (min(p >> 5, (uint32_t)(kPrivRows - 1)) << 6);
                 atomicOr(a, __builtin_amdgcn_alignbit(0u, codeL, p));
                 atomicOr(a + 64, __builtin_amdgcn_alignbit(codeL, 0u, p));
-                run += adv;
+                run = warm ? run : p + k1;
             }
         }
         over = __ballot(run > kPrivBits) != 0;
