@@ -43,8 +43,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E peak 8.0 TB/s
 VALU_PEAK_GINST_S = 1024 * 2.4 * 0.5
 METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"] if (ROOT / "BASELINE.json").exists() else \
     "Mpixels/sec encode (create-streaming) + bbox-extract ms, 1/2/4/8 GPU; bit-exact vs ref"
-KERNEL_SYMBOL = {"encode": "frs::k_encode_v3<3, false>", "analyze": "frs::k_analyze_v3<3, false, true>",
-                 "stats": "frs::k_tile_stats_vec<3>", "fused": "frs::k_fused_v6<3>"}
+KERNEL_SYMBOL = {"encode": "frs::k_encode_v4<3, false>", "analyze": "frs::k_analyze_v3<3, false, true>",
+                 "stats": "frs::k_tile_stats_vec<3>"}
 
 
 def parse():
@@ -155,17 +155,16 @@ def main():
         elapsed = float(comm.allgather_i64(np.array([int(elapsed * 1e9)])).max()) * 1e-9
     total_px = H * W
 
-    kernels = {k: ctx.profile_avg_ms(k) for k in ("stats", "analyze", "partial", "encode", "fused", "compact")}
+    kernels = {k: ctx.profile_avg_ms(k) for k in ("stats", "analyze", "partial", "encode", "compact")}
     kernels = {k: v for k, v in kernels.items() if v > 0}
     comp_bytes = int(off[-1])
     px_rank = rows * W
     # algorithmic bytes per launch: stats reads 2 B/px; analyze reads 2 B/px (4 B/px when the tile
     # stats are fused into it: min/max pass + autocorrelation pass); encode reads 2 B/px and writes the frames;
-    # compact reads + writes the frames; fused (k_fused_v6: stats, analysis and encode in one launch) reads 2 B/px
-    # and writes the frames, like the encoder alone (its two extra reads of the band are not algorithmic bytes).
+    # compact reads + writes the frames.
     fused = "stats" not in kernels
     algo = {"stats": 2 * px_rank, "analyze": (4 if fused else 2) * px_rank, "encode": 2 * px_rank + comp_bytes,
-            "fused": 2 * px_rank + comp_bytes, "compact": 2 * comp_bytes, "partial": 0}
+            "compact": 2 * comp_bytes, "partial": 0}
     dom = max(kernels, key=lambda k: kernels[k]) if kernels else "encode"
     dom_ms = kernels.get(dom, float("nan"))
     achieved = algo.get(dom, 0) / (dom_ms * 1e-3) / 1e9
@@ -194,7 +193,10 @@ def main():
         "kernels_ms": {k: round(v, 4) for k, v in kernels.items()},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic_for(args.traffic_json, dom, px_rank)},
+                     "traffic": traffic_for(args.traffic_json, dom, px_rank),
+                     # the north-star figure: the band's 2 B/px read once per step against the HBM read peak
+                     "step_read": {"bytes": 2 * px_rank, "achieved": round(2 * px_rank / (ms_per_step * 1e-3) / 1e9, 1),
+                                   "frac": round(2 * px_rank / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}},
     }
     if comm is not None:
         result["allgather_us"] = allgather_figures(comm, ag_s, np.diff(off), counts)
@@ -381,7 +383,7 @@ def sentinel2(ctx, steps=5):
     ctx.sync()
     dt = (time.perf_counter() - t0) / steps
     ctx.profile(False)
-    kern = {k: round(ctx.profile_avg_ms(k), 4) for k in ("stats", "analyze", "partial", "encode", "fused", "compact")}
+    kern = {k: round(ctx.profile_avg_ms(k), 4) for k in ("stats", "analyze", "partial", "encode", "compact")}
     arena.close()
     buf.close()
     return {"raster": f"{H}x{W} uint16", "tile_size": T, "tiles": 121, "ms_per_step": round(dt * 1e3, 3),
@@ -408,7 +410,7 @@ def convert_multiband(ctx, steps=3):
     ctx.sync()
     dt = (time.perf_counter() - t0) / steps
     ctx.profile(False)
-    kern = {k: round(ctx.profile_avg_ms(k), 4) for k in ("stats", "analyze", "partial", "encode", "fused", "assemble", "compact")}
+    kern = {k: round(ctx.profile_avg_ms(k), 4) for k in ("stats", "analyze", "partial", "encode", "assemble", "compact")}
     # the mirror (flac_to_tiff, converter.py:241-282): the whole stream decoded + de-normalised in one call
     _, mn, mx, _ = ctx.encode_tiles_device(buf.ptr, d, arena)
     out = ctx.alloc(B * H * W * 2)
@@ -453,7 +455,7 @@ def _timed_encode(ctx, buf, d, steps):
     ctx.sync()
     dt = (time.perf_counter() - t0) / steps
     ctx.profile(False)
-    kern = {k: round(ctx.profile_avg_ms(k), 4) for k in ("stats", "analyze", "partial", "encode", "fused", "assemble", "compact")}
+    kern = {k: round(ctx.profile_avg_ms(k), 4) for k in ("stats", "analyze", "partial", "encode", "assemble", "compact")}
     arena.close()
     return dt, int(off[-1]), {k: v for k, v in kern.items() if v > 0}
 

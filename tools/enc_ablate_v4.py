@@ -161,6 +161,15 @@ def phases(src):
 
 VARIANTS["v4phases"] = phases
 
+
+# analysis at 5 waves per SIMD (32-sample loads per lane: 94 VGPRs; 5 x 32 KB of LUTs fill the LDS)
+VARIANTS["ana5"] = chain(
+    gsub("__global__ void __launch_bounds__(256) k_analyze_v3(", "__global__ void __launch_bounds__(256, SLOW ? 1 : 5) k_analyze_v3("),
+    gsub("    constexpr int kChunk = SLOW ? 16 : 64;", "    constexpr int kChunk = SLOW ? 16 : 32;"))
+VARIANTS["ana5c64"] = gsub("__global__ void __launch_bounds__(256) k_analyze_v3(",
+                           "__global__ void __launch_bounds__(256, SLOW ? 1 : 5) k_analyze_v3(")
+
+
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
     for n in names:
