@@ -462,8 +462,9 @@ def _timed_encode(ctx, buf, d, steps):
 
 def convert_2band(ctx, steps=3):
     """Plain `convert` of a 16384 x 16384 x 2 int16 raster as ONE two-channel stream (converter.py:185-216): libFLAC
-    level 5's exhaustive mid/side search (L, R, M, S coded per frame, the cheapest assignment kept) -- the generic
-    kernels, device-resident."""
+    level 5's exhaustive mid/side search (L, R, M, S coded per frame, the cheapest assignment kept), device-resident:
+    the fast kernels (k_analyze_v3 of the four signals, k_encode_v4 of L/R/M as packed pairs and of the 17-bit side as
+    int32, the assignment picked from the subframe estimates in k_mc_frame_bytes, k_mc_assemble)."""
     B, H, W = 2, 16384, 16384
     buf = ctx.alloc(B * H * W * 2)
     ctx.synth_raster(buf, B, H, W, seed=6)
@@ -472,7 +473,8 @@ def convert_2band(ctx, steps=3):
     buf.close()
     return {"raster": f"{H}x{W}x{B} int16", "streams": 1, "channels": B, "ms_per_step": round(dt * 1e3, 3),
             "Mpixels_s": round(H * W / dt / 1e6, 1), "compressed_bytes": nbytes, "kernels_ms": kern,
-            "path": "generic kernels (k_analyze L/R/M/S + k_encode_frames, frame per work-group)"}
+            "path": ("generic kernels (k_analyze L/R/M/S + k_encode_frames, frame per work-group)" if "compact" in kern
+                     else "fast two-channel kernels (wave per subframe; picks from the estimates; k_mc_assemble)")}
 
 
 def raw_frames(ctx, steps=3):

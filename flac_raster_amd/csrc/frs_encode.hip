@@ -828,7 +828,7 @@ __global__ void __launch_bounds__(128) k_analyze_lpc_hi(const typename Elem<DT>:
 // thread l in libFLAC's sequential order (the same fma sequence as k_analyze's lane, so bit-identical); the fixed
 // totals, the OR and the constant test are integer reductions (order-free); thread 0 makes the decisions.
 constexpr int kPartThreads = 256;
-template <int DT>
+template <int DT, bool ST = false>
 __global__ void __launch_bounds__(kPartThreads) k_analyze_partial(const typename Elem<DT>::T *raster, EncodeParams P,
                                                                  const TileGeom *tiles, const TileNorm *norms,
                                                                  const float *__restrict__ window, SubAnalysis *out,
@@ -846,8 +846,8 @@ __global__ void __launch_bounds__(kPartThreads) k_analyze_partial(const typename
     const int64_t tile_px = (int64_t)g.h * g.w;
     const int n = (int)((tile_px - s0) < P.blocksize ? (tile_px - s0) : P.blocksize);
     const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits, P.norm_mode);
-    const int chn = blockIdx.y;  // channel (multi-channel jobs: grid.y = nch)
-    const T *tb = raster + (int64_t)(P.band0 + chn) * P.band_stride + g.r0 * P.row_stride + g.c0;
+    const int chn = blockIdx.y;  // channel (multi-channel jobs: grid.y = nch; a two-channel stream: L, R, M, S)
+    const T *tb = raster + (int64_t)(P.band0 + (ST ? 0 : chn)) * P.band_stride + g.r0 * P.row_stride + g.c0;
     if (threadIdx.x < 5) red_t[threadIdx.x] = 0;
     if (threadIdx.x == 0) red_or = red_diff = 0;
     // 1. normalise + window (samples past n are zeros, as in k_analyze)
@@ -855,7 +855,8 @@ __global__ void __launch_bounds__(kPartThreads) k_analyze_partial(const typename
         int32_t x = 0;
         if (i < n) {
             const int64_t q = s0 + i, r = q / g.w;
-            x = nz(tb[r * P.row_stride + (q - r * g.w)]);
+            if constexpr (ST) x = coded_sample<DT, true, int32_t>(tb + r * P.row_stride + (q - r * g.w), P.band_stride, nz, chn);
+            else x = nz(tb[r * P.row_stride + (q - r * g.w)]);
         }
         xs[i] = x;
         xw[i] = (double)((float)x * window[i]);
@@ -901,7 +902,7 @@ __global__ void __launch_bounds__(kPartThreads) k_analyze_partial(const typename
 #pragma unroll
         for (int l = 0; l <= kMaxLpc; l++) acc[l] = red_acc[l];
         const uint64_t tt[5] = {red_t[0], red_t[1], red_t[2], red_t[3], red_t[4]};
-        out[f * P.nch + chn] = generic_decide<false>(acc, tt, red_or, red_diff, n, P);
+        out[f * P.nvch + chn] = generic_decide<false>(acc, tt, red_or, red_diff, n, P, (ST && chn == 3) ? 1 : 0);
     }
 }
 
@@ -1996,12 +1997,12 @@ __device__ inline void norm_block8(const Chunk64<DT> &ch, int b, const TileNorm 
 // wasted bits, LPC order choice (expected bits), Levinson coefficients and quantisation of one frame from its
 // windowed autocorrelation sums (stream_encoder.c process_subframe_ / lpc.c)
 __device__ inline SubAnalysis analysis_finish(const double *acc, uint32_t or_acc, int n, const EncodeParams &P,
-                                              const uint32_t *ft) {
+                                              const uint32_t *ft, int extra = 0) {
     SubAnalysis A;
     A.n = n;
     int w = or_acc ? __builtin_ctz(or_acc) : 0;
     if (w > P.bps) w = P.bps;
-    const int sbps = P.bps - w;
+    const int sbps = P.bps - w + extra;  // (extra = 1: a two-channel stream's side signal)
     A.wasted = w;
     A.flags = 0;
     {
@@ -2143,10 +2144,14 @@ __device__ inline uint32_t ana_sad(uint32_t a, uint32_t b, uint32_t c) {  // |a 
     return d;
 }
 
-template <int DT, int KIND, int kAnaChunk>
+// ST: `base` is the left band and sig (0..3) the coded signal of a two-channel stream's mid/side pass: left, right,
+// mid = (L + R) >> 1, side = L - R (converter.py:185-194 interleaves the bands; libFLAC process_subframes_ forms mid
+// and side from the normalised samples)
+template <int DT, int KIND, int kAnaChunk, bool ST = false>
 __device__ inline void ana_autoc(const typename Elem<DT>::T *base, const EncodeParams &P, const TileGeom &g,
                                  int64_t s0, const TileNorm &tn, const int16_t *slut, const int16_t *glut,
-                                 const float *__restrict__ swin, int vec, double *acc, uint32_t &or_acc, uint32_t *ft) {
+                                 const float *__restrict__ swin, int vec, double *acc, uint32_t &or_acc, uint32_t *ft,
+                                 int sig = 0) {
     using Ch = ChunkN<DT, kAnaChunk>;
     const uint32_t r0 = udiv_inv((uint32_t)s0, (uint32_t)g.w, 1.0 / (double)g.w);
     int64_t crow = r0;
@@ -2158,8 +2163,9 @@ __device__ inline void ana_autoc(const typename Elem<DT>::T *base, const EncodeP
     // samples it has loaded anyway, which takes ~12 integer ops per sample out of this fp64-bound pass)
     for (int c = 0; c < kMaxBlock / kAnaChunk; c++) {
         const int i0 = c * kAnaChunk;
-        Ch ch;
-        ch.template load<true>(base, P.row_stride, g.w, crow, ccol, vec, kAnaChunk);
+        Ch ch, ch1;
+        if (!ST || sig != 1) ch.template load<true>(base, P.row_stride, g.w, crow, ccol, vec, kAnaChunk);
+        if (ST && sig >= 1) ch1.template load<true>(base + P.band_stride, P.row_stride, g.w, crow, ccol, vec, kAnaChunk);
         ccol += kAnaChunk;
         while (ccol >= g.w) {
             ccol -= g.w;
@@ -2170,7 +2176,14 @@ __device__ inline void ana_autoc(const typename Elem<DT>::T *base, const EncodeP
             double cur[8];
 #pragma unroll
             for (int j = 0; j < 8; j++) {
-                const int32_t x = ana_norm<DT, KIND>(ch.get(8 * b + j), tn, slut, glut);
+                int32_t x;
+                if constexpr (ST) {
+                    const int32_t l = sig == 1 ? 0 : ana_norm<DT, KIND>(ch.get(8 * b + j), tn, slut, glut);
+                    const int32_t r = sig == 0 ? 0 : ana_norm<DT, KIND>(ch1.get(8 * b + j), tn, slut, glut);
+                    x = sig == 0 ? l : sig == 1 ? r : sig == 2 ? (l + r) >> 1 : l - r;
+                } else {
+                    x = ana_norm<DT, KIND>(ch.get(8 * b + j), tn, slut, glut);
+                }
                 or_acc |= (uint32_t)x;
                 cur[j] = (double)((float)x * swin[i0 + 8 * b + j]);  // lpc.c window_data: float product
             }
@@ -2247,7 +2260,7 @@ __device__ inline void wave_tile_minmax(const typename Elem<DT>::T *base, int64_
 // and normalisation parameters (k_tile_stats_vec + k_tile_finalize) and builds the tile's LUT (k_build_lut) in
 // LDS and in global memory for the encoder -- the tile is read twice, but the separate stats pass and its
 // launches are gone.  A slow-class tile only gets its parameters written here; the SLOW launch analyses it.
-template <int DT, bool SLOW, bool STATS = false>
+template <int DT, bool SLOW, bool STATS = false, bool ST = false>
 __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *raster, EncodeParams P,
                                                    const TileGeom *tiles, TileNorm *norms,
                                                    int16_t *luts, const float *__restrict__ window,
@@ -2260,7 +2273,9 @@ __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *
     const int2 wt = wtab[wv];  // (tile, first frame of the tile handled by this wave)
     const int t = wt.x, k0w = wt.y & 0xFFFFFF, chn = wt.y >> 24;  // (tile, first frame | channel << 24)
     const TileGeom g = tiles[t];
-    const typename Elem<DT>::T *base = raster + (int64_t)(P.band0 + chn) * P.band_stride + g.r0 * P.row_stride + g.c0;
+    // (ST: the left band; ana_autoc reads the right one at + band_stride)
+    const typename Elem<DT>::T *base = raster + (int64_t)(P.band0 + (ST ? 0 : chn)) * P.band_stride +
+                                       g.r0 * P.row_stride + g.c0;
     int16_t *glut = luts + (int64_t)t * kLutCap;
     TileNorm tn;
     if constexpr (STATS) {
@@ -2304,18 +2319,20 @@ __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *
             }
             __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's LUT stores have landed (each wave reads only its own)
             __builtin_amdgcn_wave_barrier();
-            ana_autoc<DT, kAnaKindLds, kChunk>(base, P, g, s0, tn, wl, glut, window, vec, acc, or_acc, ft);
+            ana_autoc<DT, kAnaKindLds, kChunk, ST>(base, P, g, s0, tn, wl, glut, window, vec, acc, or_acc, ft, chn);
         } else {
-            ana_autoc<DT, kAnaKindZero, kChunk>(base, P, g, s0, tn, wl, glut, window, vec, acc, or_acc, ft);
+            ana_autoc<DT, kAnaKindZero, kChunk, ST>(base, P, g, s0, tn, wl, glut, window, vec, acc, or_acc, ft, chn);
         }
     } else {
         if (mode == kNormFastDiv)
-            ana_autoc<DT, kAnaKindFastDiv, kChunk>(base, P, g, s0, tn, nullptr, glut, window, vec, acc, or_acc, ft);
+            ana_autoc<DT, kAnaKindFastDiv, kChunk, ST>(base, P, g, s0, tn, nullptr, glut, window, vec, acc, or_acc, ft,
+                                                       chn);
         else
-            ana_autoc<DT, kAnaKindGeneric, kChunk>(base, P, g, s0, tn, nullptr, glut, window, vec, acc, or_acc, ft);
+            ana_autoc<DT, kAnaKindGeneric, kChunk, ST>(base, P, g, s0, tn, nullptr, glut, window, vec, acc, or_acc, ft,
+                                                       chn);
     }
     if (!live) return;
-    out[f * P.nch + chn] = analysis_finish(acc, or_acc, n, P, ft);
+    out[f * P.nvch + chn] = analysis_finish(acc, or_acc, n, P, ft, (ST && chn == 3) ? 1 : 0);
 }
 
 // ---- wave helpers (64 lanes)
@@ -2526,6 +2543,8 @@ constexpr uint64_t kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62, kValMask = (1u
 
 constexpr int kXpowHi = (kXpowBytes + 63) / 64;
 constexpr int kBufWordsV3 = kFrameWordsV3 + 64;  // + the overflow row of the code writer (lds_put_left)
+// a subframe slot (multi-channel streams): a frame's words, or the 17-bit VERBATIM side subframe (2177 words)
+constexpr int kSubWords = kFrameWordsV3 + 4;
 struct EncV3Shared {
     uint32_t bits[4][kBufWordsV3];
     int16_t lut[kLutCap];
@@ -2829,6 +2848,131 @@ __device__ inline void fixed_lane_totals(const uint32_t *E, bool l0, uint32_t *t
     tk[0] = t0, tk[1] = t1, tk[2] = t2, tk[3] = t3, tk[4] = t4;
 }
 
+// A lane's 64 consecutive samples of one coded signal, and the residual / fixed-predictor arithmetic on them.
+// LanePairs (16-bit signals): E[4 + m] = (x[2m], x[2m+1]) as int16 pairs, E[0..3] = the previous lane's last 8
+// samples (zeros on lane 0); LPC residuals by v_dot2 on packed pairs.  LaneWide (the 17-bit side signal of a
+// two-channel stream, L - R): X[8 + j] = x[j] as int32, X[0..7] the previous lane's last 8; residuals by 24-bit
+// multiply-adds (every sample and coefficient fits 24 bits; the sum stays below 2^31, libFLAC's 32-bit residual
+// path: subframe bps + precision + log2(order) <= 32).
+struct LanePairs {
+    uint32_t E[36];
+    struct Coefs {
+        uint32_t C[4];
+    };
+    __device__ inline int32_t x(int j) const {
+        const uint32_t v = E[4 + (j >> 1)];
+        return (j & 1) ? ((int32_t)v >> 16) : (int32_t)(int16_t)(v & 0xFFFFu);
+    }
+    __device__ inline void history() {
+#pragma unroll
+        for (int m = 0; m < 4; m++) E[m] = dpp_wave_shr1(E[32 + m]);
+        reg_fence(E);
+    }
+    __device__ inline void fence() { reg_fence(E); }
+    __device__ inline void totals(bool l0, uint32_t *tk, uint32_t *hk) const { fixed_lane_totals(E, l0, tk, hk); }
+    __device__ inline uint32_t diff_from_first() const {  // OR of (x ^ x[0]) over the lane (wave-uniform x[0])
+        const uint32_t x0 = uni(E[4] & 0xFFFFu);
+        const uint32_t xx = x0 | (x0 << 16);
+        uint32_t diff = 0;
+#pragma unroll
+        for (int m = 4; m < 36; m++) diff |= E[m] ^ xx;
+        return diff;
+    }
+    __device__ static inline Coefs coefs(const int32_t *q) {
+        Coefs c;
+#pragma unroll
+        for (int k = 0; k < 4; k++) c.C[k] = pack2(q[2 * k + 1], q[2 * k]);
+        return c;
+    }
+    __device__ inline void residuals(const Coefs &c, int shift, int m, int32_t &re, int32_t &ro) const {
+        residual_pair(E, c.C, shift, m, re, ro);
+    }
+    __device__ inline uint32_t warm(int lane) const {  // lane i (< 8): lane 0's sample i (as unsigned bits)
+        const int i = lane & 7;
+        uint32_t w01 = (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 0], 0);
+        w01 = (i >> 1) == 1 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 1], 0) : w01;
+        w01 = (i >> 1) == 2 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 2], 0) : w01;
+        w01 = (i >> 1) == 3 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 3], 0) : w01;
+        return (i & 1) ? (w01 >> 16) : (w01 & 0xFFFFu);
+    }
+};
+struct LaneWide {
+    int32_t X[72];
+    struct Coefs {
+        int32_t q[8];
+    };
+    __device__ inline int32_t x(int j) const { return X[8 + j]; }
+    __device__ inline void history() {
+#pragma unroll
+        for (int m = 0; m < 8; m++) X[m] = (int32_t)dpp_wave_shr1((uint32_t)X[64 + m]);
+        fence();
+    }
+    __device__ inline void fence() {
+#pragma unroll
+        for (int m = 0; m < 72; m++) asm volatile("" : "+v"(X[m]));
+    }
+    __device__ inline void totals(bool l0, uint32_t *tk, uint32_t *hk) const {
+        constexpr uint32_t M = 0x80000000u;
+        const int32_t h1 = X[7], h2 = X[6], h3 = X[5], h4 = X[4];
+        uint32_t p0 = (uint32_t)h1 ^ M, p1 = (uint32_t)(h1 - h2) ^ M, p2 = (uint32_t)((h1 - h2) - (h2 - h3)) ^ M;
+        uint32_t p3 = (uint32_t)(((h1 - h2) - (h2 - h3)) - ((h2 - h3) - (h3 - h4))) ^ M;
+        uint32_t t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+#pragma unroll
+        for (int k = 0; k < 5; k++) hk[k] = 0;
+#pragma unroll
+        for (int j = 0; j < 64; j++) {
+            const uint32_t y0 = (uint32_t)X[8 + j] ^ M;
+            const uint32_t y1 = (y0 - p0) ^ M, y2 = (y1 - p1) ^ M, y3 = (y2 - p2) ^ M;
+            if (j < 4) {
+                hk[0] = sad_u32(y0, M, hk[0]);
+                if (j >= 1) hk[1] = sad_u32(y0, p0, hk[1]);
+                if (j >= 2) hk[2] = sad_u32(y1, p1, hk[2]);
+                if (j >= 3) hk[3] = sad_u32(y2, p2, hk[3]);
+            }
+            if (j >= 4 || !l0) {
+                t0 = sad_u32(y0, M, t0);
+                t1 = sad_u32(y0, p0, t1);
+                t2 = sad_u32(y1, p1, t2);
+                t3 = sad_u32(y2, p2, t3);
+                t4 = sad_u32(y3, p3, t4);
+            }
+            p0 = y0, p1 = y1, p2 = y2, p3 = y3;
+        }
+        tk[0] = t0, tk[1] = t1, tk[2] = t2, tk[3] = t3, tk[4] = t4;
+    }
+    __device__ inline uint32_t diff_from_first() const {
+        const uint32_t x0 = uni((uint32_t)X[8]);
+        uint32_t diff = 0;
+#pragma unroll
+        for (int j = 0; j < 64; j++) diff |= (uint32_t)X[8 + j] ^ x0;
+        return diff;
+    }
+    __device__ static inline Coefs coefs(const int32_t *q) {
+        Coefs c;
+#pragma unroll
+        for (int k = 0; k < 8; k++) c.q[k] = q[k];
+        return c;
+    }
+    __device__ inline void residuals(const Coefs &c, int shift, int m, int32_t &re, int32_t &ro) const {
+        const int j = 8 + 2 * m;
+        int32_t se = 0, so = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            se = __mul24(c.q[i], X[j - 1 - i]) + se;
+            so = __mul24(c.q[i], X[j - i]) + so;
+        }
+        re = X[j] - (se >> shift);
+        ro = X[j + 1] - (so >> shift);
+    }
+    __device__ inline uint32_t warm(int lane) const {
+        const int i = lane & 7;
+        uint32_t v = (uint32_t)__builtin_amdgcn_readlane(X[8], 0);
+#pragma unroll
+        for (int k = 1; k < 8; k++) v = i == k ? (uint32_t)__builtin_amdgcn_readlane(X[8 + k], 0) : v;
+        return v;
+    }
+};
+
 // libFLAC's set_partitioned_rice_ (stream_encoder.c) for the fixed and LPC candidates of a 4096-sample frame: orders
 // 5..0, group sums merged by lane shuffles (the 32-bit form when every lane sum is below 2^24)
 __device__ __forceinline__ void rice_candidates(uint32_t sf, uint32_t sl, int of, int ol, bool cand_fixed,
@@ -3043,7 +3187,8 @@ __device__ __forceinline__ uint32_t crc16_cols(const uint32_t *fbuf, const FbMap
     return dpp_wave_xor_u32(gf_mulmod(gf_mulmod(c, S.xlo[m & 63]), S.xhi[m >> 6]));
 }
 
-template <int DT, bool SUB = false>
+// ST: units of a two-channel stream's mid/side pass (chn 0..3 = left, right, mid, side; WIDE for the side signal).
+template <int DT, bool SUB = false, bool ST = false, bool WIDE = false>
 __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *raster, const EncodeParams &P,
                                                 const TileGeom *tiles, const TileNorm *norms,
                                                 const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap,
@@ -3051,8 +3196,10 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
                                                 int want, int64_t f, int lane, const int32_t *ftile,
                                                 PendingFrame &prev, const uint4 *hdr_tab, int hdr_n,
                                                 const uint32_t *pslots, const int64_t *pbytes, int chn = 0,
-                                                uint32_t *sub_slots = nullptr, int32_t *sub_bits = nullptr) {
+                                                uint32_t *sub_slots = nullptr, int32_t *sub_bits = nullptr,
+                                                int32_t *sub_est = nullptr) {
     using T = typename Elem<DT>::T;
+    using Lane = std::conditional_t<WIDE, LaneWide, LanePairs>;
     uint32_t *fbuf = S.bits[threadIdx.x >> 6];  // holds the pending frame `prev` (or zero) on entry
     const int t = ftile[f];
     const TileGeom g = tiles[t];
@@ -3091,43 +3238,75 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
     const int64_t fk = f - g.frame_base;
     const int64_t s0 = fk * kMaxBlock;
     constexpr int n = kMaxBlock;
-    const int64_t sub = SUB ? f * P.nch + chn : f;
+    const int64_t sub = SUB ? f * P.nvch + chn : f;
     const SubAnalysis A = ana[sub];
     const int w = A.wasted;
-    const int sbps = 16 - w;
-    const T *base = raster + (int64_t)(P.band0 + chn) * P.band_stride + g.r0 * P.row_stride + g.c0;
+    const int sbps = 16 - w + ((ST && chn == 3) ? 1 : 0);
+    // (ST mid / side: the left band; the right one at + band_stride)
+    const T *base = raster + (int64_t)(P.band0 + ((ST && chn >= 2) ? 0 : chn)) * P.band_stride + g.r0 * P.row_stride +
+                    g.c0;
 
-    // ---- this lane's 64 samples, normalised and shifted, packed as int16 pairs E[4 + m] = (x[2m], x[2m+1]);
-    //      E[0..3] = the previous lane's last 8 samples (zeros on lane 0)
-    auto load_E = [&](uint32_t *E) {
+    // ---- this lane's 64 samples of the coded signal, normalised and shifted (Lane: packed pairs, or int32 for the
+    //      side signal), with the previous lane's last 8 samples
+    auto load_lane = [&](Lane &Ls) __attribute__((always_inline)) {
         Chunk64<DT> ch;
         const uint32_t sl0 = (uint32_t)s0 + 64u * (uint32_t)lane;  // tile pixels < 2^31
         const uint32_t row = udiv_inv(sl0, (uint32_t)g.w, 1.0 / (double)g.w);
-        ch.load(base, P.row_stride, g.w, row, (int)(sl0 - row * (uint32_t)g.w), (g.w % 64) == 0 ? P.vec_ok : 0, 64);
-        if (sizeof(T) == 2 && tn.mode == kNormLut && w == 0) {  // (wave-uniform) the common case
-            lut_gather_pairs(ch.w, lut, (int32_t)tn.imin, E + 4);
-        } else {
-            int32_t lo = 0;
-            norm_chunk<DT>(ch, tn, lut, [&](int j, int32_t x) {
-                if (j & 1) E[4 + (j >> 1)] = pack2(lo, x >> w);
-                else lo = x >> w;
-            });
-        }
+        const int col = (int)(sl0 - row * (uint32_t)g.w), vec = (g.w % 64) == 0 ? P.vec_ok : 0;
+        ch.load(base, P.row_stride, g.w, row, col, vec, 64);
+        const bool lutp = sizeof(T) == 2 && tn.mode == kNormLut && w == 0;  // (wave-uniform) the common case
+        auto sx = [](uint32_t v, int h) -> int32_t { return h ? ((int32_t)v >> 16) : (int32_t)(int16_t)(v & 0xFFFFu); };
+        if constexpr (WIDE) {  // side = L - R (17 bits)
+            if (lutp) {
+                uint32_t Lp[32], Rp[32];
+                lut_gather_pairs(ch.w, lut, (int32_t)tn.imin, Lp);
+                ch.load(base + P.band_stride, P.row_stride, g.w, row, col, vec, 64);
+                lut_gather_pairs(ch.w, lut, (int32_t)tn.imin, Rp);
 #pragma unroll
-        for (int m = 0; m < 4; m++) E[m] = dpp_wave_shr1(E[32 + m]);
-        reg_fence(E);
+                for (int m = 0; m < 32; m++) {
+                    Ls.X[8 + 2 * m] = sx(Lp[m], 0) - sx(Rp[m], 0);
+                    Ls.X[9 + 2 * m] = sx(Lp[m], 1) - sx(Rp[m], 1);
+                }
+            } else {
+                norm_chunk<DT>(ch, tn, lut, [&](int j, int32_t x) { Ls.X[8 + j] = x; });
+                ch.load(base + P.band_stride, P.row_stride, g.w, row, col, vec, 64);
+                norm_chunk<DT>(ch, tn, lut, [&](int j, int32_t x) { Ls.X[8 + j] = (Ls.X[8 + j] - x) >> w; });
+            }
+        } else {
+            // packed pairs of the normalised samples (shifted right by sh)
+            auto pairs = [&](uint32_t *dst, int sh) __attribute__((always_inline)) {
+                if (lutp) {  // (w == 0)
+                    lut_gather_pairs(ch.w, lut, (int32_t)tn.imin, dst);
+                } else {
+                    int32_t lo = 0;
+                    norm_chunk<DT>(ch, tn, lut, [&](int j, int32_t x) {
+                        if (j & 1) dst[j >> 1] = pack2(lo, x >> sh);
+                        else lo = x >> sh;
+                    });
+                }
+            };
+            if (ST && chn == 2) {  // mid = (L + R) >> 1, then the wasted bits
+                uint32_t Lp[32], Rp[32];
+                pairs(Lp, 0);
+                ch.load(base + P.band_stride, P.row_stride, g.w, row, col, vec, 64);
+                pairs(Rp, 0);
+#pragma unroll
+                for (int m = 0; m < 32; m++)
+                    Ls.E[4 + m] = pack2(((sx(Lp[m], 0) + sx(Rp[m], 0)) >> 1) >> w,
+                                        ((sx(Lp[m], 1) + sx(Rp[m], 1)) >> 1) >> w);
+            } else {
+                pairs(Ls.E + 4, w);
+            }
+        }
+        Ls.history();
     };
-    uint32_t E[36];
-    load_E(E);
-    auto X = [&](int j) -> int32_t {
-        const uint32_t v = E[4 + (j >> 1)];
-        return (j & 1) ? ((int32_t)v >> 16) : (int32_t)(int16_t)(v & 0xFFFFu);
-    };
+    Lane Ls;
+    load_lane(Ls);
 
     // ---- candidates: the fixed order guess from the totals (fixed.c: first minimum under <=), its lane sum; the LPC
     //      lane |r| sum
     uint32_t tk[5], hk[5], Tt[5];
-    fixed_lane_totals(E, l0, tk, hk);
+    Ls.totals(l0, tk, hk);
     dpp_wave_sum_multi<5>(tk, Tt);
     int guess;
     if (Tt[0] <= min(min(Tt[1], Tt[2]), min(Tt[3], Tt[4]))) guess = 0;
@@ -3141,13 +3320,8 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
     const float fbg = (float)(tg > 0 ? log(M_LN2 * (double)tg / dn) / M_LN2 : 0.0);
     bool constant = false;
     if (fb1 == 0.0f) {
-        reg_fence(E);
-        const uint32_t x0 = uni(E[4] & 0xFFFFu);
-        const uint32_t xx = x0 | (x0 << 16);
-        uint32_t diff = 0;
-#pragma unroll
-        for (int m = 4; m < 36; m++) diff |= E[m] ^ xx;
-        constant = dpp_wave_or_u32(diff) == 0;
+        Ls.fence();
+        constant = dpp_wave_or_u32(Ls.diff_from_first()) == 0;
     }
     const bool cand_fixed = !constant && !(fbg >= (float)sbps);
     const bool cand_lpc = !constant && (A.flags & kFlagLpcOk);
@@ -3155,16 +3329,14 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
     // the fixed candidate's lane sum of |e_of(i)|, lane 0 from i = of (the totals start at 4: lane 0 adds its i < 4)
     uint32_t sf = of == 0 ? tk[0] + (l0 ? hk[0] : 0u) : of == 1 ? tk[1] + (l0 ? hk[1] : 0u)
                 : of == 2 ? tk[2] + (l0 ? hk[2] : 0u) : of == 3 ? tk[3] + (l0 ? hk[3] : 0u) : tk[4];
-    uint32_t CL[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) CL[k] = pack2(A.q[2 * k + 1], A.q[2 * k]);
+    const typename Lane::Coefs CL = Lane::coefs(A.q);
     uint32_t sl = 0;
     if (cand_lpc) {
 #pragma unroll
         for (int m = 0; m < 32; m++) {
             if (m % 4 == 0 && m) asm volatile("" : "+v"(sl));
             int32_t re, ro;
-            residual_pair(E, CL, lshift, m, re, ro);
+            Ls.residuals(CL, lshift, m, re, ro);
             // |r| + sl in one v_sad_u32 on the sign-flipped residual
             const uint32_t se = sad_u32((uint32_t)re ^ 0x80000000u, 0x80000000u, sl);
             sl = (2 * m < kMaxLpc && l0 && 2 * m < ol) ? sl : se;
@@ -3172,7 +3344,7 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
             sl = (2 * m + 1 < kMaxLpc && l0 && 2 * m + 1 < ol) ? sl : so;
         }
     }
-    reg_fence(E);
+    Ls.fence();
     uint32_t rb_f = 0, rb_l = 0;
     int po_f = 0, po_l = 0, k_f = 0, k_l = 0;
     rice_candidates(sf, sl, of, ol, cand_fixed, cand_lpc, lane, rb_f, po_f, k_f, rb_l, po_l, k_l);
@@ -3194,15 +3366,7 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
         }
     }
     // lane i (< 8) of lane 0's warm-up sample i, lane 0's sample 0 (CONSTANT): taken now, the registers die below
-    uint32_t xi;
-    {
-        const int i = lane & 7;
-        uint32_t w01 = (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 0], 0);
-        w01 = (i >> 1) == 1 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 1], 0) : w01;
-        w01 = (i >> 1) == 2 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 2], 0) : w01;
-        w01 = (i >> 1) == 3 ? (uint32_t)__builtin_amdgcn_readlane((int)E[4 + 3], 0) : w01;
-        xi = (i & 1) ? (w01 >> 16) : (w01 & 0xFFFFu);
-    }
+    const uint32_t xi = Ls.warm(lane);
     // ---- field positions
     int src, srx;
     sample_rate_code(P.sample_rate, src, srx);
@@ -3215,7 +3379,7 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
     uint32_t pos = pos0;
     uint32_t end_bits;
     bool ok = true;
-    uint32_t C[4];
+    typename Lane::Coefs C;
     int shift = lshift, k = 0, lanes_per = 64, o = 0, po = 0;
     uint32_t run = 0;      // lane-private write position (bits)
     uint32_t seglen = 0;   // the lane's segment length (bits)
@@ -3235,12 +3399,10 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
             else if (of == 2) { qf[0] = 2; qf[1] = -1; }
             else if (of == 3) { qf[0] = 3; qf[1] = -3; qf[2] = 1; }
             else if (of == 4) { qf[0] = 4; qf[1] = -6; qf[2] = 4; qf[3] = -1; }
-#pragma unroll
-            for (int m = 0; m < 4; m++) C[m] = pack2(qf[2 * m + 1], qf[2 * m]);
+            C = Lane::coefs(qf);
             shift = 0;
         } else {
-#pragma unroll
-            for (int m = 0; m < 4; m++) C[m] = CL[m];
+            C = CL;
         }
         pos += (uint32_t)o * sbps;
         if (type == 3) pos += 9 + (uint32_t)o * A.lpc_prec;
@@ -3263,7 +3425,7 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
         for (int m = 0; m < 32; m++) {
             if (m % 4 == 0 && m) asm volatile("" : "+v"(run));
             int32_t re, ro;
-            residual_pair(E, C, shift, m, re, ro);
+            Ls.residuals(C, shift, m, re, ro);
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const int j = 2 * m + h;
@@ -3301,6 +3463,36 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
         __hip_atomic_store(&status[f], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __builtin_amdgcn_s_setprio(0);
+    if constexpr (SUB && WIDE) {
+        if (type == 1 && sbps == 17) {
+            // 17-bit VERBATIM side subframe: 69640 bits, one word past the LDS frame buffer.  A lane's 64 samples are
+            // 1088 bits = 34 words starting at subframe bit 8 + 1088 lane: packed in registers, stored to the slot
+            uint32_t X[34];
+#pragma unroll
+            for (int i = 0; i < 34; i++) X[i] = 0;
+#pragma unroll
+            for (int j = 0; j < 64; j++) {
+                const int b = 17 * j, wi = b >> 5, r = b & 31;
+                const uint32_t v = (uint32_t)Ls.x(j) & 0x1FFFFu;
+                if (r <= 15) X[wi] |= v << (15 - r);
+                else {
+                    X[wi] |= v >> (r - 15);
+                    X[wi + 1] |= v << (47 - r);
+                }
+            }
+            const uint32_t before = (uint32_t)__shfl_up((int)X[33], 1);  // the previous lane's last word
+            uint32_t *dst = sub_slots + (size_t)sub * kSubWords + 34 * lane;
+            dst[0] = ((l0 ? 0x02u : before) << 24) | (X[0] >> 8);  // (lane 0: the subframe header, VERBATIM)
+#pragma unroll
+            for (int i = 1; i < 34; i++) dst[i] = (X[i - 1] << 24) | (X[i] >> 8);
+            if (lane == 63) dst[34] = X[33] << 24;
+            if (l0) {
+                sub_bits[sub] = (int32_t)end_bits;
+                if (sub_est) sub_est[sub] = (int32_t)best;
+            }
+            return;  // (the LDS buffer was not touched: still zero)
+        }
+    }
     // ---- assembly into the v3 frame layout (word w at row w mod C, column w / C: the store and CRC read rows, the
     //      lanes' columns fall in distinct banks)
     const FbMap M = fb_map(((end_bits + 23) >> 5) + 2);  // words written: body, CRC-16 (byte aligned), one spare
@@ -3345,7 +3537,7 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
         } else if (ok) {
             // a lane outgrew its column: the v3 writer at the known offsets, from the samples loaded again (rare: the
             // registers of the first load are free for the assembly)
-            load_E(E);
+            load_lane(Ls);
             uint32_t rp = pos + run;
             if ((lane & (lanes_per - 1)) == 0) {
                 lds_put_bits2(fbuf, M, rp, (uint32_t)k, 4);
@@ -3355,7 +3547,7 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
 #pragma unroll
             for (int m = 0; m < 32; m++) {
                 int32_t re, ro;
-                residual_pair(E, C, shift, m, re, ro);
+                Ls.residuals(C, shift, m, re, ro);
 #pragma unroll
                 for (int h = 0; h < 2; h++) {
                     const int j = 2 * m + h;
@@ -3373,11 +3565,13 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
             fold = true;
         }
     } else if (type == 1) {
-        if (w == 0) {
+        if (!WIDE && w == 0) {
             // 16-bit VERBATIM: the lane's 64 samples are its 32 packed pairs (halves swapped to MSB-first order)
             uint32_t Pv[kPrivRows + 1];
 #pragma unroll
-            for (int m = 0; m < 32; m++) Pv[m] = __builtin_amdgcn_alignbit(E[4 + m], E[4 + m], 16);
+            for (int m = 0; m < 32; m++) {
+                if constexpr (!WIDE) Pv[m] = __builtin_amdgcn_alignbit(Ls.E[4 + m], Ls.E[4 + m], 16);
+            }
 #pragma unroll
             for (int m = 32; m <= kPrivRows; m++) Pv[m] = 0;
             const uint32_t off = pos + 1024u * (uint32_t)lane;
@@ -3386,7 +3580,7 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
             const uint32_t p0 = pos + (uint32_t)(64 * lane) * (uint32_t)sbps;
             const uint32_t shl = 32u - (uint32_t)sbps;
 #pragma unroll
-            for (int j = 0; j < 64; j++) lds_put_left(fbuf, M, nk4, p0 + (uint32_t)j * sbps, (uint32_t)X(j) << shl);
+            for (int j = 0; j < 64; j++) lds_put_left(fbuf, M, nk4, p0 + (uint32_t)j * sbps, (uint32_t)Ls.x(j) << shl);
             fold = true;
         }
     }
@@ -3457,7 +3651,7 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
     if constexpr (SUB) {
         // the subframe's words (bits past end_bits are zeros) to its slot, then re-zero the buffer
         if (ok) {
-            uint32_t *dst = sub_slots + (size_t)sub * kFrameWordsV3;
+            uint32_t *dst = sub_slots + (size_t)sub * kSubWords;
             const uint32_t nw = (end_bits + 31) >> 5;
             for (uint32_t wi = (uint32_t)lane; wi < nw; wi += 64) dst[wi] = fbuf[M(wi)];
             for (uint32_t i = 0; i < M.c; i++) fbuf[(i << 6) | (uint32_t)lane] = 0;
@@ -3465,6 +3659,7 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
             zero_wave_buf(fbuf, lane);
         }
         if (l0) sub_bits[sub] = ok ? (int32_t)end_bits : -1;
+        if (l0 && sub_est) sub_est[sub] = (int32_t)best;  // (a two-channel stream picks its assignment by these)
         (void)fbytes;
         return;
     }
@@ -3477,15 +3672,17 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
     prev.f = f, prev.fbytes = fbytes, prev.ok = ok, prev.map = M;
 }
 
-template <int DT, bool SUB = false>
-__global__ void __launch_bounds__(256, sizeof(typename Elem<DT>::T) <= 2 ? 3 : 1) k_encode_v4(const typename Elem<DT>::T *raster, EncodeParams P,
+// SUB: the units are subframes -- (frame, channel) of a >= 3-channel stream, or of a two-channel stream's mid/side
+// pass (ST): left, right, mid in one launch, the 17-bit side signals (WIDE) in another.
+template <int DT, bool SUB = false, bool ST = false, bool WIDE = false>
+__global__ void __launch_bounds__(256, (sizeof(typename Elem<DT>::T) <= 2 && !WIDE) ? (ST ? 2 : 3) : 1) k_encode_v4(const typename Elem<DT>::T *raster, EncodeParams P,
                                                   const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
                                                   const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap,
                                                   int64_t *frame_off, uint64_t *status, int *ticket_ctr, int *err,
                                                   const int32_t *__restrict__ ftile, const uint4 *__restrict__ hdr_tab,
                                                   int hdr_n, const uint32_t *__restrict__ pslots,
                                                   const int64_t *__restrict__ pbytes, uint32_t *sub_slots = nullptr,
-                                                  int32_t *sub_bits = nullptr) {
+                                                  int32_t *sub_bits = nullptr, int32_t *sub_est = nullptr) {
     __shared__ __attribute__((aligned(16))) EncV3Shared S;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int i = threadIdx.x; i < 4096; i += blockDim.x) (&S.crc8x[0][0])[i] = (&c_crc16x8[0][0])[i];
@@ -3498,12 +3695,14 @@ __global__ void __launch_bounds__(256, sizeof(typename Elem<DT>::T) <= 2 ? 3 : 1
     uint32_t *fbuf = S.bits[wave];
     while (true) {
         __syncthreads();  // previous ticket's readers of S.ticket / S.lut are done
-        const int64_t nunits = SUB ? P.nframes * P.nch : P.nframes;
+        constexpr int kUpfSt = WIDE ? 1 : 3;  // units per frame of a two-channel launch
+        const int upf = ST ? kUpfSt : P.nch;
+        const int64_t nunits = SUB ? P.nframes * upf : P.nframes;
         if (threadIdx.x == 0) {
             const int tk = atomicAdd(ticket_ctr, 1);
             S.ticket = tk;
             const int64_t u0 = (int64_t)tk * 4;
-            S.want = (u0 < nunits) ? ftile[SUB ? u0 / P.nch : u0] : -1;
+            S.want = (u0 < nunits) ? ftile[SUB ? u0 / upf : u0] : -1;
         }
         __syncthreads();
         const int64_t fbase = (int64_t)S.ticket * 4;
@@ -3522,13 +3721,13 @@ __global__ void __launch_bounds__(256, sizeof(typename Elem<DT>::T) <= 2 ? 3 : 1
         if constexpr (SUB) {
             const int64_t v = fbase + wave;
             if (v < nunits) {
-                const int64_t f = v / P.nch;
-                const int chn = (int)(v - f * P.nch);
+                const int64_t f = v / upf;
+                const int chn = WIDE ? 3 : (int)(v - f * upf);
                 const TileGeom g = tiles[ftile[f]];
                 if (!(g.partial && f - g.frame_base == g.nframes - 1))
-                    encode_frame_v4<DT, true>(raster, P, tiles, norms, ana, arena, arena_cap, frame_off, status, err, S,
-                                              want, f, lane, ftile, prev, hdr_tab, hdr_n, pslots, pbytes, chn,
-                                              sub_slots, sub_bits);
+                    encode_frame_v4<DT, true, ST, WIDE>(raster, P, tiles, norms, ana, arena, arena_cap, frame_off,
+                                                        status, err, S, want, f, lane, ftile, prev, hdr_tab, hdr_n,
+                                                        pslots, pbytes, chn, sub_slots, sub_bits, sub_est);
             }
         } else {
             const int64_t f = fbase + wave;
@@ -3548,14 +3747,15 @@ __global__ void __launch_bounds__(256, sizeof(typename Elem<DT>::T) <= 2 ? 3 : 1
 // k_mc_assemble writes them (the tile's partial last frame comes sealed from the generic kernels).
 
 // frame header of a full 4096-sample frame (RFC 9639 9.1, as k_encode_frames writes it); returns its bytes
-__device__ inline int mc_frame_header(uint8_t *h, uint32_t v, int nch, int sr) {
+// chcode: the channel assignment nibble (nch - 1 for independent channels; 8 / 9 / 10 left-side / right-side / mid-side)
+__device__ inline int mc_frame_header(uint8_t *h, uint32_t v, int chcode, int sr) {
     int src, srx;
     sample_rate_code(sr, src, srx);
     int hb = 0;
     h[hb++] = 0xFF;
     h[hb++] = 0xF8;
     h[hb++] = (uint8_t)((12 << 4) | src);
-    h[hb++] = (uint8_t)(((nch - 1) << 4) | (4 << 1));
+    h[hb++] = (uint8_t)((chcode << 4) | (4 << 1));
     if (v < 0x80) h[hb++] = (uint8_t)v;
     else if (v < 0x800) { h[hb++] = (uint8_t)(0xC0 | (v >> 6)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
     else if (v < 0x10000) { h[hb++] = (uint8_t)(0xE0 | (v >> 12)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
@@ -3571,8 +3771,25 @@ __device__ inline int mc_frame_header(uint8_t *h, uint32_t v, int nch, int sr) {
     return hb;
 }
 
+// A two-channel stream's frame (P.nvch == 4: L, R, M, S coded): libFLAC process_subframes_ keeps the assignment with
+// the fewest estimated bits among independent (L, R), left-side (L, S), right-side (S, R), mid-side (M, S) -- in that
+// order, a later one only when strictly smaller (stream_encoder.c; oracle orc_encode_frames_level).
+__device__ inline int st_pick(const int32_t *est4) {
+    const uint32_t e0 = (uint32_t)est4[0], e1 = (uint32_t)est4[1], e2 = (uint32_t)est4[2], e3 = (uint32_t)est4[3];
+    const uint32_t bits[4] = {e0 + e1, e0 + e3, e1 + e3, e2 + e3};
+    int ca = 0;
+    for (int k = 1; k < 4; k++)
+        if (bits[k] < bits[ca]) ca = k;
+    return ca;
+}
+__device__ inline void st_subs(int ca, int &a, int &b) {  // coded signals of an assignment (left/right order)
+    a = ca == 2 ? 3 : ca == 3 ? 2 : 0;
+    b = ca == 0 ? 1 : ca == 2 ? 1 : 3;
+}
+
 __global__ void k_mc_frame_bytes(const EncodeParams P, const TileGeom *tiles, const int32_t *ftile,
-                                 const int32_t *sub_bits, const int64_t *pbytes, int64_t *frame_bytes, int *err) {
+                                 const int32_t *sub_bits, const int64_t *pbytes, int64_t *frame_bytes, int *err,
+                                 const int32_t *sub_est = nullptr, int8_t *pick = nullptr) {
     const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= P.nframes) return;
     const TileGeom g = tiles[ftile[f]];
@@ -3582,9 +3799,17 @@ __global__ void k_mc_frame_bytes(const EncodeParams P, const TileGeom *tiles, co
         return;
     }
     uint8_t h[16];
-    int64_t bits = 8 * mc_frame_header(h, (uint32_t)fk, P.nch, P.sample_rate);
+    const bool st = P.nvch == 4 && P.nch == 2;
+    int chcode = P.nch - 1, sa = 0, sb = 1;
+    if (st) {
+        const int ca = st_pick(sub_est + f * 4);
+        pick[f] = (int8_t)ca;
+        chcode = ca == 0 ? 1 : 7 + ca;
+        st_subs(ca, sa, sb);
+    }
+    int64_t bits = 8 * mc_frame_header(h, (uint32_t)fk, chcode, P.sample_rate);
     for (int c = 0; c < P.nch; c++) {
-        const int32_t b = sub_bits[f * P.nch + c];
+        const int32_t b = sub_bits[f * P.nvch + (st ? (c ? sb : sa) : c)];
         if (b < 0) atomicOr(err, 2);
         bits += b < 0 ? 0 : b;
     }
@@ -3598,7 +3823,8 @@ __global__ void k_mc_frame_bytes(const EncodeParams P, const TileGeom *tiles, co
 __global__ void __launch_bounds__(256) k_mc_assemble(const EncodeParams P, const TileGeom *tiles, const int32_t *ftile,
                                                     const uint32_t *sub_slots, const int32_t *sub_bits,
                                                     const uint32_t *pslots, const int64_t *pbytes,
-                                                    const int64_t *frame_off, uint8_t *arena) {
+                                                    const int64_t *frame_off, uint8_t *arena,
+                                                    const int8_t *pick = nullptr) {
     extern __shared__ uint32_t W[];  // nch * kFrameWordsV3 + 16 words
     __shared__ uint16_t T[4][256];
     __shared__ uint32_t wc[4];
@@ -3615,9 +3841,17 @@ __global__ void __launch_bounds__(256) k_mc_assemble(const EncodeParams P, const
     }
     wg_load_crc_tables(T);
     uint8_t h[16];
-    const int hb = mc_frame_header(h, (uint32_t)fk, P.nch, P.sample_rate);
+    const bool st = P.nvch == 4 && P.nch == 2;  // two channels: the picked pair of L, R, M, S
+    int chcode = P.nch - 1, sa = 0, sb = 1;
+    if (st) {
+        const int ca = pick[f];
+        chcode = ca == 0 ? 1 : 7 + ca;
+        st_subs(ca, sa, sb);
+    }
+    auto unit = [&](int c) -> int64_t { return f * P.nvch + (st ? (c ? sb : sa) : c); };
+    const int hb = mc_frame_header(h, (uint32_t)fk, chcode, P.sample_rate);
     int64_t total = 8 * hb;
-    for (int c = 0; c < P.nch; c++) total += max(0, sub_bits[f * P.nch + c]);
+    for (int c = 0; c < P.nch; c++) total += max(0, sub_bits[unit(c)]);
     const int nwz = (int)(((total + 7) >> 3) + 2 + 3) / 4 + 1;  // words of body + CRC-16, one spare
     for (int i = tid; i < nwz; i += 256) W[i] = 0;
     __syncthreads();
@@ -3625,8 +3859,8 @@ __global__ void __launch_bounds__(256) k_mc_assemble(const EncodeParams P, const
         for (int i = 0; i < hb; i++) W[i >> 2] |= (uint32_t)h[i] << (24 - 8 * (i & 3));
     int64_t o = 8 * hb;
     for (int c = 0; c < P.nch; c++) {
-        const int32_t nbits = sub_bits[f * P.nch + c];
-        const uint32_t *sw = sub_slots + (size_t)(f * P.nch + c) * kFrameWordsV3;
+        const int32_t nbits = sub_bits[unit(c)];
+        const uint32_t *sw = sub_slots + (size_t)unit(c) * kSubWords;
         const int nw = (nbits + 31) >> 5, sh = (int)(o & 31);
         const int64_t w0 = o >> 5;
         const int64_t wl = (o + nbits - 1) >> 5;  // last destination word holding a bit of this subframe
@@ -3918,7 +4152,7 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     FRS_HIP(ctx->tile_sizes.ensure(sizeof(int64_t) * (ntiles + 1) + 64));
     // pinned staging: tiles | wave table | packed results (the previous call has synchronised, so it is free)
     const size_t pin_tiles = 0, pin_wt = (sizeof(TileGeom) * ntiles + 255) & ~(size_t)255;
-    const size_t wt_cap = (size_t)(nframes / 64 + ntiles + 1) * (size_t)std::max(1, d->nbands);
+    const size_t wt_cap = (size_t)(nframes / 64 + ntiles + 1) * (size_t)std::max(1, (int)P.nvch);
     const size_t pin_res = (pin_wt + sizeof(int2) * wt_cap + 255) & ~(size_t)255;
     const size_t res_bytes = sizeof(int64_t) * (3 * (size_t)ntiles + 2);
     const size_t pin_pl = (pin_res + res_bytes + 255) & ~(size_t)255;  // partial-frame list of the fast path
@@ -3929,10 +4163,13 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     const bool fast = allow_fast && !ctx->force_generic && level5 && P.bps == 16 && P.nch == 1 && P.norm_mode == 0 &&
                       d->blocksize == 4096 && !Elem<DT>::is_float;
     // multi-channel streams of >= 3 channels (plain convert of a multi-band raster): libFLAC codes their channels
-    // independently, so the fast kernels code the subframes and k_mc_assemble joins them (2 channels: libFLAC's
-    // stereo decorrelation, generic kernels)
-    const bool mc = allow_fast && !ctx->force_generic && level5 && P.bps == 16 && P.nch >= 3 && P.nch <= 8 &&
-                    P.norm_mode == 0 && d->blocksize == 4096 && !Elem<DT>::is_float;
+    // independently, so the fast kernels code the subframes and k_mc_assemble joins them.  Two channels (st2):
+    // libFLAC's mid/side pass codes L, R, M and S (17 bits) as subframes and keeps the cheapest pair by their
+    // estimates (k_mc_frame_bytes picks, k_mc_assemble joins)
+    const bool st2 = allow_fast && !ctx->force_generic && level5 && P.bps == 16 && P.nch == 2 && P.nvch == 4 &&
+                     P.norm_mode == 0 && d->blocksize == 4096 && !Elem<DT>::is_float;
+    const bool mc = st2 || (allow_fast && !ctx->force_generic && level5 && P.bps == 16 && P.nch >= 3 && P.nch <= 8 &&
+                            P.norm_mode == 0 && d->blocksize == 4096 && !Elem<DT>::is_float);
     int64_t npartial = 0;
     int64_t *hplist = ctx->pin.at<int64_t>(pin_pl);
     if (geo_hit) {
@@ -4035,7 +4272,7 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                 int2 *wt = ctx->pin.at<int2>(pin_wt);
                 nwaves = 0;
                 for (int ti = 0; ti < ntiles; ti++)
-                    for (int c = 0; c < P.nch; c++)  // (tile, first frame | channel << 24)
+                    for (int c = 0; c < P.nvch; c++)  // (tile, first frame | coded signal << 24)
                         for (int k0 = 0; k0 < tiles[ti].nframes; k0 += 64) wt[nwaves++] = make_int2(ti, k0 | (c << 24));
                 FRS_HIP(ctx->wave_tab.ensure(sizeof(int2) * nwaves));
                 FRS_HIP(hipMemcpyAsync(ctx->wave_tab.ptr, wt, sizeof(int2) * nwaves, hipMemcpyHostToDevice, st));
@@ -4047,12 +4284,21 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                 if constexpr (sizeof(T) == 2)
                     k_analyze_v3<DT, false, true><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
                                                                          ctx->window.as<float>(), dana, wtab, nwaves);
+            } else if (st2) {
+                k_analyze_v3<DT, false, false, true><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms,
+                                                                             ctx->luts.as<int16_t>(),
+                                                                             ctx->window.as<float>(), dana, wtab, nwaves);
             } else {
                 k_analyze_v3<DT, false><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
                                                                 ctx->window.as<float>(), dana, wtab, nwaves);
             }
-            k_analyze_v3<DT, true><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
-                                                           ctx->window.as<float>(), dana, wtab, nwaves);
+            if (st2)
+                k_analyze_v3<DT, true, false, true><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms,
+                                                                            ctx->luts.as<int16_t>(),
+                                                                            ctx->window.as<float>(), dana, wtab, nwaves);
+            else
+                k_analyze_v3<DT, true><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
+                                                               ctx->window.as<float>(), dana, wtab, nwaves);
             prof_end(ctx, "analyze", ev);
             if (!geo_hit) {  // the geometry's device copies are (being) uploaded on this stream: cache them
                 ctx->geo_tiles = tiles;
@@ -4077,11 +4323,19 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
             ctx->geo_ptrs[2] = ctx->plist.ptr;
             FRS_HIP(ctx->slots.ensure((size_t)npartial * P.slot_words * 4));
             const int64_t *dpl = ctx->plist.as<int64_t>();
-            k_analyze_partial<DT><<<dim3((unsigned)npartial, (unsigned)P.nch), kPartThreads, 0, st>>>(
-                raster, P, dtiles, dnorms, ctx->window.as<float>(), dana, dpl);
-            k_encode_frames<DT><<<(unsigned)npartial, kEncThreads, 0, st>>>(raster, P, dtiles, dnorms, dana,
-                                                                           ctx->slots.as<uint32_t>(), dpbytes,
-                                                                           err_flag, dpl);
+            if (st2) {
+                k_analyze_partial<DT, true><<<dim3((unsigned)npartial, 4u), kPartThreads, 0, st>>>(
+                    raster, P, dtiles, dnorms, ctx->window.as<float>(), dana, dpl);
+                k_encode_frames<DT, true><<<(unsigned)npartial, kEncThreads, 0, st>>>(
+                    raster, P, dtiles, dnorms, dana, ctx->slots.as<uint32_t>(), dpbytes, err_flag, dpl, nullptr,
+                    nullptr, 0);
+            } else {
+                k_analyze_partial<DT><<<dim3((unsigned)npartial, (unsigned)P.nch), kPartThreads, 0, st>>>(
+                    raster, P, dtiles, dnorms, ctx->window.as<float>(), dana, dpl);
+                k_encode_frames<DT><<<(unsigned)npartial, kEncThreads, 0, st>>>(raster, P, dtiles, dnorms, dana,
+                                                                               ctx->slots.as<uint32_t>(), dpbytes,
+                                                                               err_flag, dpl);
+            }
             k_seal_partial<<<(unsigned)npartial, 256, 0, st>>>(ctx->slots.as<uint32_t>(), P.slot_words, dpbytes,
                                                                npartial);
             prof_end(ctx, "partial", ev);
@@ -4089,27 +4343,45 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         uint64_t *dstatus = ctx->status.as<uint64_t>();
         int *ticket = reinterpret_cast<int *>(dstatus + nframes);
         if (mc) {
-            const int64_t nsub = nframes * P.nch;
-            FRS_HIP(ctx->sub_slots.ensure(sizeof(uint32_t) * (size_t)nsub * kFrameWordsV3));
+            const int64_t nsub = nframes * P.nvch;
+            FRS_HIP(ctx->sub_slots.ensure(sizeof(uint32_t) * (size_t)nsub * kSubWords));
             FRS_HIP(ctx->sub_bits.ensure(sizeof(int32_t) * (size_t)nsub));
             FRS_HIP(ctx->mc_bytes.ensure(sizeof(int64_t) * (size_t)(nframes + 1)));
-            FRS_HIP(hipMemsetAsync(ticket, 0, sizeof(int), st));
+            FRS_HIP(hipMemsetAsync(ticket, 0, 2 * sizeof(int), st));
             uint32_t *dsub = ctx->sub_slots.as<uint32_t>();
             int32_t *dsbits = ctx->sub_bits.as<int32_t>();
             int64_t *dmcb = ctx->mc_bytes.as<int64_t>();
+            int32_t *dsest = nullptr;
+            int8_t *dpick = nullptr;
+            if (st2) {
+                FRS_HIP(ctx->sub_est.ensure(sizeof(int32_t) * (size_t)nsub));
+                FRS_HIP(ctx->st_pick.ensure((size_t)nframes + 64));
+                dsest = ctx->sub_est.as<int32_t>();
+                dpick = ctx->st_pick.as<int8_t>();
+            }
             prof_begin(ctx, "encode", &ev);
-            {
-                static int nwg_max = 0;  // (per instantiation; the same gfx950 target for every device)
-                if (nwg_max == 0) FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nwg_max, k_encode_v4<DT, true>, 256, 0));
+            // (one occupancy query per kernel instantiation; the same gfx950 target for every device)
+            auto launch = [&](auto kern, int &nwg_max, int64_t units, int *tk) {
+                if (nwg_max == 0) FRS_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nwg_max, kern, 256, 0));
                 int64_t grid = (int64_t)std::max(1, nwg_max) * ctx->num_cus;
-                grid = std::min<int64_t>(grid, (nsub + 3) / 4);
-                k_encode_v4<DT, true><<<(unsigned)grid, 256, 0, st>>>(
+                grid = std::min<int64_t>(grid, (units + 3) / 4);
+                kern<<<(unsigned)grid, 256, 0, st>>>(
                     raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(), dana, reinterpret_cast<uint8_t *>(arena_dev),
-                    arena_cap, ctx->frame_off.as<int64_t>(), dstatus, ticket, err_flag, ctx->frame_tile.as<int32_t>(),
-                    ctx->hdr_tab.as<uint4>(), 0, ctx->slots.as<uint32_t>(), dpbytes, dsub, dsbits);
+                    arena_cap, ctx->frame_off.as<int64_t>(), dstatus, tk, err_flag, ctx->frame_tile.as<int32_t>(),
+                    ctx->hdr_tab.as<uint4>(), 0, ctx->slots.as<uint32_t>(), dpbytes, dsub, dsbits, dsest);
+                return FRS_OK;
+            };
+            if (st2) {  // left, right, mid (16-bit) in one launch; the 17-bit side signals in another
+                static int nwg_lrm = 0, nwg_side = 0;
+                if (int rc2 = launch(k_encode_v4<DT, true, true, false>, nwg_lrm, nframes * 3, ticket)) return rc2;
+                if (int rc2 = launch(k_encode_v4<DT, true, true, true>, nwg_side, nframes, ticket + 1)) return rc2;
+            } else {
+                static int nwg_mc = 0;
+                if (int rc2 = launch(k_encode_v4<DT, true>, nwg_mc, nsub, ticket)) return rc2;
             }
             k_mc_frame_bytes<<<(unsigned)((nframes + 255) / 256), 256, 0, st>>>(P, dtiles, ctx->frame_tile.as<int32_t>(),
-                                                                               dsbits, dpbytes, dmcb, err_flag);
+                                                                               dsbits, dpbytes, dmcb, err_flag, dsest,
+                                                                               dpick);
             prof_end(ctx, "encode", ev);
             k_scan_sizes<<<1, kScanThreads, 0, st>>>(dmcb, ctx->frame_off.as<int64_t>(), nframes);
             int64_t total = 0;
@@ -4133,7 +4405,7 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
             prof_begin(ctx, "assemble", &ev);
             k_mc_assemble<<<(unsigned)nframes, 256, mc_lds, st>>>(
                 P, dtiles, ctx->frame_tile.as<int32_t>(), dsub, dsbits, ctx->slots.as<uint32_t>(), dpbytes,
-                ctx->frame_off.as<int64_t>(), reinterpret_cast<uint8_t *>(arena_dev));
+                ctx->frame_off.as<int64_t>(), reinterpret_cast<uint8_t *>(arena_dev), dpick);
             prof_end(ctx, "assemble", ev);
             k_gather_tile_off<<<(ntiles + 1 + 255) / 256, 256, 0, st>>>(ctx->frame_off.as<int64_t>(), dtiles, ntiles,
                                                                        total, ctx->tile_sizes.as<int64_t>());

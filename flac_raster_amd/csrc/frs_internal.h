@@ -101,6 +101,7 @@ struct frs_ctx {
     // per-frame assignment of the group leaders and the leader frame list
     DevBuf lpc_cand, window_hi, loose_assign, loose_lead;
     int window_hi_bs = 0, window_hi_parts = 0;
+    DevBuf sub_est, st_pick;  // two-channel fast path: subframe estimates (L, R, M, S), the assignment per frame
 };
 
 #define FRS_HIP(call)                                                                  \

@@ -88,10 +88,16 @@ def test_stereo_encode_matches_oracle(gpu_ctx, case):
     name, arr, bits = _cases()[case]
     B, H, W = arr.shape
     d = gpu_ctx.make_desc(H, W, arr.dtype, nbands=2, tile_h=H, tile_w=W, sample_rate=44100, bits_per_sample=bits)
+    gpu_ctx.profile(True)
+    gpu_ctx.profile_reset()
     arena, off, mn, mx, bps = gpu_ctx.encode_tiles_host(arr, d)
+    compact_ms = gpu_ctx.profile_avg_ms("compact")
+    gpu_ctx.profile(False)
     fr, pcm, obps, omn, omx = _oracle_frames(arr, bits)
     assert bps == obps and mn[0] == omn and mx[0] == omx, name
     assert arena.tobytes() == fr, name
+    if bps == 16:  # 16-bit streams take the fast two-channel kernels (L, R, M as packed pairs, S as int32)
+        assert compact_ms < 0, f"{name}: expected the fast stereo path, got the generic kernels"
 
 
 def test_stereo_spatial_encode_matches_oracle(gpu_ctx):
