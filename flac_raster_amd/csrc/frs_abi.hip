@@ -122,7 +122,7 @@ void frs_ctx_destroy(frs_ctx *ctx) {
     frs::prof_collect(ctx);
     DevBuf *bufs[] = {&ctx->tiles, &ctx->norms, &ctx->analysis, &ctx->slots, &ctx->frame_bytes, &ctx->frame_off,
                       &ctx->window, &ctx->tile_sizes, &ctx->luts, &ctx->status, &ctx->frame_tile, &ctx->hdr_tab, &ctx->wave_tab, &ctx->plist, &ctx->lpc_cand, &ctx->sub_est, &ctx->st_pick, &ctx->window_hi, &ctx->loose_assign, &ctx->loose_lead, &ctx->sub_slots, &ctx->sub_bits, &ctx->mc_bytes, &ctx->raster_stage, &ctx->arena_stage, &ctx->host_pack,
-                      &ctx->dec_cand, &ctx->dec_count, &ctx->dec_pcm, &ctx->dec_soff, &ctx->dec_next, &ctx->dec_status, &ctx->dec_fb, &ctx->dec_sel,
+                      &ctx->dec_cand, &ctx->dec_count, &ctx->dec_pcm, &ctx->dec_soff, &ctx->dec_next, &ctx->dec_status, &ctx->dec_fb, &ctx->dec_sel, &ctx->dec_crc,
                       &ctx->dec_chass};
     for (DevBuf *b : bufs) b->release();
     ctx->pin.release();

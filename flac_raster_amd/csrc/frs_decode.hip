@@ -28,6 +28,34 @@ namespace frs {
 __constant__ uint8_t d_crc8[256];
 __constant__ uint16_t d_crc16[256];
 __device__ __attribute__((aligned(16))) uint16_t d_crc16x4[4][256];  // slice-by-4 tables (T_0 = d_crc16), host-computed once per device
+__device__ __attribute__((aligned(16))) uint16_t d_xpow_lo[256];   // x^(8m) mod P, m < 256
+__device__ uint16_t d_xpow_hi[4096];  // x^(8*256*m) mod P
+
+// a * b mod P (CRC-16 polynomial P = x^16 + x^15 + x^2 + 1), bitwise
+__device__ inline uint32_t dec_gfmul(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 15; i >= 0; i--) {
+        r <<= 1;
+        if (r & 0x10000u) r ^= 0x18005u;
+        if ((b >> i) & 1u) r ^= a;
+    }
+    return r;
+}
+// c * x^(8m) mod P: the CRC state c advanced over m zero bytes (m < 2^20)
+__device__ inline uint32_t crc_xpow(uint32_t c, uint32_t m) {
+    if (c == 0 || m == 0) return c;
+    return dec_gfmul(dec_gfmul(c, d_xpow_lo[m & 255]), d_xpow_hi[m >> 8]);
+}
+__device__ inline uint32_t gf_pow16(uint32_t b, uint64_t e) {  // b^e mod P
+    uint32_t r = 1;
+    while (e) {
+        if (e & 1) r = dec_gfmul(r, b);
+        b = dec_gfmul(b, b);
+        e >>= 1;
+    }
+    return r;
+}
 
 struct FrameHdr {
     int32_t ok;
@@ -190,6 +218,74 @@ __device__ inline uint32_t win_dword(const uint4 &w0, const uint4 &w1, int idx) 
     return r;
 }
 
+// ---- prefix CRC-16 of the selection range (two-pass form): the span check without a second read of the bytes.
+// A frame's CRC-16 footer verifies iff CRC([p, e)) == 0, and with pc(p) = CRC-16 of the range's bytes [0, p)
+// (init 0, no final xor: CRC(A B) = CRC(A) x^(8|B|) + CRC(B)), CRC([p, e)) = pc(e) + pc(p) x^(8(e - p)).  So the
+// selection pass, which reads every byte anyway, also folds them: each lane the CRC of its 16 bytes (slice-by-16),
+// a Horner state per lane over the wave's 16 steps, and -- only on steps holding a candidate or a stream boundary --
+// the step's prefix (the 64 lanes' states reduced) and the lanes' exclusive in-step scan, from which a point's
+// prefix within its 64 KB block follows.  A one-work-group scan chains the blocks; the span check is then one
+// comparison per candidate pair (k_span_pcrc) instead of re-reading every frame (k_span_crc_lane).
+constexpr int kSelCrcTab = 16 * 256 + 2 * 256 + 12 * 256;  // u16 entries: T16 | MK | ML[6]
+__device__ __attribute__((aligned(16))) uint16_t d_selcrc_tab[kSelCrcTab];  // host-computed once per device
+struct SelCrcLds {
+    uint16_t T[16][256];     // T[k][v]: CRC-16 of byte v followed by k zero bytes
+    uint16_t MK[2][256];     // multiply by x^(8 * 1024) (one step): [0] high byte, [1] low byte of the operand
+    uint16_t ML[6][2][256];  // multiply by x^(8 * 16 * 2^i) (lane tree level i)
+    uint16_t E[4][16][64];   // wave, step, lane: CRC of the step's bytes before the lane's 16 (point steps only)
+    uint32_t SW[4][16];      // wave, step: CRC of the wave's bytes before the step (point steps only)
+    uint32_t W[4];           // wave: CRC of its 16 KB
+    uint32_t WP[4];          // wave: CRC of the block's bytes before it
+};
+static_assert(offsetof(SelCrcLds, E) == 2 * kSelCrcTab, "tables first, contiguous");
+__device__ inline void sel_crc_load_tables(SelCrcLds *cx, int tid, int nthreads) {
+    for (int i = tid; i < kSelCrcTab / 8; i += nthreads)
+        reinterpret_cast<uint4 *>(&cx->T[0][0])[i] = reinterpret_cast<const uint4 *>(d_selcrc_tab)[i];
+}
+__device__ inline uint32_t crc_mul_tab(uint32_t c, const uint16_t (*M)[256]) { return (uint32_t)M[0][c >> 8] ^ M[1][c & 0xFFu]; }
+__device__ inline uint32_t chunk_crc16(const uint4 &v, const uint16_t (*T)[256]) {  // 16 bytes (LE dwords) from 0
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t c = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) c ^= T[15 - (4 * q + b)][(w[q] >> (8 * b)) & 0xFFu];
+    return c;
+}
+// every lane: XOR over lanes L of a_L x^(128 (63 - L)) -- the CRC of the 64 consecutive 16-byte pieces
+__device__ inline uint32_t lane_reduce_crc(uint32_t a, int lane, const uint16_t (*ML)[2][256]) {
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)a, 1 << i);
+        const bool hi = (lane >> i) & 1;
+        a = crc_mul_tab(hi ? o : a, ML[i]) ^ (hi ? a : o);
+    }
+    return a;
+}
+// lane L: the CRC of pieces 0 .. L - 1 (Kogge-Stone over the lanes)
+__device__ inline uint32_t lane_excl_scan_crc(uint32_t c, int lane, const uint16_t (*ML)[2][256]) {
+    uint32_t x = c;
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, 1 << i);
+        if (lane >= (1 << i)) x = crc_mul_tab(y, ML[i]) ^ x;
+    }
+    const uint32_t e = (uint32_t)__shfl_up((int)x, 1);
+    return lane ? e : 0u;
+}
+// CRC of the wave's bytes [wave start, point) for a point at step k, lane `lane`, byte j of its 16 (point steps'
+// SW / E recorded); the lane's first j bytes are read again (rare: candidates and stream boundaries)
+__device__ inline uint32_t sel_point_crc(const SelCrcLds *cx, int wv, int k, int lane, int j, const uint8_t *abase,
+                                         int64_t qc, int lead) {
+    uint32_t r = crc_xpow(cx->SW[wv][k], 16u * (uint32_t)lane + (uint32_t)j) ^ crc_xpow(cx->E[wv][k][lane], (uint32_t)j);
+    uint32_t c = 0;
+    for (int b = 0; b < j; b++) {
+        const uint32_t byte = qc + b >= lead ? abase[qc + b] : 0u;
+        c = ((c << 8) & 0xFFFFu) ^ cx->T[0][((c >> 8) ^ byte) & 0xFFu];
+    }
+    return r ^ c;
+}
+
 // The sync patterns `raw` (bit j: a 0xFF 0xF8/F9 pair at byte j) of one lane's 16 bytes `cur` (blob position p0),
 // `nxt` = the following 16 bytes: the bits whose header parses (header_ok_regs on the 32-byte window; the global
 // parse when the window does not hold the next 16 bytes).  Out of line: the rare path must not keep the caller's
@@ -232,9 +328,10 @@ __device__ __attribute__((noinline)) uint32_t sel_check_candidates(uint4 cur, ui
 // Only a header starting in the wave's last 16 bytes takes the global parse.  Headers are bounded by the blob end
 // (not the stream end: a header straddling a stream boundary becomes a candidate whose CRC span never verifies).
 // Returns the lane's candidate count.
-template <int STEPS = kSelSteps>
+template <int STEPS = kSelSteps, bool CRC = false>
 __device__ inline int sel_masks_co(const uint8_t *blob, int64_t nbytes, const int64_t *soff, int ns, int channels,
-                                   int stream_bps, int64_t qw, int lane, uint32_t *m) {
+                                   int stream_bps, int64_t qw, int lane, uint32_t *m, SelCrcLds *cx = nullptr,
+                                   int wv = 0, uint32_t bsteps = 0) {
     constexpr int kSelSteps = STEPS;
     const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
     const uint8_t *base = blob - lead;
@@ -253,6 +350,7 @@ __device__ inline int sel_masks_co(const uint8_t *blob, int64_t nbytes, const in
     const int64_t qlast = qw + 1024 * kSelSteps;  // the byte after the wave's 16 KB
     const uint32_t after = (lane == 63 && qlast < qend) ? base[qlast] : 0u;
     int cnt = 0;
+    uint32_t acc = 0;  // CRC: Horner state of this lane's pieces over the steps so far
 #pragma unroll
     for (int k = 0; k < kSelSteps; k++) {
         // first byte of the next 16 bytes: lane L + 1's word 0 (lane 63: next step's lane 0)
@@ -294,6 +392,28 @@ __device__ inline int sel_masks_co(const uint8_t *blob, int64_t nbytes, const in
         }
         m[k] = mask;
         cnt += __builtin_popcount(mask);
+        if constexpr (CRC) {
+            uint4 cv = v[k];
+            if (qw + 1024 * k + 16 * lane == 0 && lead) {  // bytes before the blob start count as zeros
+                auto keep = [&](uint32_t w, int d) -> uint32_t {
+                    const int nb = lead - 4 * d;  // leading bytes of this dword to clear
+                    return nb >= 4 ? 0u : nb <= 0 ? w : (w & ~((1u << (8 * nb)) - 1u));
+                };
+                cv = make_uint4(keep(cv.x, 0), keep(cv.y, 1), keep(cv.z, 2), keep(cv.w, 3));
+            }
+            const uint32_t c = chunk_crc16(cv, cx->T);
+            if (__ballot(mask != 0) || ((bsteps >> k) & 1u)) {  // (wave-uniform) a point step
+                const uint32_t sw = lane_reduce_crc(acc, lane, cx->ML);
+                const uint32_t e = lane_excl_scan_crc(c, lane, cx->ML);
+                cx->E[wv][k][lane] = (uint16_t)e;
+                if (lane == 0) cx->SW[wv][k] = sw;
+            }
+            acc = crc_mul_tab(acc, cx->MK) ^ c;
+        }
+    }
+    if constexpr (CRC) {
+        const uint32_t w = lane_reduce_crc(acc, lane, cx->ML);
+        if (lane == 0) cx->W[wv] = w;
     }
     return cnt;
 }
@@ -310,9 +430,11 @@ __device__ inline int wave_excl_scan_i32(int v, int lane, int &total) {
 }
 
 // candidate positions of one wave in (k, lane, j) order from output index `base`; past the cap only counted
-template <int STEPS = kSelSteps>
+// CRC: ccrc[idx] = CRC of [origin, candidate), `pre` = CRC of [origin, wave start)
+template <int STEPS = kSelSteps, bool CRC = false>
 __device__ inline void sel_emit_co(const uint32_t *m, int64_t qw, int lane, int lead, int64_t base, int64_t *cpos,
-                                   int64_t cap) {
+                                   int64_t cap, uint16_t *ccrc = nullptr, const SelCrcLds *cx = nullptr, int wv = 0,
+                                   const uint8_t *abase = nullptr, uint32_t pre = 0) {
     constexpr int kSelSteps = STEPS;
 #pragma unroll
     for (int k = 0; k < kSelSteps; k++) {
@@ -324,7 +446,14 @@ __device__ inline void sel_emit_co(const uint32_t *m, int64_t qw, int lane, int 
             while (mask) {
                 const int j = __builtin_ctz(mask);
                 mask &= mask - 1;
-                if (idx < cap) cpos[idx] = qw + 1024 * k + 16 * lane + j - lead;
+                if (idx < cap) {
+                    cpos[idx] = qw + 1024 * k + 16 * lane + j - lead;
+                    if constexpr (CRC) {
+                        const int64_t qc = qw + 1024 * k + 16 * lane;
+                        ccrc[idx] = (uint16_t)(crc_xpow(pre, (uint32_t)(qc + j - qw)) ^
+                                               sel_point_crc(cx, wv, k, lane, j, abase, qc, lead));
+                    }
+                }
                 idx++;
             }
         }
@@ -413,15 +542,48 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_select(const uint8_t *blob
 // only a block with more candidates than its scratch holds reads its 64 KB again (the range used to be read twice in
 // full: 3.1 GB more per whole-arena decode).
 constexpr int kSelBlkCap = 32;  // candidates kept per 64 KB block (a C4 block holds ~8 frame starts)
+
+// CRC combine of the block's four 16 KB waves (thread 0): WP[w] = CRC of the block's bytes before wave w; returns the
+// block's CRC
+__device__ inline uint32_t sel_crc_block(SelCrcLds *cx) {
+    const uint32_t X = d_xpow_hi[64];  // x^(8 * 16384)
+    uint32_t pre = 0;
+#pragma unroll
+    for (int w = 0; w < kSelThreads / 64; w++) {
+        cx->WP[w] = pre;
+        pre = dec_gfmul(pre, X) ^ cx->W[w];
+    }
+    return pre;
+}
+
+// CRC (prefix-CRC span check): the block's CRC to bcrc[b], each kept candidate's CRC from the block start to bipc
+// (beside bpos), and each stream boundary inside the block (bfirst[b]: the first such stream index, soff[s] + lead
+// past the block start) to sbib[s]
+template <bool CRC = false>
 __global__ void __launch_bounds__(kSelThreads) k_sync_count(const uint8_t *blob, int64_t nbytes, const int64_t *soff,
                                                           int ns, int channels, int stream_bps, int32_t *bcount,
-                                                          int64_t *bpos) {
+                                                          int64_t *bpos, uint16_t *bcrc = nullptr,
+                                                          uint16_t *bipc = nullptr, const uint32_t *bfirst = nullptr,
+                                                          uint16_t *sbib = nullptr) {
     __shared__ int s_wsum[kSelThreads / 64];
+    __shared__ typename std::conditional<CRC, SelCrcLds, char>::type cxs;
+    SelCrcLds *cx = CRC ? reinterpret_cast<SelCrcLds *>(&cxs) : nullptr;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
     const int64_t qw = (int64_t)blockIdx.x * kSelBytes + (int64_t)(kSelBytes / 4) * wv;
+    uint32_t bsteps = 0;  // this wave's steps holding a stream boundary
+    const int sb0 = CRC ? (int)bfirst[blockIdx.x] : -1;
+    if constexpr (CRC) {
+        sel_crc_load_tables(cx, t, kSelThreads);
+        for (int sidx = sb0; sidx >= 0 && sidx <= ns; sidx++) {
+            const int64_t q = soff[sidx] + lead;
+            if (q >= qw + kSelBytes / 4) break;
+            if (q >= qw) bsteps |= 1u << ((q - qw) >> 10);
+        }
+        __syncthreads();
+    }
     uint32_t m[kSelSteps];
-    int c = sel_masks_co(blob, nbytes, soff, ns, channels, stream_bps, qw, lane, m);
+    int c = sel_masks_co<kSelSteps, CRC>(blob, nbytes, soff, ns, channels, stream_bps, qw, lane, m, cx, wv, bsteps);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
     if (lane == 0) s_wsum[wv] = c;
@@ -433,15 +595,44 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_count(const uint8_t *blob,
         tot += s_wsum[k];
     }
     if (t == 0) bcount[blockIdx.x] = tot;
-    if (tot <= kSelBlkCap) {  // (block-uniform) keep the positions: the placement pass copies them
-        const int64_t slot = (int64_t)blockIdx.x * kSelBlkCap;
+    const int64_t slot = (int64_t)blockIdx.x * kSelBlkCap;
+    if constexpr (CRC) {
+        if (t == 0) bcrc[blockIdx.x] = (uint16_t)sel_crc_block(cx);
+        __syncthreads();
+        const uint8_t *abase = blob - lead;
+        if (tot <= kSelBlkCap)
+            sel_emit_co<kSelSteps, true>(m, qw, lane, lead, slot + wbase, bpos, slot + kSelBlkCap, bipc, cx, wv, abase,
+                                         cx->WP[wv]);
+        for (int sidx = sb0; sidx >= 0 && sidx <= ns; sidx++) {  // (wave-uniform loop) stream boundaries
+            const int64_t q = soff[sidx] + lead;
+            if (q >= qw + kSelBytes / 4) break;
+            if (q < qw) continue;
+            const int64_t d = q - qw;
+            if (lane == (int)((d >> 4) & 63))
+                sbib[sidx] = (uint16_t)(crc_xpow(cx->WP[wv], (uint32_t)d) ^
+                                        sel_point_crc(cx, wv, (int)(d >> 10), lane, (int)(d & 15), abase, q - (d & 15),
+                                                      lead));
+        }
+    } else if (tot <= kSelBlkCap) {  // (block-uniform) keep the positions: the placement pass copies them
         sel_emit_co(m, qw, lane, lead, slot + wbase, bpos, slot + kSelBlkCap);
     }
 }
 
+// stream boundaries for the prefix-CRC span check: bfirst[b] = the smallest stream index s >= 1 whose start
+// soff[s] + lead lies inside 64 KB block b (not at its first byte); bfirst is 0xFF-filled before
+__global__ void k_bound_mark(const int64_t *soff, int ns, int lead, uint32_t *bfirst) {
+    const int sidx = (int)(blockIdx.x * blockDim.x + threadIdx.x) + 1;
+    if (sidx > ns) return;
+    const int64_t q = soff[sidx] + lead;
+    if (q & (kSelBytes - 1)) atomicMin(&bfirst[q / kSelBytes], (uint32_t)sidx);
+}
+
 // exclusive scan of the block counts in one work-group (bbase[n] = total -> counts[0]); zeroes the later counters
-__global__ void __launch_bounds__(1024) k_sync_scan(const int32_t *bcount, int64_t *bbase, int64_t n, int *counts) {
+// CRC (bcrc != nullptr): also BP[i] = CRC of the range's bytes before block i, i = 0 .. n (BP[n]: all n blocks)
+__global__ void __launch_bounds__(1024) k_sync_scan(const int32_t *bcount, int64_t *bbase, int64_t n, int *counts,
+                                                  const uint16_t *bcrc = nullptr, uint32_t *BP = nullptr) {
     __shared__ int64_t wsum[16];
+    __shared__ uint32_t wcrc[16];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int64_t c = (n + 1023) / 1024;
     const int64_t a = min(n, (int64_t)t * c), b = min(n, a + c);
@@ -471,26 +662,69 @@ __global__ void __launch_bounds__(1024) k_sync_scan(const int32_t *bcount, int64
         counts[2] = 0;
         counts[3] = 0;
     }
+    if (!bcrc) return;
+    // thread t folds blocks [t c, t c + c) (blocks >= n: zeros), Kogge-Stone over the threads with the uniform
+    // multipliers KB^(c 2^i), KB = x^(8 * 64 KB); then each thread re-walks its blocks from its exclusive prefix
+    const uint32_t KB = d_xpow_hi[256];
+    const int64_t a2 = (int64_t)t * c;
+    uint32_t h = 0;
+    for (int64_t i = a2; i < a2 + c; i++) h = dec_gfmul(h, KB) ^ (i < n ? (uint32_t)bcrc[i] : 0u);
+    const uint32_t Mc = gf_pow16(KB, (uint64_t)c);  // one thread's span
+    uint32_t x2 = h, mo = Mc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x2, o);
+        if (lane >= o) x2 = dec_gfmul(y, mo) ^ x2;
+        mo = dec_gfmul(mo, mo);  // Mc^(2o)
+    }
+    if (lane == 63) wcrc[wv] = x2;  // the wave's 64 c blocks
+    __syncthreads();
+    const uint32_t M64 = mo;  // Mc^64
+    uint32_t pre = 0;
+    for (int k = 0; k < wv; k++) pre = dec_gfmul(pre, M64) ^ wcrc[k];
+    const uint32_t incl = dec_gfmul(pre, gf_pow16(Mc, (uint64_t)(lane + 1))) ^ x2;  // blocks [0, (t + 1) c)
+    const uint32_t up = (uint32_t)__shfl_up((int)incl, 1);
+    uint32_t rc = lane ? up : pre;  // blocks [0, t c)
+    for (int64_t i = a2; i < a2 + c && i <= n; i++) {
+        BP[i] = rc;
+        if (i < n) rc = dec_gfmul(rc, KB) ^ bcrc[i];
+    }
+    if (a2 + c == n) BP[n] = rc;  // (n a multiple of c: no thread's range holds index n)
 }
 
 // placement: a block's kept positions to cpos[bbase ...]; a block whose candidates overflowed its scratch recomputes
-// its flags (re-reads its 64 KB) and emits them directly
+// its flags (re-reads its 64 KB) and emits them directly.  CRC: pcrc[i] = CRC of the range's bytes before candidate i
+template <bool CRC = false>
 __global__ void __launch_bounds__(kSelThreads) k_sync_scatter(const uint8_t *blob, int64_t nbytes, const int64_t *soff,
                                                             int ns, int channels, int stream_bps, const int64_t *bbase,
                                                             int64_t *cpos, int64_t cap, const int32_t *bcount,
-                                                            const int64_t *bpos) {
+                                                            const int64_t *bpos, uint16_t *pcrc = nullptr,
+                                                            const uint32_t *BP = nullptr,
+                                                            const uint16_t *bipc = nullptr) {
     __shared__ int s_wsum[kSelThreads / 64];
+    __shared__ typename std::conditional<CRC, SelCrcLds, char>::type cxs;
+    SelCrcLds *cx = CRC ? reinterpret_cast<SelCrcLds *>(&cxs) : nullptr;
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int tot = bcount[blockIdx.x];
+    const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
+    const int64_t bq0 = (int64_t)blockIdx.x * kSelBytes;
     if (tot <= kSelBlkCap) {  // (block-uniform)
         const int64_t dst = bbase[blockIdx.x] + t;
-        if (t < tot && dst < cap) cpos[dst] = bpos[(int64_t)blockIdx.x * kSelBlkCap + t];
+        if (t < tot && dst < cap) {
+            const int64_t src = (int64_t)blockIdx.x * kSelBlkCap + t;
+            const int64_t p = bpos[src];
+            cpos[dst] = p;
+            if constexpr (CRC) pcrc[dst] = (uint16_t)(crc_xpow(BP[blockIdx.x], (uint32_t)(p + lead - bq0)) ^ bipc[src]);
+        }
         return;
     }
-    const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
-    const int64_t qw = (int64_t)blockIdx.x * kSelBytes + (int64_t)(kSelBytes / 4) * wv;
+    if constexpr (CRC) {
+        sel_crc_load_tables(cx, t, kSelThreads);
+        __syncthreads();
+    }
+    const int64_t qw = bq0 + (int64_t)(kSelBytes / 4) * wv;
     uint32_t m[kSelSteps];
-    int c = sel_masks_co(blob, nbytes, soff, ns, channels, stream_bps, qw, lane, m);
+    int c = sel_masks_co<kSelSteps, CRC>(blob, nbytes, soff, ns, channels, stream_bps, qw, lane, m, cx, wv, 0u);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
     if (lane == 0) s_wsum[wv] = c;
@@ -498,7 +732,15 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_scatter(const uint8_t *blo
     int wbase = 0;
 #pragma unroll
     for (int k = 0; k < kSelThreads / 64; k++) wbase += k < wv ? s_wsum[k] : 0;
-    sel_emit_co(m, qw, lane, lead, bbase[blockIdx.x] + wbase, cpos, cap);
+    if constexpr (CRC) {
+        if (t == 0) (void)sel_crc_block(cx);
+        __syncthreads();
+        const uint32_t pre = crc_xpow(BP[blockIdx.x], (uint32_t)(qw - bq0)) ^ cx->WP[wv];  // bytes before the wave
+        sel_emit_co<kSelSteps, true>(m, qw, lane, lead, bbase[blockIdx.x] + wbase, cpos, cap, pcrc, cx, wv, blob - lead,
+                                     pre);
+    } else {
+        sel_emit_co(m, qw, lane, lead, bbase[blockIdx.x] + wbase, cpos, cap);
+    }
 }
 
 // Fused de-normalisation of decoded samples (converter.py:88-110 after pyflac + soundfile's PCM_16 WAV round
@@ -603,19 +845,6 @@ __device__ inline void stage_words(uint32_t *stage, const uint8_t *blob, int64_t
     }
 }
 constexpr int kSpanWords = 6144;  // 24 KB stage
-__device__ __attribute__((aligned(16))) uint16_t d_xpow_lo[256];   // x^(8m) mod P, m < 256
-__device__ uint16_t d_xpow_hi[4096];  // x^(8*256*m) mod P
-
-__device__ inline uint32_t dec_gfmul(uint32_t a, uint32_t b) {
-    uint32_t r = 0;
-#pragma unroll
-    for (int i = 15; i >= 0; i--) {
-        r <<= 1;
-        if (r & 0x10000u) r ^= 0x18005u;
-        if ((b >> i) & 1u) r ^= a;
-    }
-    return r;
-}
 
 __global__ void __launch_bounds__(64) k_span_crc_wave(const uint8_t *blob, const int64_t *soff, int ns,
                                                      const int64_t *cpos, const int *ncand, int cand_cap,
@@ -785,6 +1014,50 @@ __global__ void __launch_bounds__(256) k_span_crc_lane(const uint8_t *blob, cons
     }
 }
 
+// Span check from the selection's prefix CRCs (two-pass form), one lane per candidate: the first later candidate e
+// (or the stream end) with pc(e) == pc(p) x^(8(e - p)), i.e. the span's CRC-16 footer verifies -- the same candidates
+// tried in the same order as k_span_crc_lane, without reading a byte.  The stream end's prefix comes from its block's
+// prefix and the in-block value the count pass left (sbib).
+__global__ void __launch_bounds__(256) k_span_pcrc(const int64_t *soff, int ns, const int64_t *cpos, const int *ncand,
+                                                  int cand_cap, int64_t max_frame, const uint16_t *pcrc,
+                                                  const uint32_t *BP, const uint16_t *sbib, int lead, int64_t *ends,
+                                                  int32_t *nexti) {
+    const int nc = *ncand;
+    if (nc > cand_cap) return;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nc; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t p = cpos[i];
+        const int s = stream_of(soff, ns, p);
+        const int64_t send = soff[s + 1];
+        const int64_t lim = min(send, p + max_frame);
+        const uint32_t pp = pcrc[i];
+        int64_t result = -1;
+        int32_t rnext = -1;
+        for (int64_t j = i + 1;; j++) {
+            const int64_t cj = j < nc ? cpos[j] : send;
+            const int64_t e = cj > send ? send : cj;
+            if (e > lim) break;
+            if (e >= p + 7) {
+                uint32_t pe;
+                if (j < nc && cj == e) {
+                    pe = pcrc[j];
+                } else {  // the stream end
+                    const int64_t q = send + lead;
+                    const int64_t off = q & (kSelBytes - 1);
+                    pe = crc_xpow(BP[q / kSelBytes], (uint32_t)off) ^ (off ? (uint32_t)sbib[s + 1] : 0u);
+                }
+                if (pe == crc_xpow(pp, (uint32_t)(e - p))) {
+                    result = e;
+                    rnext = (j < nc && cpos[j] < send) ? (int32_t)j : -2;
+                    break;
+                }
+            }
+            if (e >= send) break;
+        }
+        ends[i] = result;
+        nexti[i] = rnext;
+    }
+}
+
 // Frame chain of each stream from its first byte: one work-group per stream loads the stream's candidate ->
 // next-candidate links (the span kernels' nexti) into LDS and lane 0 walks them, one LDS read per frame (streams
 // with more candidates than the LDS table walk global memory).  frame_cand[fbase[s] + k] = candidate of frame k,
@@ -800,25 +1073,28 @@ __device__ inline int lower_bound_pos(const int64_t *cpos, int n, int64_t p) {
     }
     return lo;
 }
-__global__ void __launch_bounds__(64) k_chain_lds(const int64_t *soff, int ns, const int64_t *cpos, const int *ncand,
-                                                 int cand_cap,
-                                                 const int32_t *nexti, const int64_t *fbase, int64_t *frame_cand,
-                                                 int *bad) {
+__global__ void __launch_bounds__(1024) k_chain_lds(const int64_t *soff, int ns, const int64_t *cpos, const int *ncand,
+                                                   int cand_cap,
+                                                   const int32_t *nexti, const int64_t *fbase, int64_t *frame_cand,
+                                                   int *bad) {
     __shared__ int32_t nx[kChainLds];
     __shared__ int32_t rng[2];
+    __shared__ int32_t wcnt[16];
+    __shared__ int32_t sbad;
     const int s = blockIdx.x;
     if (s >= ns) return;
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nt = blockDim.x, nw = nt >> 6;
     const int nc = *ncand;
     const int64_t fb = fbase[s], nf = fbase[s + 1] - fb;
     if (nc > cand_cap) {  // uniform: the selection overflowed its buffer (the host reports it)
-        for (int64_t k = lane; k < nf; k += 64) frame_cand[fb + k] = -1;
-        if (lane == 0) atomicAdd(bad, 1);
+        for (int64_t k = tid; k < nf; k += nt) frame_cand[fb + k] = -1;
+        if (tid == 0) atomicAdd(bad, 1);
         return;
     }
-    if (lane == 0) {
+    if (tid == 0) {
         rng[0] = ns == 1 ? 0 : lower_bound_pos(cpos, nc, soff[s]);
         rng[1] = ns == 1 ? nc : lower_bound_pos(cpos, nc, soff[s + 1]);
+        sbad = 0;
     }
     __syncthreads();
     const int c0 = rng[0], c1 = rng[1];
@@ -828,42 +1104,46 @@ __global__ void __launch_bounds__(64) k_chain_lds(const int64_t *soff, int ns, c
         // dependent LDS reads by one lane, ~10 us).  Optimistic parallel ranking instead: the verified candidates
         // (link != -1) in position order ARE the chain when there are nf of them, each links to the next and the last
         // to the stream end -- checked below; anything else (a false sync with a verified span) falls back to the
-        // exact walk.
+        // exact walk.  All of the work-group's waves rank (one wave per stream of a batched decode, 16 for the one
+        // long stream of a plain multi-band convert).
         int64_t cnt = 0;
-        for (int i0 = c0; i0 < c1; i0 += 256) {
-            int32_t v[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int i = i0 + 64 * u + lane;
-                v[u] = i < c1 ? nexti[i] : -1;
+        for (int i0 = c0; i0 < c1; i0 += nt) {
+            const int i = i0 + tid;
+            const int32_t v = i < c1 ? nexti[i] : -1;
+            const uint64_t m = __ballot(v != -1);
+            if (lane == 0) wcnt[wv] = __popcll(m);
+            __syncthreads();
+            int64_t before = cnt, tot = 0;
+            for (int k = 0; k < nw; k++) {
+                before += k < wv ? wcnt[k] : 0;
+                tot += wcnt[k];
             }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int i = i0 + 64 * u + lane;
-                const uint64_t m = __ballot(v[u] != -1);
-                const int64_t r = cnt + __popcll(m & ((1ull << lane) - 1ull));
-                if (v[u] != -1 && r < nf) frame_cand[fb + r] = i;
-                cnt += __popcll(m);
-            }
+            const int64_t r = before + __popcll(m & ((1ull << lane) - 1ull));
+            if (v != -1 && r < nf) frame_cand[fb + r] = i;
+            cnt += tot;
+            __syncthreads();  // wcnt reused
         }
         bool good = cnt == nf;
         if (good) {
             __threadfence();
+            __syncthreads();
             bool bad_link = false;
-            for (int64_t k = lane; k < nf; k += 64) {
+            for (int64_t k = tid; k < nf; k += nt) {
                 const int64_t ci = frame_cand[fb + k];
                 const int32_t want = k + 1 < nf ? (int32_t)frame_cand[fb + k + 1] : -2;
                 bad_link |= nexti[ci] != want || (k == 0 && ci != c0);  // frame 0 is the stream's first byte
             }
-            good = __ballot(bad_link) == 0;
+            if (bad_link) sbad = 1;
+            __syncthreads();
+            good = sbad == 0;
         }
         if (good) return;
         __threadfence();
     }
     if (in_lds)
-        for (int k = lane; k < c1 - c0; k += 64) nx[k] = nexti[c0 + k];
+        for (int k = tid; k < c1 - c0; k += nt) nx[k] = nexti[c0 + k];
     __syncthreads();
-    if (lane != 0) return;
+    if (tid != 0) return;
     bool ok = c0 < c1 && cpos[c0] == soff[s];
     int64_t k = 0;
     int idx = c0;
@@ -2529,6 +2809,37 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
             hi[m] = (uint16_t)pw;
             pw = mulmod(pw, step);
         }
+        // prefix-CRC selection tables: slice-by-16, x^(8 * 1024), x^(8 * 16 * 2^i) as byte-split multipliers
+        static uint16_t sct[kSelCrcTab];
+        {
+            uint16_t *T = sct, *MK = sct + 16 * 256, *ML = sct + 18 * 256;
+            for (int i = 0; i < 256; i++) {
+                uint16_t c = t16[i];
+                T[i] = c;
+                for (int j = 1; j < 16; j++) {
+                    c = (uint16_t)(((c << 8) & 0xFFFF) ^ t16[c >> 8]);
+                    T[256 * j + i] = c;
+                }
+            }
+            auto xpow8 = [&](uint64_t m) {  // x^(8m) mod P
+                uint32_t r = 1, b = 0x100;
+                while (m) {
+                    if (m & 1) r = mulmod(r, b);
+                    b = mulmod(b, b);
+                    m >>= 1;
+                }
+                return r;
+            };
+            auto split = [&](uint16_t *M, uint32_t K) {
+                for (int v = 0; v < 256; v++) {
+                    M[v] = (uint16_t)mulmod((uint32_t)v << 8, K);
+                    M[256 + v] = (uint16_t)mulmod((uint32_t)v, K);
+                }
+            };
+            split(MK, xpow8(1024));
+            for (int i = 0; i < 6; i++) split(ML + 512 * i, xpow8(16u << i));
+        }
+        FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(d_selcrc_tab), sct, sizeof(sct), 0, hipMemcpyHostToDevice, st));
         FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(d_xpow_lo), lo, sizeof(lo), 0, hipMemcpyHostToDevice, st));
         FRS_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(d_xpow_hi), hi, sizeof(hi), 0, hipMemcpyHostToDevice, st));
         FRS_HIP(hipStreamSynchronize(st));
@@ -2620,6 +2931,18 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     int64_t *cpos = ctx->dec_cand.as<int64_t>();
     int64_t *ends = cpos + cand_cap;
     int32_t *nexti = ctx->dec_next.as<int32_t>();
+    // multi-channel decodes of a large range (the two-pass selection): the span check from prefix CRCs the selection
+    // folds (k_span_pcrc), within the x^(8m) table range.  Measured (round 5, MI355X): a 4-band 16384^2 stream (one
+    // stream of 65536 32-KB frames: the lane span check has few, long spans) select + span 2.49 -> 1.94 ms; the C4
+    // batched mono decode (6241 streams of 8-KB frames) 2.16 -> 3.21 ms (the selection's CRC fold costs more than the
+    // reading span check it replaces: 1 LDS table lookup per byte either way, at lower occupancy), so mono keeps the
+    // reading form.  FRS_SPAN_READ=1 / 2 forces the reading / prefix form (tests).
+    const char *span_env = getenv("FRS_SPAN_READ");
+    const int span_mode = span_env ? atoi(span_env) : 0;
+    const bool pcrc_span = span_mode != 1 && (span_mode == 2 || mcl) && nblocks > kSelOnePassBlocks &&
+                           (lane || !pipe) && max_frame < (int64_t)4096 * 256;
+    uint32_t *BPv = nullptr;
+    uint16_t *sbibv = nullptr, *pcrcv = nullptr;
     hipEvent_t ev;
     prof_begin(ctx, "decode", &ev);
     if (nblocks <= kSelOnePassBlocks) {
@@ -2638,18 +2961,47 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         int32_t *bcount = ctx->dec_sel.as<int32_t>();
         int64_t *bbase = ctx->dec_sel.as<int64_t>() + (nblocks + 1) / 2 + 1;
         int64_t *bpos = bbase + nblocks + 1;
-        k_sync_count<<<(unsigned)nblocks, kSelThreads, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams, channels, bps,
-                                                                bcount, bpos);
-        k_sync_scan<<<1, 1024, 0, st>>>(bcount, bbase, nblocks, ncand);
-        k_sync_scatter<<<(unsigned)nblocks, kSelThreads, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams, channels, bps,
-                                                                  bbase, cpos, cand_cap, bcount, bpos);
+        if (pcrc_span) {
+            // [BP u32 (nblocks + 1) | bfirst u32 nblocks | bcrc u16 nblocks | bipc u16 32 nblocks | sbib u16 ns + 1 |
+            //  pcrc u16 cand_cap]
+            const size_t nb = (size_t)nblocks;
+            const size_t bytes = 4 * (nb + 1) + 4 * nb + 2 * nb + 2 * kSelBlkCap * nb + 2 * ((size_t)nstreams + 1) +
+                                 2 * (size_t)cand_cap + 64;
+            FRS_HIP(ctx->dec_crc.ensure(bytes));
+            BPv = ctx->dec_crc.as<uint32_t>();
+            uint32_t *bfirst = BPv + nb + 1;
+            uint16_t *bcrc = reinterpret_cast<uint16_t *>(bfirst + nb);
+            uint16_t *bipc = bcrc + nb;
+            sbibv = bipc + kSelBlkCap * nb;
+            pcrcv = sbibv + nstreams + 1;
+            const int lead = (int)(reinterpret_cast<uintptr_t>(blob_dev) & 15);
+            FRS_HIP(hipMemsetAsync(bfirst, 0xFF, 4 * nb, st));
+            k_bound_mark<<<(unsigned)((nstreams + 255) / 256), 256, 0, st>>>(dsoff, nstreams, lead, bfirst);
+            k_sync_count<true><<<(unsigned)nblocks, kSelThreads, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams,
+                                                                          channels, bps, bcount, bpos, bcrc, bipc,
+                                                                          bfirst, sbibv);
+            k_sync_scan<<<1, 1024, 0, st>>>(bcount, bbase, nblocks, ncand, bcrc, BPv);
+            k_sync_scatter<true><<<(unsigned)nblocks, kSelThreads, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams,
+                                                                            channels, bps, bbase, cpos, cand_cap,
+                                                                            bcount, bpos, pcrcv, BPv, bipc);
+        } else {
+            k_sync_count<<<(unsigned)nblocks, kSelThreads, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams, channels,
+                                                                    bps, bcount, bpos);
+            k_sync_scan<<<1, 1024, 0, st>>>(bcount, bbase, nblocks, ncand);
+            k_sync_scatter<<<(unsigned)nblocks, kSelThreads, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams, channels,
+                                                                      bps, bbase, cpos, cand_cap, bcount, bpos);
+        }
     }
     prof_end(ctx, "decode", ev);
     prof_begin(ctx, "decode_span", &ev);
     // launched before the host knows the candidate count (no mid-query sync): an upper-bound grid strides over
     // *ncand on the device; an overflowing selection makes every later kernel a no-op and is reported below
-    if (lane || !pipe) {  // batched (or long multi-channel / 32-bit frames, which the wave form would walk on one lane
-                          // past its LDS stage): one lane per candidate, over an upper-bound grid (no mid-call sync)
+    if (pcrc_span) {
+        k_span_pcrc<<<(unsigned)((std::min<int64_t>(cand_cap, 2 * frames + 256) + 255) / 256), 256, 0, st>>>(
+            dsoff, nstreams, cpos, ncand, (int)cand_cap, max_frame, pcrcv, BPv, sbibv,
+            (int)(reinterpret_cast<uintptr_t>(blob_dev) & 15), ends, nexti);
+    } else if (lane || !pipe) {  // batched (or long multi-channel / 32-bit frames, which the wave form would walk on
+                                 // one lane past its LDS stage): one lane per candidate, over an upper-bound grid
         k_span_crc_lane<<<(unsigned)((std::min<int64_t>(cand_cap, 2 * frames + 256) + 255) / 256), 256, 0, st>>>(
             blob_dev, dsoff, nstreams, cpos, ncand, (int)cand_cap, max_frame, ends, nexti);
     } else if (max_frame < (int64_t)4096 * 256) {  // x^(8m) table range of the wave CRC
@@ -2660,7 +3012,8 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         k_span_crc<<<(unsigned)((cand_cap + 63) / 64), 64, 0, st>>>(blob_dev, dsoff, nstreams, cpos, ncand,
                                                                     (int)cand_cap, max_frame, ends, nexti);
     }
-    k_chain_lds<<<nstreams, 64, 0, st>>>(dsoff, nstreams, cpos, ncand, (int)cand_cap, nexti, dfbase, dchain, bad);
+    k_chain_lds<<<nstreams, nstreams == 1 ? 1024 : 64, 0, st>>>(dsoff, nstreams, cpos, ncand, (int)cand_cap, nexti,
+                                                                 dfbase, dchain, bad);
     prof_end(ctx, "decode_span", ev);
     DecOut dout;
     dout.out = out_dev;

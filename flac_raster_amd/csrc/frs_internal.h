@@ -78,7 +78,7 @@ struct frs_ctx {
     hipStream_t h2d_stream = nullptr, d2h_stream = nullptr;  // its copy engines' streams (created on first use)
     DevBuf host_pack;                  // device side of the packed fast-path results
     // decode scratch
-    DevBuf dec_cand, dec_count, dec_pcm, dec_soff, dec_next, dec_status, dec_fb, dec_sel, dec_chass;
+    DevBuf dec_cand, dec_count, dec_pcm, dec_soff, dec_next, dec_status, dec_fb, dec_sel, dec_chass, dec_crc;
     int decode_lane = -1;    // FRS_DECODE_LANE=0/1 (tests): force the pipelined / lane-per-frame decoder
     uint32_t dec_epoch = 0;  // call counter tagging the candidate selection's look-back words (24 bits, never 0)
     // profiling

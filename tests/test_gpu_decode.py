@@ -265,12 +265,16 @@ def test_wrapped_lpc_prediction_decodes_exactly(gpu_ctx, kind, monkeypatch):
     dctx.close()
 
 
-def test_large_range_dense_candidates_lossless(gpu_ctx):
+@pytest.mark.parametrize("span", ["pcrc", "read"])
+def test_large_range_dense_candidates_lossless(gpu_ctx, span, monkeypatch):
     """Ranges above 16 MB take the two-pass selection: per-64-KB-block counts that keep up to 32 candidate positions
     per block, a scan, and a placement pass that copies them (a block with more candidates re-reads its bytes).
     Ramps code to tiny frames (hundreds of sync candidates per block: the re-read path), noise in the other half of
-    the same job to ~8 KB frames (the kept-positions path); all tiles decode losslessly in one call."""
-    from flac_raster_amd import streaming
+    the same job to ~8 KB frames (the kept-positions path); all tiles decode losslessly in one call.  span="pcrc": the
+    span check from the prefix CRCs the selection folds (k_span_pcrc); "read": the span check that reads every frame
+    again (k_span_crc_lane).  A flipped byte anywhere ends in FrsError either way."""
+    from flac_raster_amd import _native, streaming
+    monkeypatch.setenv("FRS_SPAN_READ", "1" if span == "read" else "2")
     rng = np.random.default_rng(5)
     H, W, T = 6144, 6144, 512
     y, x = np.mgrid[0:H, 0:W]
@@ -289,3 +293,12 @@ def test_large_range_dense_candidates_lossless(gpu_ctx):
     for (c0, r0, w, h), n in zip(streaming.tile_grid(H, W, T), counts):
         assert np.array_equal(vals[a:a + n].reshape(h, w), band[r0:r0 + h, c0:c0 + w]), (r0, c0)
         a += n
+    pcm = gpu_ctx.decode_frames_host(arena, off, counts, channels=1, bps=16)
+    for t in (0, len(counts) // 2 + 3, len(counts) - 1):  # a ramp tile, a noise tile, the last tile
+        ref = O.decode_frames(arena[off[t]:off[t + 1]].tobytes(), 1, 16, counts[t])
+        assert np.array_equal(pcm[int(np.sum(counts[:t])):int(np.sum(counts[:t + 1]))], ref), t
+    for pos in (int(off[1]) + 37, int(off[len(counts) // 2 + 3]) + 5000, int(off[-1]) - 3):  # frame bodies, a footer
+        flipped = arena.copy()
+        flipped[pos] ^= 0x10
+        with pytest.raises(_native.FrsError):
+            gpu_ctx.decode_frames_host(flipped, off, counts, channels=1, bps=16)
