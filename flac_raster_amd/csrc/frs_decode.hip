@@ -2429,44 +2429,6 @@ struct LaneReader {
     }
 };
 
-// Channel-planar int32 PCM of the multi-channel lane decoder -> the interleaved output (de-normalised when fused,
-// int32 PCM otherwise): one thread per output element, elements in output order (coalesced stores).
-// Two-channel streams (fchass != nullptr): the frame's channel assignment (written by the lane decoder) undoes
-// libFLAC's stereo decorrelation here -- left-side R = L - S, right-side L = R + S, mid-side from (M << 1 | S & 1).
-__global__ void __launch_bounds__(256) k_interleave_dn(const int32_t *planar, const int64_t *poff, const int64_t *fbase,
-                                                      int ns, int nch, int blocksize, int32_t *pcm, DecOut dout,
-                                                      const int8_t *fchass) {
-    const int64_t total = (poff[ns] - poff[0]) * nch;
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t g = poff[0] + e / nch;  // sample index
-        const int c = (int)(e - (g - poff[0]) * nch);
-        int lo = 0, hi = ns - 1;  // stream of sample g
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (poff[mid] <= g) lo = mid;
-            else hi = mid - 1;
-        }
-        const int64_t i = g - poff[lo];
-        const int64_t fi = fbase[lo] + i / blocksize;
-        int32_t x = planar[(fi * nch + c) * (int64_t)blocksize + (i % blocksize)];
-        if (fchass) {
-            const int ca = fchass[fi];
-            if (ca >= 8) {
-                const int64_t a = planar[(fi * 2) * (int64_t)blocksize + (i % blocksize)];
-                const int64_t sd = planar[(fi * 2 + 1) * (int64_t)blocksize + (i % blocksize)];
-                if (ca == 8) x = c == 0 ? (int32_t)a : (int32_t)(a - sd);
-                else if (ca == 9) x = c == 0 ? (int32_t)(a + sd) : (int32_t)sd;
-                else {
-                    const int64_t mid = (a * 2) | (sd & 1);
-                    x = (int32_t)(c == 0 ? (mid + sd) >> 1 : (mid - sd) >> 1);
-                }
-            }
-        }
-        if (dout.out) dn_store(dout, g * nch + c, x, dout.dn[lo]);
-        else pcm[g * nch + c] = x;
-    }
-}
-
 // converter.py:88-110 value of one decoded sample as the bits of a <= 4-byte output element
 template <int OUT>
 __device__ inline uint32_t dn_bits_t(const DecOut &o, int32_t pcm, float2 p) {
@@ -2481,6 +2443,66 @@ __device__ inline uint32_t dn_bits_t(const DecOut &o, int32_t pcm, float2 p) {
         const int64_t r = (int64_t)rintf(a);
         if constexpr (OUT == kOutU8) return (uint32_t)(uint8_t)r;
         else return (uint32_t)(uint16_t)r;
+    }
+}
+
+// Channel-planar int32 PCM of the multi-channel lane decoder -> the interleaved output (de-normalised when fused,
+// int32 PCM otherwise).  One work-group per (frame, 256-sample chunk): its stream is found once (block-uniform), and
+// each thread takes one sample position with all nch channels -- nch coalesced planar reads, nch adjacent output
+// elements (a thread per output element, each locating its stream and frame by 64-bit division, was 4.6 ms for a
+// 4-band 16384^2 stream: integer-divide bound).
+// Two-channel streams (fchass != nullptr): the frame's channel assignment (written by the lane decoder) undoes
+// libFLAC's stereo decorrelation here -- left-side R = L - S, right-side L = R + S, mid-side from (M << 1 | S & 1).
+__global__ void __launch_bounds__(256) k_interleave_dn(const int32_t *planar, const int64_t *poff, const int64_t *fbase,
+                                                      int ns, int nch, int blocksize, int32_t *pcm, DecOut dout,
+                                                      const int8_t *fchass, int cpf) {
+    const int64_t fi = blockIdx.x / (unsigned)cpf;
+    const int i = (int)(blockIdx.x - fi * cpf) * 256 + (int)threadIdx.x;  // sample position in the frame
+    if (i >= blocksize) return;
+    int lo = 0, hi = ns - 1;  // stream of frame fi (block-uniform)
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (fbase[mid] <= fi) lo = mid;
+        else hi = mid - 1;
+    }
+    const int64_t g = poff[lo] + (fi - fbase[lo]) * blocksize + i;  // sample index
+    if (g >= poff[lo + 1]) return;
+    const int32_t *src = planar + fi * nch * (int64_t)blocksize + i;
+    int32_t x[8];
+#pragma unroll
+    for (int c = 0; c < 8; c++) x[c] = c < nch ? src[(int64_t)c * blocksize] : 0;
+    if (fchass) {
+        const int ca = fchass[fi];
+        const int64_t a = x[0], sd = x[1];
+        if (ca == 8) x[1] = (int32_t)(a - sd);
+        else if (ca == 9) x[0] = (int32_t)(a + sd);
+        else if (ca == 10) {
+            const int64_t mid = (a * 2) | (sd & 1);
+            x[0] = (int32_t)((mid + sd) >> 1);
+            x[1] = (int32_t)((mid - sd) >> 1);
+        }
+    }
+    if (dout.out && (dout.dtype == FRS_DT_I16 || dout.dtype == FRS_DT_U16) && !(nch & 1)) {
+        // 16-bit outputs of an even channel count: the thread's nch elements in 4-byte (8-byte for 4 channels) stores
+        uint32_t v[8];
+#pragma unroll
+        for (int c = 0; c < 8; c++) v[c] = c < nch ? dn_bits_t<kOutI16>(dout, x[c], dout.dn[lo]) : 0u;
+        uint16_t *o = static_cast<uint16_t *>(dout.out) + g * nch;
+        if (nch == 4) {
+            *reinterpret_cast<uint2 *>(o) = make_uint2(v[0] | (v[1] << 16), v[2] | (v[3] << 16));
+        } else {
+#pragma unroll
+            for (int c = 0; c < 8; c += 2)
+                if (c < nch) *reinterpret_cast<uint32_t *>(o + c) = v[c] | (v[c + 1] << 16);
+        }
+        return;
+    }
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+        if (c < nch) {
+            if (dout.out) dn_store(dout, g * nch + c, x[c], dout.dn[lo]);
+            else pcm[g * nch + c] = x[c];
+        }
     }
 }
 
@@ -3056,8 +3078,9 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         k_decode_frames_lane<kOutPcm, true><<<(unsigned)((frames + 255) / 256), 256, 0, st>>>(
             blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, dchain, frames, bps, pcm_dev, blocksize, nvalid, dout,
             fbl, fbc, channels, planar, fchass);
-        k_interleave_dn<<<(unsigned)std::min<int64_t>((nsamp_all * channels + 255) / 256, 16 * (int64_t)ctx->num_cus),
-                          256, 0, st>>>(planar, dpoff, dfbase, nstreams, channels, blocksize, pcm_dev, dout, fchass);
+        const int cpf = (blocksize + 255) / 256;
+        k_interleave_dn<<<(unsigned)(frames * cpf), 256, 0, st>>>(planar, dpoff, dfbase, nstreams, channels, blocksize,
+                                                                 pcm_dev, dout, fchass, cpf);
         k_decode_frames_wave_list<<<(unsigned)std::min<int64_t>(frames, 4 * (int64_t)ctx->num_cus), 64, 0, st>>>(
             blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, dchain, channels, bps, pcm_dev, blocksize, nvalid,
             dout, fbl, fbc);
