@@ -498,9 +498,11 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_select(const uint8_t *blob
         if (ord == 0) {
             if (lane == 0) {
                 __hip_atomic_store(&status[0], tag | kSelIncl | (uint64_t)tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                counts[1] = 0;  // nvalid, bad, lane-decoder queue: zeroed here (later kernels run after this one)
-                counts[2] = 0;
+                counts[1] = 0;  // nvalid, bad, lane-decoder queue, optimistic-decode fallback flag and count:
+                counts[2] = 0;  // zeroed here (later kernels run after this one)
                 counts[3] = 0;
+                counts[6] = 0;  // (ints 4-5 hold the selection ticket)
+                counts[7] = 0;
             }
         } else {
             if (lane == 0)
@@ -661,6 +663,8 @@ __global__ void __launch_bounds__(1024) k_sync_scan(const int32_t *bcount, int64
         counts[1] = 0;
         counts[2] = 0;
         counts[3] = 0;
+        counts[6] = 0;  // (ints 4-5 hold the selection ticket)
+        counts[7] = 0;
     }
     if (!bcrc) return;
     // thread t folds blocks [t c, t c + c) (blocks >= n: zeros), Kogge-Stone over the threads with the uniform
@@ -1775,15 +1779,24 @@ __device__ inline void lds_publish(volatile int32_t *p, int32_t v) {
 }
 __device__ inline int32_t lds_poll(volatile int32_t *p) { return *p; }
 
+// OPT (small ranges, launched right after the selection): the optimistic form -- when the selection found exactly
+// one candidate per frame and each stream's first at its first byte, frame i IS candidate i and its span ends at
+// candidate i + 1 (or the stream end), so the span check and the chain are skipped: the consumer wave checks the
+// span's CRC-16 over the staged bytes while the producer parses, and a frame counts (flags[7]) only when its CRC and
+// its end both verify.  Anything else (a false sync, a frame the producer would hand to the one-lane decoder) sets
+// flags[6], and the host runs the span check, chain and the non-optimistic decoder after all.
+template <bool OPT = false>
 __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob, const int64_t *soff, int ns,
                                                            const int64_t *poff, const int64_t *cpos,
                                                            const int64_t *ends, const int64_t *fbase,
                                                            const int64_t *frame_cand, int64_t nframes, int channels,
                                                            int stream_bps, int32_t *pcm, int blocksize, int *nvalid,
-                                                           DecOut dout) {
+                                                           DecOut dout, const int *ncand = nullptr,
+                                                           int *flags = nullptr) {
     __shared__ uint32_t stage[kDecStageWords + 2 * kRiceWinQ + 4];  // + the window step's look-ahead words
     __shared__ int32_t resbuf[kDecResMax];
     __shared__ PipeInfo info;
+    __shared__ __attribute__((aligned(16))) uint16_t ct4[OPT ? 4 : 1][256];  // slice-by-4 CRC-16 tables (OPT)
     // restored samples as int16 pairs + the producer's Rice-window jump tables (window + fixed points); a frame
     // that falls back to the one-lane decoder under a fused decode is decoded into `fb` instead (same bytes)
     union PipeU {
@@ -1799,10 +1812,34 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     const int64_t fi = blockIdx.x;
     if (fi >= nframes) return;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t ci = frame_cand[fi];
-    if (ci < 0 || ends[ci] < 0) return;  // not on a verified chain (the host reports it)
-    const int64_t fpos = cpos[ci], fend_known = ends[ci];
-    const int s = stream_of(soff, ns, fpos);
+    int64_t fpos, fend_known;
+    int s;
+    if constexpr (OPT) {
+        int lo = 0, hi = ns - 1;  // stream of frame fi
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (fbase[mid] <= fi) lo = mid;
+            else hi = mid - 1;
+        }
+        s = lo;
+        bool okmap = *ncand == (int)nframes;
+        fpos = okmap ? cpos[fi] : 0;
+        fend_known = okmap ? (fi + 1 < fbase[s + 1] ? cpos[fi + 1] : soff[s + 1]) : 0;
+        okmap = okmap && fpos >= soff[s] && (fi != fbase[s] || fpos == soff[s]) && fend_known > fpos &&
+                fend_known <= soff[s + 1];
+        if (!okmap) {
+            if (threadIdx.x == 0) atomicOr(&flags[6], 1);
+            return;
+        }
+        for (int k = threadIdx.x; k < 128; k += 128)
+            reinterpret_cast<uint4 *>(&ct4[0][0])[k] = reinterpret_cast<const uint4 *>(&d_crc16x4[0][0])[k];
+    } else {
+        const int64_t ci = frame_cand[fi];
+        if (ci < 0 || ends[ci] < 0) return;  // not on a verified chain (the host reports it)
+        fpos = cpos[ci];
+        fend_known = ends[ci];
+        s = stream_of(soff, ns, fpos);
+    }
     const int64_t send = soff[s + 1];
     const int64_t wb = fpos >> 2, we = (fend_known + 3) >> 2;
     const bool staged = we - wb <= kDecStageWords;
@@ -1843,6 +1880,11 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                 if (st) lds_publish(&vi->state, st);
             }
         };
+        if (OPT && !staged) {  // (the one-lane decoder needs the verified chain)
+            if (lane == 0) atomicOr(&flags[6], 1);
+            finish(kPipeError, 0);
+            return;
+        }
         if (!staged) {
             finish(kPipeFallback, 0);
             if (lane == 0)
@@ -1870,6 +1912,11 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
         }
         const int sbps = __builtin_amdgcn_readfirstlane(cd.bps) - w;
         auto fallback = [&]() {
+            if (OPT) {
+                if (lane == 0) atomicOr(&flags[6], 1);
+                finish(kPipeError, 0);
+                return;
+            }
             finish(kPipeFallback, 0);
             for (int64_t k = lane; k < we - wb + 4; k += 64) stage[k] = __builtin_bswap32(stage[k]);  // back to LE
             __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -1886,7 +1933,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
             const int32_t v = br.sbits(sbps);
             for (int i = lane; i < bs; i += 64) put(i, (int32_t)((uint32_t)v << w));
             const int ok = end_ok();
-            if (ok && lane == 0) atomicAdd(nvalid, 1);
+            if (!OPT && ok && lane == 0) atomicAdd(nvalid, 1);
             finish(kPipeDone, ok);
             return;
         }
@@ -1904,7 +1951,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
             }
             br.seek(Pe);
             const int ok = end_ok();
-            if (ok && lane == 0) atomicAdd(nvalid, 1);
+            if (!OPT && ok && lane == 0) atomicAdd(nvalid, 1);
             finish(kPipeDone, ok);
             return;
         }
@@ -2093,9 +2140,37 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
         return;
     }
     // ================= consumer (wave 1): LPC / FIXED restore behind the producer
+    bool crc_ok = true;
+    if constexpr (OPT) {
+        // CRC-16 of the span [fpos, fend) over the staged big-endian words (bytes outside it zeroed: leading zeros
+        // leave a CRC from 0 unchanged, trailing ones multiply it by x^8, which is invertible mod P) == 0
+        const int nw = (int)(we - wb), cw = (nw + 63) / 64;
+        const int a = min(nw, lane * cw), b = min(nw, a + cw);
+        uint32_t c = 0;
+        for (int k = a; k < b; k++) {
+            const int64_t byte0 = 4 * (wb + k);
+            const int lo = (int)min<int64_t>(4, max<int64_t>(0, fpos - byte0));
+            const int hi = (int)min<int64_t>(4, max<int64_t>(0, fend_known - byte0));
+            const uint32_t m1 = lo >= 4 ? 0u : (0xFFFFFFFFu >> (8 * lo)), m2 = hi <= 0 ? 0u : (0xFFFFFFFFu << (8 * (4 - hi)));
+            const uint32_t w = stage[k] & m1 & m2;
+            c = (uint32_t)ct4[3][((c >> 8) ^ (w >> 24)) & 0xFF] ^ ct4[2][((c & 0xFF) ^ ((w >> 16) & 0xFF)) & 0xFF] ^
+                ct4[1][(w >> 8) & 0xFF] ^ ct4[0][w & 0xFF];
+        }
+        c = crc_xpow(c, 4u * (uint32_t)(nw - b));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c ^= (uint32_t)__shfl_xor((int)c, o);
+        crc_ok = c == 0;
+    }
     int st;
     while ((st = lds_poll(&vi->state)) == 0) __builtin_amdgcn_s_sleep(1);
-    if (st != kPipeRestore) return;  // handled by the producer
+    if (st != kPipeRestore) {  // handled by the producer
+        if constexpr (OPT) {
+            while (lds_poll(&vi->finished) == 0) __builtin_amdgcn_s_sleep(1);
+            __asm__ volatile("" ::: "memory");
+            if (st == kPipeDone && info.valid && crc_ok && lane == 0) atomicAdd(&flags[7], 1);
+        }
+        return;
+    }
     const int o = info.o, shift = info.shift, w = info.w, bs = info.bs;
     // coefficient pairs C[k] = (c[2k+1] << 16 | c[2k] & 0xffff): dot2 with history pair H[k] = (x[i-2k-2], x[i-2k-1])
     uint32_t C[4], H[4] = {0, 0, 0, 0};
@@ -2160,23 +2235,57 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     const int head = min(bs, (o + 63) & ~63);
     generic(o, head);
     int i = head;
-    // whole 64-sample groups, fully unrolled: residual j of the group by v_readlane with an immediate lane index,
-    // no per-sample branches or scalar index arithmetic
-    for (; !failed && i + 64 <= bs; i += 64) {
-        if (!wait_for(i + 64)) {
-            failed = true;
-            break;
-        }
-        const int vr = resbuf[i + lane];
+    // whole 64-sample groups, fully unrolled, two samples per step on pair-aligned history: Q[m] = (x[2m+1] << 16 |
+    // x[2m] & 0xffff), the output layout, in a four-register ring renamed by the unroll (no per-sample shifting of the
+    // history).  x[2m] = r + (sum_k dot2(Q[m-1-k], C'[k]) >> shift), C'[k] = (q[2k] << 16 | q[2k+1]); x[2m+1] adds
+    // q[0] x[2m] to dot2s of the same pairs against D'[k] = (q[2k+1] << 16 | q[2k+2]).  Residual j of the group by
+    // v_readlane with an immediate lane index.  (Per sample ~8.5 instructions instead of ~12: the lone consumer wave
+    // issues one every ~8 cycles.)
+    if (!failed && i + 64 <= bs) {
+        auto pk = [](int32_t hi, int32_t lo) { return ((uint32_t)hi << 16) | ((uint32_t)lo & 0xFFFFu); };
+        const int32_t q0 = info.cq[0];
+        uint32_t Ce[4], Co[4], Qr[4];
 #pragma unroll
-        for (int j = 0; j < 64; j++) restore(__builtin_amdgcn_readlane(vr, j), i + j, (j & 1) != 0);
+        for (int k = 0; k < 4; k++) {
+            Ce[k] = pk(info.cq[2 * k], info.cq[2 * k + 1]);
+            Co[k] = pk(info.cq[2 * k + 1], k < 3 ? info.cq[2 * k + 2] : 0);
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // the head's pairs are in xout
+#pragma unroll
+        for (int k = 0; k < 4; k++) Qr[3 - k] = i ? xout[(i >> 1) - 1 - k] : 0u;  // Qr[3] = Q[m-1] .. Qr[0] = Q[m-4]
+        for (; i + 64 <= bs; i += 64) {
+            if (!wait_for(i + 64)) {
+                failed = true;
+                break;
+            }
+            const int vr = resbuf[i + lane];
+#pragma unroll
+            for (int p2 = 0; p2 < 32; p2++) {
+                const uint32_t A = Qr[(p2 + 3) & 3], B = Qr[(p2 + 2) & 3], Cc = Qr[(p2 + 1) & 3], Dd = Qr[p2 & 3];
+                int32_t pe = dec_dot2(Dd, Ce[3], 0);
+                pe = dec_dot2(Cc, Ce[2], pe);
+                pe = dec_dot2(B, Ce[1], pe);
+                int32_t po = dec_dot2(Dd, Co[3], 0);
+                po = dec_dot2(Cc, Co[2], po);
+                po = dec_dot2(B, Co[1], po);
+                po = dec_dot2(A, Co[0], po);
+                pe = dec_dot2(A, Ce[0], pe);
+                const int32_t xe = __builtin_amdgcn_readlane(vr, 2 * p2) + (pe >> shift);
+                const int32_t xo = __builtin_amdgcn_readlane(vr, 2 * p2 + 1) + ((po + q0 * xe) >> shift);
+                const uint32_t qn = __builtin_amdgcn_perm((uint32_t)xo, (uint32_t)xe, 0x05040100u);
+                xout[(i >> 1) + p2] = qn;
+                Qr[p2 & 3] = qn;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) H[k] = __builtin_amdgcn_alignbit(Qr[3 - k], Qr[3 - k], 16);  // for the tail
     }
     if (!failed && i < bs) generic(i, bs);
     if (!failed && (bs & 1)) xout[bs >> 1] = H[0] & 0xFFFFu;
     while (lds_poll(&vi->finished) == 0) __builtin_amdgcn_s_sleep(1);
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_wave_barrier();
-    if (failed || !info.valid) return;
+    if (failed || !info.valid || !crc_ok) return;
     const int16_t *x16 = reinterpret_cast<const int16_t *>(xout);
     const int dt = fused ? dout.dtype : -1;
     if ((dt == FRS_DT_I16 || dt == FRS_DT_U16 || dt == FRS_DT_U8) && dout.shift == 0 && (obase & 7) == 0 &&
@@ -2211,7 +2320,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     } else {
         for (int i = lane; i < bs; i += 64) put(i, (int32_t)((uint32_t)(int32_t)x16[i] << w));
     }
-    if (lane == 0) atomicAdd(nvalid, 1);
+    if (lane == 0) atomicAdd(OPT ? &flags[7] : nvalid, 1);
 }
 
 // One wave per frame: the frame's bytes are staged in LDS by the whole wave (coalesced dword loads), then lane 0
@@ -2931,7 +3040,7 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     const size_t tab = sizeof(int64_t) * (size_t)(nstreams + 1);
     const size_t dn_bytes = fused ? sizeof(float2) * (size_t)nstreams : 0;
     FRS_HIP(ctx->dec_soff.ensure(3 * tab + dn_bytes + sizeof(int64_t) * frames + 64));
-    FRS_HIP(ctx->pin.ensure(3 * tab + dn_bytes + 96));
+    FRS_HIP(ctx->pin.ensure(3 * tab + dn_bytes + 128));
     int64_t *htab = ctx->pin.at<int64_t>(0);
     memcpy(htab, stream_off, tab);
     memcpy(htab + (nstreams + 1), fbase.data(), tab);
@@ -3015,6 +3124,35 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         }
     }
     prof_end(ctx, "decode", ev);
+    DecOut dout;
+    dout.out = out_dev;
+    dout.dn = ddn;
+    dout.dtype = out_dtype;
+    dout.shift = bps > 16 ? 16 : 0;
+    int *hv = reinterpret_cast<int *>(reinterpret_cast<char *>(htab) + ((3 * tab + dn_bytes + 15) & ~(size_t)15));
+    // small mono ranges (C5 queries): the optimistic pipe decode first (no span check, no chain); only when it
+    // declined (counts[6]: a false sync, a frame for the one-lane decoder) do the span check, chain and decode below
+    // run, after one more host round trip.  FRS_PIPE_OPT=0 disables it (tests)
+    const char *opt_env = getenv("FRS_PIPE_OPT");
+    const bool pipe_opt = pipe && !lane && max_frame < (int64_t)4096 * 256 && !(opt_env && atoi(opt_env) == 0);
+    if (pipe_opt) {
+        prof_begin(ctx, "decode_frames", &ev);
+        k_decode_frames_pipe<true><<<(unsigned)frames, 128, 0, st>>>(blob_dev, dsoff, nstreams, dpoff, cpos, ends,
+                                                                     dfbase, dchain, frames, channels, bps, pcm_dev,
+                                                                     blocksize, nvalid, dout, ncand, ncand);
+        prof_end(ctx, "decode_frames", ev);
+        FRS_HIP(hipGetLastError());
+        FRS_HIP(hipMemcpyAsync(hv, ncand, sizeof(int) * 8, hipMemcpyDeviceToHost, st));
+        FRS_HIP(hipStreamSynchronize(st));
+        if (hv[6] == 0) {
+            prof_collect(ctx);
+            if (hv[7] != frames) {
+                ctx->err = "decoded " + std::to_string(hv[7]) + " valid frames, expected " + std::to_string(frames);
+                return FRS_E_CORRUPT;
+            }
+            return FRS_OK;
+        }
+    }
     prof_begin(ctx, "decode_span", &ev);
     // launched before the host knows the candidate count (no mid-query sync): an upper-bound grid strides over
     // *ncand on the device; an overflowing selection makes every later kernel a no-op and is reported below
@@ -3037,12 +3175,7 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     k_chain_lds<<<nstreams, nstreams == 1 ? 1024 : 64, 0, st>>>(dsoff, nstreams, cpos, ncand, (int)cand_cap, nexti,
                                                                  dfbase, dchain, bad);
     prof_end(ctx, "decode_span", ev);
-    DecOut dout;
-    dout.out = out_dev;
-    dout.dn = ddn;
-    dout.dtype = out_dtype;
-    dout.shift = bps > 16 ? 16 : 0;
-    prof_begin(ctx, "decode_frames", &ev);
+    prof_begin(ctx, pipe_opt ? "decode_fallback" : "decode_frames", &ev);
     if (lane) {
         FRS_HIP(ctx->dec_fb.ensure(sizeof(int32_t) * (size_t)frames + 64));
         int32_t *fbl = ctx->dec_fb.as<int32_t>();
@@ -3092,10 +3225,9 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         k_decode_frames_wave<<<(unsigned)frames, 64, 0, st>>>(blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase,
                                                               dchain, frames, channels, bps, pcm_dev, blocksize, nvalid,
                                                               dout);
-    prof_end(ctx, "decode_frames", ev);
+    prof_end(ctx, pipe_opt ? "decode_fallback" : "decode_frames", ev);
     FRS_HIP(hipGetLastError());
-    int *hv = reinterpret_cast<int *>(reinterpret_cast<char *>(htab) + ((3 * tab + dn_bytes + 15) & ~(size_t)15));
-    FRS_HIP(hipMemcpyAsync(hv, ncand, sizeof(int) * 4, hipMemcpyDeviceToHost, st));
+    FRS_HIP(hipMemcpyAsync(hv, ncand, sizeof(int) * 8, hipMemcpyDeviceToHost, st));
     FRS_HIP(hipStreamSynchronize(st));
     prof_collect(ctx);
     if (ctx->prof && (lane || mcl)) {  // frames the lane decoder handed to the wave decoder (profile_avg_ms of this name)
@@ -3108,8 +3240,9 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
                    "): not a FLAC stream of the expected layout";
         return FRS_E_CORRUPT;
     }
-    if (hv[2] != 0 || hv[1] != frames) {
-        ctx->err = "decoded " + std::to_string(hv[1]) + " valid frames, expected " + std::to_string(frames) +
+    const int valid = hv[1];
+    if (hv[2] != 0 || valid != frames) {
+        ctx->err = "decoded " + std::to_string(valid) + " valid frames, expected " + std::to_string(frames) +
                    (hv[2] ? " (broken frame chain)" : "");
         return FRS_E_CORRUPT;
     }

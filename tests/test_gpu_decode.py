@@ -47,7 +47,9 @@ def _bands():
             ("flat", flat, 256), ("spiky", spiky, 256), ("u8", u8, 200)]
 
 
-DECODERS = {"pipe": {"FRS_DECODE_LANE": "0"},      # two-wave pipelined decoder (latency; C5 queries)
+DECODERS = {"pipe": {"FRS_DECODE_LANE": "0"},      # two-wave pipelined decoder (latency; C5 queries), optimistic:
+            #                                       candidates = frames, CRC-16 checked inside the decoder
+            "pipe_chain": {"FRS_DECODE_LANE": "0", "FRS_PIPE_OPT": "0"},  # the same after the span check + chain
             "lane": {"FRS_DECODE_LANE": "1"},      # lane-per-frame decoder (throughput; batched decodes)
             "wave": {"FRS_FORCE_GENERIC": "1"}}    # one-lane wave decoder (any layout)
 
