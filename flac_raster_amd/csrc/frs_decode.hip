@@ -1768,6 +1768,7 @@ struct PipeInfo {
     int32_t progress;    // residuals published in resbuf (samples [o, progress) are ready)
     int32_t valid;       // producer's verdict at the end: 1 = frame ends at its CRC footer
     int32_t finished;    // producer done (valid final)
+    int32_t crc_ok;      // OPT: the span's CRC-16 verifies (set before finished)
     int32_t o, shift, w, bs;
     int32_t cq[8];
     int32_t wu[8];
@@ -1794,7 +1795,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                                                            DecOut dout, const int *ncand = nullptr,
                                                            int *flags = nullptr) {
     __shared__ uint32_t stage[kDecStageWords + 2 * kRiceWinQ + 4];  // + the window step's look-ahead words
-    __shared__ int32_t resbuf[kDecResMax];
+    __shared__ __attribute__((aligned(16))) int32_t resbuf[kDecResMax];
     __shared__ PipeInfo info;
     __shared__ __attribute__((aligned(16))) uint16_t ct4[OPT ? 4 : 1][256];  // slice-by-4 CRC-16 tables (OPT)
     // restored samples as int16 pairs + the producer's Rice-window jump tables (window + fixed points); a frame
@@ -1850,6 +1851,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
         info.progress = 0;
         info.finished = 0;
         info.valid = 0;
+        info.crc_ok = 0;
     }
     __syncthreads();
     const int64_t nsamp = poff[s + 1] - poff[s];
@@ -1873,7 +1875,32 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     volatile PipeInfo *vi = &info;
     if (wave == 0) {
         // ================= producer: parse + Rice decode (wave-uniform, scalar unit)
+        // OPT: CRC-16 of the span [fpos, fend) over the staged big-endian words (bytes outside it zeroed: leading
+        // zeros leave a CRC from 0 unchanged, trailing ones multiply it by x^8, invertible mod P) == 0 -- computed by
+        // this wave after its Rice windows (the consumer's restore is the decode's critical path)
+        auto span_crc = [&]() {
+            if constexpr (OPT) {
+                const int nw = (int)(we - wb), cw = (nw + 63) / 64;
+                const int a = min(nw, lane * cw), b = min(nw, a + cw);
+                uint32_t c = 0;
+                for (int k = a; k < b; k++) {
+                    const int64_t byte0 = 4 * (wb + k);
+                    const int lo = (int)min<int64_t>(4, max<int64_t>(0, fpos - byte0));
+                    const int hi = (int)min<int64_t>(4, max<int64_t>(0, fend_known - byte0));
+                    const uint32_t m1 = lo >= 4 ? 0u : (0xFFFFFFFFu >> (8 * lo));
+                    const uint32_t m2 = hi <= 0 ? 0u : (0xFFFFFFFFu << (8 * (4 - hi)));
+                    const uint32_t w = stage[k] & m1 & m2;
+                    c = (uint32_t)ct4[3][((c >> 8) ^ (w >> 24)) & 0xFF] ^ ct4[2][((c & 0xFF) ^ ((w >> 16) & 0xFF)) & 0xFF] ^
+                        ct4[1][(w >> 8) & 0xFF] ^ ct4[0][w & 0xFF];
+                }
+                c = crc_xpow(c, 4u * (uint32_t)(nw - b));
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) c ^= (uint32_t)__shfl_xor((int)c, o);
+                if (lane == 0) info.crc_ok = c == 0;
+            }
+        };
         auto finish = [&](int st, int valid) {
+            if (st == kPipeDone) span_crc();
             if (lane == 0) {
                 info.valid = valid;
                 lds_publish(&vi->finished, 1);
@@ -2013,8 +2040,8 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
         };
 #pragma unroll
         for (int k = 0; k < 6; k++) {  // jump-table entries past the window are fixed points
-            jt[k][kRiceWinBits + lane] = (uint16_t)(kRiceWinBits + lane);
-            jt[k][kRiceWinBits + 64 + lane] = (uint16_t)(kRiceWinBits + 64 + lane);
+            jt[k][kRiceWinBits + lane] = (uint16_t)(2 * (kRiceWinBits + lane));
+            jt[k][kRiceWinBits + 64 + lane] = (uint16_t)(2 * (kRiceWinBits + 64 + lane));
         }
         for (int p = 0; p < (1 << po) && !bad; p++) {
             br.seek(P);
@@ -2024,7 +2051,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                 const int nb = (int)br.bits(5);
                 for (int j = 0; j < left; j++, i++) {
                     const int32_t r = nb ? br.sbits(nb) : 0;
-                    if (lane == 0) resbuf[i] = r;
+                    if (lane == 0) resbuf[i] = (int32_t)((uint32_t)r << shift);
                 }
                 P = br.pos();
                 publish();
@@ -2056,16 +2083,25 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                 const uint64_t wB = ((uint64_t)stage[wi + 2] << 32) | stage[wi + 3];
                 // chain by pointer jumping: jt[k][c] = the code start 2^k codes after candidate c (absorbing at a
                 // long code and past the window), so lane m finds the m-th code start in six dependent LDS reads;
-                // the values are decoded after it, only at the chain's code starts
+                // the values are decoded after it, only at the chain's code starts.  Entries hold BYTE offsets into a
+                // row (2 c), so a lookup's address is the entry itself plus the row's immediate offset (no scaling)
                 const int cap = left < 64 ? left : 64;
                 int jq[kRiceWinQ];
+                {
+                    // the lane's 64 bits from its first candidate; candidate t's code ends k1 bits after the first set
+                    // bit at or after t: those first-set positions by a backward select chain over the top 16 bits
+                    // (one 64-bit clz for the rest) instead of a shift + clz per candidate.  A code whose stop bit
+                    // lies past these 64 bits is left absorbing (the chain's long-code path decodes it).
+                    const uint64_t X = sh ? (wA << sh) | (wB >> (64u - sh)) : wA;
+                    const uint64_t X16 = X << 16;
+                    int f = (X16 ? __builtin_clzll(X16) : 64) + 16;  // 80: no set bit in [16, 64)
+                    const uint32_t top = (uint32_t)(X >> 48);
+                    const int c0 = kRiceWinQ * lane;
 #pragma unroll
-                for (int t = 0; t < kRiceWinQ; t++) {
-                    const uint32_t s2 = sh + (uint32_t)t;  // < 64
-                    const uint64_t win = s2 ? (wA << s2) | (wB >> (64u - s2)) : wA;
-                    const int tot = (win ? __builtin_clzll(win) : 64) + k1;
-                    const int c = kRiceWinQ * lane + t;
-                    jq[t] = tot <= 64 ? c + tot : c;
+                    for (int t = kRiceWinQ - 1; t >= 0; t--) {
+                        f = ((top >> (15 - t)) & 1u) ? t : f;
+                        jq[t] = 2 * (f + k1 - t <= 64 ? c0 + f + k1 : c0 + t);
+                    }
                 }
                 auto store_run = [&](uint16_t *row) {  // jq -> row[kRiceWinQ * lane ...], 16 bytes at a time
 #pragma unroll
@@ -2082,33 +2118,37 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
 #pragma unroll
                 for (int k = 0; k < 5; k++) {
 #pragma unroll
-                    for (int q = 0; q < kRiceWinQ; q++) jq[q] = jt[k][jq[q]];
+                    for (int q = 0; q < kRiceWinQ; q++)
+                        jq[q] = *reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(jt[k]) + jq[q]);
                     store_run(jt[k + 1]);
                 }
-                int posv = 0;
+                auto jt_at = [&](int k, int byteoff) -> int {
+                    return *reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(jt[k]) + byteoff);
+                };
+                int posv = 0;  // (byte offset)
 #pragma unroll
                 for (int k = 0; k < 6; k++) {
-                    const int nx = jt[k][posv];
+                    const int nx = jt_at(k, posv);
                     posv = ((lane >> k) & 1) ? nx : posv;
                 }
-                const int nxt = jt[0][posv];
-                const uint64_t chain = __ballot(posv < kRiceWinBits && nxt != posv && lane < cap);  // lanes 0..cnt-1
+                const int nxt = jt_at(0, posv);
+                const uint64_t chain = __ballot(posv < 2 * kRiceWinBits && nxt != posv && lane < cap);  // lanes 0..cnt-1
                 const int cnt = __builtin_popcountll(chain);
                 int cur;
                 bool lng = false;
                 if (cnt < cap) {  // stopped at a long code (inside the window) or past the window
-                    cur = __builtin_amdgcn_readlane(posv, cnt);
+                    cur = __builtin_amdgcn_readlane(posv, cnt) >> 1;
                     lng = cur < kRiceWinBits;
                 } else {
-                    cur = __builtin_amdgcn_readlane(nxt, cnt - 1);
+                    cur = __builtin_amdgcn_readlane(nxt, cnt - 1) >> 1;
                 }
                 {
-                    const uint32_t bc = P + (uint32_t)posv, wc = bc >> 5;  // lane m: the m-th code of the window
+                    const uint32_t bc = P + (uint32_t)(posv >> 1), wc = bc >> 5;  // lane m: the m-th code of the window
                     const uint64_t win = window64(stage[wc], stage[wc + 1], stage[wc + 2], bc & 31u);
                     const int z = win ? __builtin_clzll(win) : 64;
                     const uint32_t low = kp ? (uint32_t)((win << (z + 1)) >> (64 - kp)) : 0u;
                     const uint32_t u = ((uint32_t)z << kp) | low;
-                    if (lane < cnt) resbuf[i + lane] = (int32_t)((u >> 1) ^ (uint32_t)(-(int32_t)(u & 1)));
+                    if (lane < cnt) resbuf[i + lane] = (int32_t)(((u >> 1) ^ (uint32_t)(-(int32_t)(u & 1))) << shift);
                 }
                 const int i0 = i;
                 i += cnt;
@@ -2122,7 +2162,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                         break;
                     }
                     const uint32_t uu = (q << kp) | br.bits(kp);
-                    if (lane == 0) resbuf[i] = (int32_t)((uu >> 1) ^ (uint32_t)(-(int32_t)(uu & 1)));
+                    if (lane == 0) resbuf[i] = (int32_t)(((uu >> 1) ^ (uint32_t)(-(int32_t)(uu & 1))) << shift);
                     i++;
                     left--;
                     P = br.pos();
@@ -2132,42 +2172,22 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
         }
         br.seek(P);  // the frame's end check reads br.pos()
         const int ok = !bad && end_ok();
+        if (lane == 0) lds_publish(&vi->progress, bad ? -1 : bs);
+        span_crc();
         if (lane == 0) {
             info.valid = ok;
-            lds_publish(&vi->progress, bad ? -1 : bs);
             lds_publish(&vi->finished, 1);
         }
         return;
     }
     // ================= consumer (wave 1): LPC / FIXED restore behind the producer
-    bool crc_ok = true;
-    if constexpr (OPT) {
-        // CRC-16 of the span [fpos, fend) over the staged big-endian words (bytes outside it zeroed: leading zeros
-        // leave a CRC from 0 unchanged, trailing ones multiply it by x^8, which is invertible mod P) == 0
-        const int nw = (int)(we - wb), cw = (nw + 63) / 64;
-        const int a = min(nw, lane * cw), b = min(nw, a + cw);
-        uint32_t c = 0;
-        for (int k = a; k < b; k++) {
-            const int64_t byte0 = 4 * (wb + k);
-            const int lo = (int)min<int64_t>(4, max<int64_t>(0, fpos - byte0));
-            const int hi = (int)min<int64_t>(4, max<int64_t>(0, fend_known - byte0));
-            const uint32_t m1 = lo >= 4 ? 0u : (0xFFFFFFFFu >> (8 * lo)), m2 = hi <= 0 ? 0u : (0xFFFFFFFFu << (8 * (4 - hi)));
-            const uint32_t w = stage[k] & m1 & m2;
-            c = (uint32_t)ct4[3][((c >> 8) ^ (w >> 24)) & 0xFF] ^ ct4[2][((c & 0xFF) ^ ((w >> 16) & 0xFF)) & 0xFF] ^
-                ct4[1][(w >> 8) & 0xFF] ^ ct4[0][w & 0xFF];
-        }
-        c = crc_xpow(c, 4u * (uint32_t)(nw - b));
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) c ^= (uint32_t)__shfl_xor((int)c, o);
-        crc_ok = c == 0;
-    }
     int st;
     while ((st = lds_poll(&vi->state)) == 0) __builtin_amdgcn_s_sleep(1);
     if (st != kPipeRestore) {  // handled by the producer
         if constexpr (OPT) {
             while (lds_poll(&vi->finished) == 0) __builtin_amdgcn_s_sleep(1);
             __asm__ volatile("" ::: "memory");
-            if (st == kPipeDone && info.valid && crc_ok && lane == 0) atomicAdd(&flags[7], 1);
+            if (st == kPipeDone && info.valid && info.crc_ok && lane == 0) atomicAdd(&flags[7], 1);
         }
         return;
     }
@@ -2195,12 +2215,14 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     bool failed = false;
     // one sample of the recurrence: x = r + (sum q.x >> shift), the four dot2 over (newest, older) pairs with the
     // oldest pairs first so only the last one waits on x[i-1]; the history pairs then shift by one sample
-    auto restore = [&](int32_t r, int i, bool odd) {
-        int32_t pred = dec_dot2(H[3], C[3], 0);
+    // (residuals arrive pre-shifted, R = r << shift: x = (R + sum q.x) >> shift, exact in wrapping int32 for
+    // shift <= 15 and a 16-bit x)
+    auto restore = [&](int32_t R, int i, bool odd) {
+        int32_t pred = dec_dot2(H[3], C[3], R);
         pred = dec_dot2(H[2], C[2], pred);
         pred = dec_dot2(H[1], C[1], pred);
         pred = dec_dot2(H[0], C[0], pred);
-        const int32_t x = r + (pred >> shift);
+        const int32_t x = pred >> shift;
         H[3] = __builtin_amdgcn_alignbit(H[3], H[2], 16);
         H[2] = __builtin_amdgcn_alignbit(H[2], H[1], 16);
         H[1] = __builtin_amdgcn_alignbit(H[1], H[0], 16);
@@ -2258,22 +2280,28 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                 failed = true;
                 break;
             }
-            const int vr = resbuf[i + lane];
+            int4 rr = make_int4(0, 0, 0, 0);
+            const int4 *rp = reinterpret_cast<const int4 *>(&resbuf[i]);  // (base pointers: immediate ds offsets)
+            uint32_t *xp = xout + (i >> 1);
 #pragma unroll
             for (int p2 = 0; p2 < 32; p2++) {
+                // four (pre-shifted) residuals at a time, every lane reading the same 16 bytes: they arrive in VGPRs
+                // and seed the dot2 accumulators (no per-sample v_readlane + v_mov)
+                if (!(p2 & 1)) rr = rp[p2 >> 1];
+                const int32_t Re = (p2 & 1) ? rr.z : rr.x, Ro = (p2 & 1) ? rr.w : rr.y;
                 const uint32_t A = Qr[(p2 + 3) & 3], B = Qr[(p2 + 2) & 3], Cc = Qr[(p2 + 1) & 3], Dd = Qr[p2 & 3];
-                int32_t pe = dec_dot2(Dd, Ce[3], 0);
+                int32_t pe = dec_dot2(Dd, Ce[3], Re);
                 pe = dec_dot2(Cc, Ce[2], pe);
                 pe = dec_dot2(B, Ce[1], pe);
-                int32_t po = dec_dot2(Dd, Co[3], 0);
+                int32_t po = dec_dot2(Dd, Co[3], Ro);
                 po = dec_dot2(Cc, Co[2], po);
                 po = dec_dot2(B, Co[1], po);
                 po = dec_dot2(A, Co[0], po);
                 pe = dec_dot2(A, Ce[0], pe);
-                const int32_t xe = __builtin_amdgcn_readlane(vr, 2 * p2) + (pe >> shift);
-                const int32_t xo = __builtin_amdgcn_readlane(vr, 2 * p2 + 1) + ((po + q0 * xe) >> shift);
+                const int32_t xe = pe >> shift;
+                const int32_t xo = (__mul24(q0, xe) + po) >> shift;
                 const uint32_t qn = __builtin_amdgcn_perm((uint32_t)xo, (uint32_t)xe, 0x05040100u);
-                xout[(i >> 1) + p2] = qn;
+                xp[p2] = qn;
                 Qr[p2 & 3] = qn;
             }
         }
@@ -2285,7 +2313,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     while (lds_poll(&vi->finished) == 0) __builtin_amdgcn_s_sleep(1);
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_wave_barrier();
-    if (failed || !info.valid || !crc_ok) return;
+    if (failed || !info.valid || (OPT && !info.crc_ok)) return;
     const int16_t *x16 = reinterpret_cast<const int16_t *>(xout);
     const int dt = fused ? dout.dtype : -1;
     if ((dt == FRS_DT_I16 || dt == FRS_DT_U16 || dt == FRS_DT_U8) && dout.shift == 0 && (obase & 7) == 0 &&
