@@ -349,34 +349,54 @@ def select_frame(index: Dict, tile_id: Optional[int] = None, last: bool = False,
     raise ValueError("Must specify --tile-id, --bbox, --center, or --last")
 
 
+_GRID_CACHE: List[Tuple[Dict, int, Optional[tuple]]] = []  # (index, len(frames), grid) of recently queried indexes
+
+
+def _grid_of(index: Dict) -> Optional[tuple]:
+    """The row-major tile grid of an index as create-streaming writes it (tile size, columns, rows, the transform's
+    scale/offset terms, the frames' bboxes as tuples), or None when the index is not that grid.  Derived once per
+    index object (a bbox query is latency-bound: the per-query dict walks cost more than the tests themselves)."""
+    frames = index["frames"]
+    for idx, n, g in _GRID_CACHE:
+        if idx is index and n == len(frames):
+            return g
+    T, W, H, t = index.get("tile_size"), index.get("width"), index.get("height"), index.get("transform")
+    g = None
+    if T and W and H and t and len(t) >= 6 and t[1] == 0 and t[3] == 0 and t[0] != 0 and t[4] != 0:
+        tc, tr = -(-int(W) // int(T)), -(-int(H) // int(T))
+        if len(frames) == tc * tr and all(fr["frame_id"] == k for k, fr in enumerate(frames)):
+            g = (int(T), tc, tr, float(t[0]), float(t[2]), float(t[4]), float(t[5]),
+                 [tuple(fr["bbox"]) for fr in frames])
+    _GRID_CACHE.insert(0, (index, len(frames), g))
+    del _GRID_CACHE[8:]
+    return g
+
+
 def first_intersecting(index: Dict, bbox: Sequence[float]) -> Optional[Dict]:
     """intersecting(index, bbox)[0] (cli.py:976-987) without the linear scan when the index is the
     row-major tile grid create-streaming writes: only tiles within one tile of the bbox's pixel footprint
     are tested, in index order, with the same strict inequalities on the stored bboxes."""
-    T, W, H, t = index.get("tile_size"), index.get("width"), index.get("height"), index.get("transform")
-    frames = index["frames"]
-    ok = bool(T and W and H and t and len(t) >= 6 and t[1] == 0 and t[3] == 0 and t[0] != 0 and t[4] != 0)
-    if ok:
-        tc, tr = -(-int(W) // int(T)), -(-int(H) // int(T))
-        ok = len(frames) == tc * tr
-    if not ok:
+    g = _grid_of(index)
+    if g is None:
         hits = intersecting(index, bbox)
         return hits[0] if hits else None
+    T, tc, tr, a, c, e, f, boxes = g
     x0, y0, x1, y1 = bbox
-    a, c, e, f = float(t[0]), float(t[2]), float(t[4]), float(t[5])
-    ca, cb = sorted(((x0 - c) / a, (x1 - c) / a))
-    ra, rb = sorted(((y0 - f) / e, (y1 - f) / e))
-    ct0, ct1 = max(0, int(math.floor(ca / T)) - 1), min(tc - 1, int(math.floor(cb / T)) + 1)
-    rt0, rt1 = max(0, int(math.floor(ra / T)) - 1), min(tr - 1, int(math.floor(rb / T)) + 1)
+    ca, cb = (x0 - c) / a, (x1 - c) / a
+    if cb < ca:
+        ca, cb = cb, ca
+    ra, rb = (y0 - f) / e, (y1 - f) / e
+    if rb < ra:
+        ra, rb = rb, ra
+    floor = math.floor
+    ct0, ct1 = max(0, floor(ca / T) - 1), min(tc - 1, floor(cb / T) + 1)
+    rt0, rt1 = max(0, floor(ra / T) - 1), min(tr - 1, floor(rb / T) + 1)
     for r in range(rt0, rt1 + 1):
+        k = r * tc
         for cc in range(ct0, ct1 + 1):
-            fr = frames[r * tc + cc]
-            if fr["frame_id"] != r * tc + cc:  # not the plain grid order: fall back to the scan
-                hits = intersecting(index, bbox)
-                return hits[0] if hits else None
-            b = fr["bbox"]
+            b = boxes[k + cc]
             if x0 < b[2] and x1 > b[0] and y0 < b[3] and y1 > b[1]:
-                return fr
+                return index["frames"][k + cc]
     return None
 
 
