@@ -311,8 +311,10 @@ __device__ __attribute__((noinline)) uint32_t sel_check_candidates(uint4 cur, ui
             }
             ok = header_ok_regs(h, min<int64_t>(nbytes - p, 16), channels);
         } else {
+            // (one stream: its end is the range end -- the single-stream latency path passes its tables as kernel
+            // arguments, so soff may not be in device memory yet)
             const int st = stream_of(soff, ns, p);
-            ok = parse_header(blob, p, soff[st + 1], channels, stream_bps).ok;
+            ok = parse_header(blob, p, ns == 1 ? nbytes : soff[st + 1], channels, stream_bps).ok;
         }
         if (ok) mask |= 1u << j;
     }
@@ -461,15 +463,22 @@ __device__ inline void sel_emit_co(const uint32_t *m, int64_t qw, int lane, int 
     }
 }
 
+// One stream (a bbox query's tile): its call tables [soff | fbase | poff | (max - min, min)] ride in the kernel
+// arguments and block 0 writes them to `tabdst` for the later kernels (no host-to-device copy per query)
+struct SmallTabs {
+    int64_t v[7];
+};
 template <int STEPS>
 __global__ void __launch_bounds__(kSelThreads) k_sync_select(const uint8_t *blob, int64_t nbytes, const int64_t *soff,
                                                            int ns, int channels, int stream_bps, uint64_t *status,
                                                            unsigned long long *ticket, uint32_t epoch, int64_t nblocks,
-                                                           int64_t *cpos, int64_t cap, int *counts) {
+                                                           int64_t *cpos, int64_t cap, int *counts,
+                                                           int64_t *tabdst = nullptr, SmallTabs tabs = {}) {
     constexpr int kSelSteps = STEPS, kSelBytes = STEPS * 1024 * (kSelThreads / 64);
     __shared__ int64_t s_ord, s_base;
     __shared__ int s_wsum[kSelThreads / 64];
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (tabdst && blockIdx.x == 0 && t < 7) tabdst[t] = tabs.v[t];
     if (t == 0) {
         const int64_t o = (int64_t)atomicAdd(ticket, 1ull);
         if (o == nblocks - 1) atomicExch(ticket, 0ull);  // every ticket of this launch is drawn: re-arm
@@ -1780,6 +1789,18 @@ __device__ inline void lds_publish(volatile int32_t *p, int32_t v) {
 }
 __device__ inline int32_t lds_poll(volatile int32_t *p) { return *p; }
 
+// OPT: the last work-group to finish (flags[8] counts them; re-armed to 0) copies the call's counters flags[0..7] to
+// page-locked host memory, so the host reads them after its stream synchronisation without a device-to-host copy
+__device__ inline void pipe_wg_exit(int *flags, int64_t nframes, int *hout) {
+    __threadfence();
+    const int t = atomicAdd(&flags[8], 1);
+    if (t == (int)nframes - 1) {
+        flags[8] = 0;
+        __threadfence();
+        for (int k = 0; k < 8; k++) hout[k] = __hip_atomic_load(&flags[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence_system();
+    }
+}
 // OPT (small ranges, launched right after the selection): the optimistic form -- when the selection found exactly
 // one candidate per frame and each stream's first at its first byte, frame i IS candidate i and its span ends at
 // candidate i + 1 (or the stream end), so the span check and the chain are skipped: the consumer wave checks the
@@ -1793,7 +1814,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                                                            const int64_t *frame_cand, int64_t nframes, int channels,
                                                            int stream_bps, int32_t *pcm, int blocksize, int *nvalid,
                                                            DecOut dout, const int *ncand = nullptr,
-                                                           int *flags = nullptr) {
+                                                           int *flags = nullptr, int *hout = nullptr) {
     __shared__ uint32_t stage[kDecStageWords + 2 * kRiceWinQ + 4];  // + the window step's look-ahead words
     __shared__ __attribute__((aligned(16))) int32_t resbuf[kDecResMax];
     __shared__ PipeInfo info;
@@ -1829,7 +1850,12 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
         okmap = okmap && fpos >= soff[s] && (fi != fbase[s] || fpos == soff[s]) && fend_known > fpos &&
                 fend_known <= soff[s + 1];
         if (!okmap) {
-            if (threadIdx.x == 0) atomicOr(&flags[6], 1);
+            if (threadIdx.x == 0) {
+                atomicOr(&flags[6], 1);
+                __threadfence();
+            }
+            __syncthreads();
+            if (threadIdx.x == 64) pipe_wg_exit(flags, nframes, hout);
             return;
         }
         for (int k = threadIdx.x; k < 128; k += 128)
@@ -1908,7 +1934,10 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
             }
         };
         if (OPT && !staged) {  // (the one-lane decoder needs the verified chain)
-            if (lane == 0) atomicOr(&flags[6], 1);
+            if (lane == 0) {
+                atomicOr(&flags[6], 1);
+                __threadfence();
+            }
             finish(kPipeError, 0);
             return;
         }
@@ -1940,7 +1969,10 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
         const int sbps = __builtin_amdgcn_readfirstlane(cd.bps) - w;
         auto fallback = [&]() {
             if (OPT) {
-                if (lane == 0) atomicOr(&flags[6], 1);
+                if (lane == 0) {
+                    atomicOr(&flags[6], 1);
+                    __threadfence();
+                }
                 finish(kPipeError, 0);
                 return;
             }
@@ -2188,6 +2220,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
             while (lds_poll(&vi->finished) == 0) __builtin_amdgcn_s_sleep(1);
             __asm__ volatile("" ::: "memory");
             if (st == kPipeDone && info.valid && info.crc_ok && lane == 0) atomicAdd(&flags[7], 1);
+            if (lane == 0) pipe_wg_exit(flags, nframes, hout);
         }
         return;
     }
@@ -2313,7 +2346,10 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     while (lds_poll(&vi->finished) == 0) __builtin_amdgcn_s_sleep(1);
     __builtin_amdgcn_s_waitcnt(0xC07F);
     __builtin_amdgcn_wave_barrier();
-    if (failed || !info.valid || (OPT && !info.crc_ok)) return;
+    if (failed || !info.valid || (OPT && !info.crc_ok)) {
+        if (OPT && lane == 0) pipe_wg_exit(flags, nframes, hout);
+        return;
+    }
     const int16_t *x16 = reinterpret_cast<const int16_t *>(xout);
     const int dt = fused ? dout.dtype : -1;
     if ((dt == FRS_DT_I16 || dt == FRS_DT_U16 || dt == FRS_DT_U8) && dout.shift == 0 && (obase & 7) == 0 &&
@@ -2348,7 +2384,10 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     } else {
         for (int i = lane; i < bs; i += 64) put(i, (int32_t)((uint32_t)(int32_t)x16[i] << w));
     }
-    if (lane == 0) atomicAdd(OPT ? &flags[7] : nvalid, 1);
+    if (lane == 0) {
+        atomicAdd(OPT ? &flags[7] : nvalid, 1);
+        if (OPT) pipe_wg_exit(flags, nframes, hout);
+    }
 }
 
 // One wave per frame: the frame's bytes are staged in LDS by the whole wave (coalesced dword loads), then lane 0
@@ -2432,6 +2471,7 @@ __global__ void __launch_bounds__(64) k_decode_frames_wave_list(const uint8_t *b
 // k_decode_frames_wave_list (which rewrites all of its samples).  A frame counts as valid when its
 // subframe ends exactly at the CRC-16 footer found by the span check.
 constexpr int kOutPcm = 0, kOutI16 = 1, kOutU16 = 2, kOutU8 = 3, kOutAny = 4;
+constexpr int kOutPlanar16 = 5;  // raw 16-bit PCM (the multi-channel planar scratch of >= 3 independent channels)
 
 struct LaneReader {
     const uint8_t *abase;  // blob aligned down to 16 bytes; chunk q covers abase[q, q + 16)
@@ -2571,6 +2611,8 @@ template <int OUT>
 __device__ inline uint32_t dn_bits_t(const DecOut &o, int32_t pcm, float2 p) {
     if constexpr (OUT == kOutPcm) {
         return (uint32_t)pcm;
+    } else if constexpr (OUT == kOutPlanar16) {
+        return (uint32_t)pcm & 0xFFFFu;
     } else {
         const float v = (float)(pcm >> o.shift) * (1.0f / 32768.0f);
         float a = __fadd_rn(v, 1.0f);
@@ -2592,7 +2634,7 @@ __device__ inline uint32_t dn_bits_t(const DecOut &o, int32_t pcm, float2 p) {
 // libFLAC's stereo decorrelation here -- left-side R = L - S, right-side L = R + S, mid-side from (M << 1 | S & 1).
 __global__ void __launch_bounds__(256) k_interleave_dn(const int32_t *planar, const int64_t *poff, const int64_t *fbase,
                                                       int ns, int nch, int blocksize, int32_t *pcm, DecOut dout,
-                                                      const int8_t *fchass, int cpf) {
+                                                      const int8_t *fchass, int cpf, int planar16) {
     const int64_t fi = blockIdx.x / (unsigned)cpf;
     const int i = (int)(blockIdx.x - fi * cpf) * 256 + (int)threadIdx.x;  // sample position in the frame
     if (i >= blocksize) return;
@@ -2604,10 +2646,16 @@ __global__ void __launch_bounds__(256) k_interleave_dn(const int32_t *planar, co
     }
     const int64_t g = poff[lo] + (fi - fbase[lo]) * blocksize + i;  // sample index
     if (g >= poff[lo + 1]) return;
-    const int32_t *src = planar + fi * nch * (int64_t)blocksize + i;
     int32_t x[8];
+    if (planar16) {  // (>= 3 independent 16-bit channels: half the scratch bytes)
+        const int16_t *src = reinterpret_cast<const int16_t *>(planar) + fi * nch * (int64_t)blocksize + i;
 #pragma unroll
-    for (int c = 0; c < 8; c++) x[c] = c < nch ? src[(int64_t)c * blocksize] : 0;
+        for (int c = 0; c < 8; c++) x[c] = c < nch ? src[(int64_t)c * blocksize] : 0;
+    } else {
+        const int32_t *src = planar + fi * nch * (int64_t)blocksize + i;
+#pragma unroll
+        for (int c = 0; c < 8; c++) x[c] = c < nch ? src[(int64_t)c * blocksize] : 0;
+    }
     if (fchass) {
         const int ca = fchass[fi];
         const int64_t a = x[0], sd = x[1];
@@ -2656,13 +2704,13 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
                                                            DecOut dout, int32_t *fb_list, int *fb_count,
                                                            int nch = 1, int32_t *planar = nullptr,
                                                            int8_t *fchass = nullptr) {
-    static_assert(!MC || OUT == kOutPcm, "channel-planar int32 output");
+    static_assert(!MC || OUT == kOutPcm || OUT == kOutPlanar16, "channel-planar int32 / int16 output");
     constexpr int es = OUT == kOutPcm ? 4 : OUT == kOutU8 ? 1 : 2;  // kOutAny: per-sample dn_store
     // 1- and 2-byte outputs: a lane's aligned 8-sample groups are staged in LDS (slot-major: every ds op of the wave
     // is one contiguous 1 KB) and leave 8 groups at a time, i.e. a whole 128-byte line (64 B for bytes) as back-to-back
     // stores -- one 16-byte store per step to 64 different lines had the L2 write each line back several times
     // (PMC: 5x the output bytes written)
-    constexpr bool kStage = OUT == kOutI16 || OUT == kOutU16 || OUT == kOutU8;
+    constexpr bool kStage = OUT == kOutI16 || OUT == kOutU16 || OUT == kOutU8 || OUT == kOutPlanar16;
     __shared__ uint4 ostage[kStage ? 4 : 1][kStage ? 8 : 1][kStage ? 64 : 1];
     const int64_t fi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint8_t *obytes = MC ? reinterpret_cast<uint8_t *>(planar)
@@ -2684,7 +2732,7 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
             if (MC && fchass && cd.ok) fchass[fi] = (int8_t)cd.chass;
             if (cd.ok && cd.frame_no == kk && cd.bs <= blocksize && first + cd.bs <= nsamp && take_all) {
                 const int bs = cd.bs;
-                const float2 dnp = OUT != kOutPcm ? dout.dn[s] : make_float2(0.f, 0.f);
+                const float2 dnp = OUT != kOutPcm && OUT != kOutPlanar16 ? dout.dn[s] : make_float2(0.f, 0.f);
                 LaneReader br;
                 br.init(blob, fpos + cd.hdr_len, send);
                 for (int chn = 0; chn < (MC ? nch : 1) && take_all; chn++) {
@@ -3076,7 +3124,14 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     float2 *hdn = reinterpret_cast<float2 *>(htab + 3 * (nstreams + 1));
     if (fused)  // python-float arithmetic first (data_max - data_min in double), then NEP 50 casts to float32
         for (int s = 0; s < nstreams; s++) hdn[s] = make_float2((float)(dmax[s] - dmin[s]), (float)dmin[s]);
-    FRS_HIP(hipMemcpyAsync(ctx->dec_soff.ptr, htab, 3 * tab + dn_bytes, hipMemcpyHostToDevice, st));
+    // one stream through the one-pass selection (a bbox query): the tables ride in the selection kernel's arguments
+    const bool tabs_by_arg = nstreams == 1 && nblocks <= kSelOnePassBlocks;
+    SmallTabs stabs = {};
+    if (tabs_by_arg) {
+        memcpy(stabs.v, htab, 3 * tab + dn_bytes);  // 6 int64 + one float2
+    } else {
+        FRS_HIP(hipMemcpyAsync(ctx->dec_soff.ptr, htab, 3 * tab + dn_bytes, hipMemcpyHostToDevice, st));
+    }
     int64_t *dsoff = ctx->dec_soff.as<int64_t>();
     int64_t *dfbase = dsoff + (nstreams + 1);
     int64_t *dpoff = dfbase + (nstreams + 1);
@@ -3108,11 +3163,11 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         if (sel_small)
             k_sync_select<kSelStepsSmall><<<(unsigned)nblocks, kSelThreads, 0, st>>>(
                 blob_dev, blob_bytes, dsoff, nstreams, channels, bps, ctx->dec_status.as<uint64_t>(), ticket,
-                ctx->dec_epoch, nblocks, cpos, cand_cap, ncand);
+                ctx->dec_epoch, nblocks, cpos, cand_cap, ncand, tabs_by_arg ? dsoff : nullptr, stabs);
         else
             k_sync_select<kSelSteps><<<(unsigned)nblocks, kSelThreads, 0, st>>>(
                 blob_dev, blob_bytes, dsoff, nstreams, channels, bps, ctx->dec_status.as<uint64_t>(), ticket,
-                ctx->dec_epoch, nblocks, cpos, cand_cap, ncand);
+                ctx->dec_epoch, nblocks, cpos, cand_cap, ncand, tabs_by_arg ? dsoff : nullptr, stabs);
     } else {
         // (its own buffer: the one-pass status words must keep their epoch tags)
         // [bcount int32 | bbase int64 | bpos: kSelBlkCap positions per block]
@@ -3164,14 +3219,21 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     const char *opt_env = getenv("FRS_PIPE_OPT");
     const bool pipe_opt = pipe && !lane && max_frame < (int64_t)4096 * 256 && !(opt_env && atoi(opt_env) == 0);
     if (pipe_opt) {
+        // the last work-group copies the counters into hv (page-locked) itself: no device-to-host copy to wait for
+        hv[6] = -1;
         prof_begin(ctx, "decode_frames", &ev);
         k_decode_frames_pipe<true><<<(unsigned)frames, 128, 0, st>>>(blob_dev, dsoff, nstreams, dpoff, cpos, ends,
                                                                      dfbase, dchain, frames, channels, bps, pcm_dev,
-                                                                     blocksize, nvalid, dout, ncand, ncand);
+                                                                     blocksize, nvalid, dout, ncand, ncand, hv);
         prof_end(ctx, "decode_frames", ev);
         FRS_HIP(hipGetLastError());
-        FRS_HIP(hipMemcpyAsync(hv, ncand, sizeof(int) * 8, hipMemcpyDeviceToHost, st));
         FRS_HIP(hipStreamSynchronize(st));
+        if (__atomic_load_n(&hv[6], __ATOMIC_ACQUIRE) == -1) {  // (not expected) the epilogue did not run: copy, re-arm
+            FRS_HIP(hipMemcpyAsync(hv, ncand, sizeof(int) * 8, hipMemcpyDeviceToHost, st));
+            FRS_HIP(hipMemsetAsync(ncand + 8, 0, sizeof(int), st));
+            FRS_HIP(hipStreamSynchronize(st));
+            if (hv[6] == 0) hv[6] = 1;  // decide by the full path
+        }
         if (hv[6] == 0) {
             prof_collect(ctx);
             if (hv[7] != frames) {
@@ -3236,12 +3298,18 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
             FRS_HIP(ctx->dec_chass.ensure((size_t)frames + 64));
             fchass = ctx->dec_chass.as<int8_t>();
         }
-        k_decode_frames_lane<kOutPcm, true><<<(unsigned)((frames + 255) / 256), 256, 0, st>>>(
-            blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, dchain, frames, bps, pcm_dev, blocksize, nvalid, dout,
-            fbl, fbc, channels, planar, fchass);
+        const int planar16 = channels >= 3;  // independent channels of <= 16 bits (two: the side is 17 bits)
+        if (planar16)
+            k_decode_frames_lane<kOutPlanar16, true><<<(unsigned)((frames + 255) / 256), 256, 0, st>>>(
+                blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, dchain, frames, bps, pcm_dev, blocksize, nvalid,
+                dout, fbl, fbc, channels, planar, fchass);
+        else
+            k_decode_frames_lane<kOutPcm, true><<<(unsigned)((frames + 255) / 256), 256, 0, st>>>(
+                blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, dchain, frames, bps, pcm_dev, blocksize, nvalid,
+                dout, fbl, fbc, channels, planar, fchass);
         const int cpf = (blocksize + 255) / 256;
         k_interleave_dn<<<(unsigned)(frames * cpf), 256, 0, st>>>(planar, dpoff, dfbase, nstreams, channels, blocksize,
-                                                                 pcm_dev, dout, fchass, cpf);
+                                                                 pcm_dev, dout, fchass, cpf, planar16);
         k_decode_frames_wave_list<<<(unsigned)std::min<int64_t>(frames, 4 * (int64_t)ctx->num_cus), 64, 0, st>>>(
             blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, dchain, channels, bps, pcm_dev, blocksize, nvalid,
             dout, fbl, fbc);
