@@ -3675,7 +3675,9 @@ __device__ __forceinline__ void encode_frame_v4(const typename Elem<DT>::T *rast
 // SUB: the units are subframes -- (frame, channel) of a >= 3-channel stream, or of a two-channel stream's mid/side
 // pass (ST): left, right, mid in one launch, the 17-bit side signals (WIDE) in another.
 template <int DT, bool SUB = false, bool ST = false, bool WIDE = false>
-__global__ void __launch_bounds__(256, (sizeof(typename Elem<DT>::T) <= 2 && !WIDE) ? (ST ? 2 : 3) : 1) k_encode_v4(const typename Elem<DT>::T *raster, EncodeParams P,
+// (3 waves per SIMD for mono / >= 3-channel 16-bit units; 2 for the two-channel launches: L/R/M need 195 VGPRs, the
+// int32 side 256 -- capped from 262, a 32-byte spill: convert_2band encode 3.17 -> 2.78 ms against 1 wave per SIMD)
+__global__ void __launch_bounds__(256, sizeof(typename Elem<DT>::T) <= 2 ? (ST ? 2 : 3) : 1) k_encode_v4(const typename Elem<DT>::T *raster, EncodeParams P,
                                                   const TileGeom *tiles, const TileNorm *norms, const int16_t *luts,
                                                   const SubAnalysis *ana, uint8_t *arena, int64_t arena_cap,
                                                   int64_t *frame_off, uint64_t *status, int *ticket_ctr, int *err,
