@@ -2147,11 +2147,13 @@ __device__ inline uint32_t ana_sad(uint32_t a, uint32_t b, uint32_t c) {  // |a 
 // ST: `base` is the left band and sig (0..3) the coded signal of a two-channel stream's mid/side pass: left, right,
 // mid = (L + R) >> 1, side = L - R (converter.py:185-194 interleaves the bands; libFLAC process_subframes_ forms mid
 // and side from the normalised samples)
-template <int DT, int KIND, int kAnaChunk, bool ST = false>
+// SIG >= 0 (ST): the signal fixed at compile time, so a wave loads and normalises only the bands it needs
+template <int DT, int KIND, int kAnaChunk, bool ST = false, int SIG = -1>
 __device__ inline void ana_autoc(const typename Elem<DT>::T *base, const EncodeParams &P, const TileGeom &g,
                                  int64_t s0, const TileNorm &tn, const int16_t *slut, const int16_t *glut,
                                  const float *__restrict__ swin, int vec, double *acc, uint32_t &or_acc, uint32_t *ft,
-                                 int sig = 0) {
+                                 int sig_rt = 0) {
+    const int sig = SIG >= 0 ? SIG : sig_rt;
     using Ch = ChunkN<DT, kAnaChunk>;
     const uint32_t r0 = udiv_inv((uint32_t)s0, (uint32_t)g.w, 1.0 / (double)g.w);
     int64_t crow = r0;
@@ -2304,6 +2306,24 @@ __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *
 #pragma unroll
     for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
     uint32_t or_acc = 0, ft[5];
+    // ST: one specialisation per coded signal (left / right read one band, mid / side both, in half-size chunks):
+    // the runtime-selected form kept both bands' chunks and normalisations live (242 VGPRs, 2 waves per SIMD)
+#define FRS_ANA_SIG(KIND, SLUT)                                                                                           \
+    do {                                                                                                                \
+        if constexpr (ST) {                                                                                             \
+            if (chn == 0)                                                                                               \
+                ana_autoc<DT, KIND, kChunk, true, 0>(base, P, g, s0, tn, SLUT, glut, window, vec, acc, or_acc, ft);     \
+            else if (chn == 1)                                                                                          \
+                ana_autoc<DT, KIND, kChunk, true, 1>(base, P, g, s0, tn, SLUT, glut, window, vec, acc, or_acc, ft);     \
+            else if (chn == 2)                                                                                          \
+                ana_autoc<DT, KIND, kChunkMS, true, 2>(base, P, g, s0, tn, SLUT, glut, window, vec, acc, or_acc, ft);   \
+            else                                                                                                        \
+                ana_autoc<DT, KIND, kChunkMS, true, 3>(base, P, g, s0, tn, SLUT, glut, window, vec, acc, or_acc, ft);   \
+        } else {                                                                                                        \
+            ana_autoc<DT, KIND, kChunk, false>(base, P, g, s0, tn, SLUT, glut, window, vec, acc, or_acc, ft, chn);      \
+        }                                                                                                               \
+    } while (0)
+    constexpr int kChunkMS = kChunk > 16 ? kChunk / 2 : kChunk;
     if constexpr (!SLOW) {
         int16_t *wl = slut[wave];
         if (mode == kNormLut) {
@@ -2319,20 +2339,19 @@ __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *
             }
             __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's LUT stores have landed (each wave reads only its own)
             __builtin_amdgcn_wave_barrier();
-            ana_autoc<DT, kAnaKindLds, kChunk, ST>(base, P, g, s0, tn, wl, glut, window, vec, acc, or_acc, ft, chn);
+            FRS_ANA_SIG(kAnaKindLds, wl);
         } else {
-            ana_autoc<DT, kAnaKindZero, kChunk, ST>(base, P, g, s0, tn, wl, glut, window, vec, acc, or_acc, ft, chn);
+            FRS_ANA_SIG(kAnaKindZero, wl);
         }
     } else {
         if (mode == kNormFastDiv)
-            ana_autoc<DT, kAnaKindFastDiv, kChunk, ST>(base, P, g, s0, tn, nullptr, glut, window, vec, acc, or_acc, ft,
-                                                       chn);
+            FRS_ANA_SIG(kAnaKindFastDiv, nullptr);
         else
-            ana_autoc<DT, kAnaKindGeneric, kChunk, ST>(base, P, g, s0, tn, nullptr, glut, window, vec, acc, or_acc, ft,
-                                                       chn);
+            FRS_ANA_SIG(kAnaKindGeneric, nullptr);
     }
     if (!live) return;
     out[f * P.nvch + chn] = analysis_finish(acc, or_acc, n, P, ft, (ST && chn == 3) ? 1 : 0);
+#undef FRS_ANA_SIG
 }
 
 // ---- wave helpers (64 lanes)
