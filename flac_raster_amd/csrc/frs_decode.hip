@@ -2460,10 +2460,10 @@ __global__ void __launch_bounds__(64) k_decode_frames_wave_list(const uint8_t *b
 
 // ------------------------------------------------------------------ lane-per-frame decoder (batched decodes)
 // Throughput form for decodes of many frames (a whole arena, FLAC -> TIFF of a large raster): one lane per frame,
-// eight samples per step.  Each lane walks its own frame with a 64-bit bit cache fed from a six-dword queue of
-// big-endian words; the queue is topped up once per step from a 16-byte chunk whose load was issued a step earlier
-// (so loads rarely stall), and cache refills inside a step are branch-free selects.  Partition boundaries are
-// consumed by conditional shifts, the LPC recurrence runs on an eight-register ring with compile-time slots (no
+// eight samples per step.  Each lane walks its own frame through a ring of big-endian dwords in LDS (RingReader:
+// a code is read from a 32-bit window at the lane's bit position and consumed by an add; the ring is refilled once
+// per step from 16-byte chunks whose loads were issued a chunk earlier).  Partition boundaries are consumed by
+// conditional position steps, the LPC recurrence runs on an eight-register ring with compile-time slots (no
 // register indexing), and each step's eight outputs leave in one vector store (8 to 32 bytes; scattered 2-byte
 // stores from 64 lanes cost ~13x the bytes in partial-line writes).  The output kind is a template parameter, so
 // the per-sample work has no dtype switch.  Taken: mono streams of <= 16-bit samples, FIXED / LPC (order <= 8,
@@ -2472,137 +2472,110 @@ __global__ void __launch_bounds__(64) k_decode_frames_wave_list(const uint8_t *b
 // subframe ends exactly at the CRC-16 footer found by the span check.
 constexpr int kOutPcm = 0, kOutI16 = 1, kOutU16 = 2, kOutU8 = 3, kOutAny = 4;
 constexpr int kOutPlanar16 = 5;  // raw 16-bit PCM (the multi-channel planar scratch of >= 3 independent channels)
+constexpr int kDecStageSlots = 8;  // 16-byte output groups staged per lane before a flush (one 128-byte line)
 
-struct LaneReader {
+// Per-lane bit reader over a ring of kRingSlots big-endian dwords in LDS (column layout: slot s of a lane at
+// col[64 s], so a wave's reads and writes of one slot each hit 64 distinct banks; slot kRingSlots repeats slot 0, so
+// a two-dword window never wraps).  p is the next unread bit, counted from the first loaded chunk; a read is one
+// ds_read2 of the dwords holding bits [p, p + 64) and one 64-bit shift, so consuming a code is an add to p -- no
+// cache shifts and no queue bookkeeping per sample.  16-byte chunks enter the ring when it runs low (fill), each
+// chunk's global load issued one chunk ahead.  (Measured, C4 batched decode: 8 ring slots with a refill every 4
+// codes, i.e. 4 instead of 3 work-groups per CU, 3.20 -> 3.45 ms; every chunk also folded into the frame's CRC-16 as it
+// enters the ring, slice-by-4 in LDS, so no separate span check: 3.20 -> 3.85 ms.)
+constexpr int kRingSlots = 16;
+struct RingReader {
+    uint32_t *col;         // this lane's slot 0
     const uint8_t *abase;  // blob aligned down to 16 bytes; chunk q covers abase[q, q + 16)
     int64_t lead;          // blob - abase
+    int64_t q0;            // aligned offset of the first chunk (bit 0 of p)
     int64_t next;          // aligned offset of the next chunk to load
     int64_t end;           // stream end (blob bytes)
-    uint64_t c;            // left-aligned bit cache
-    int n;                 // valid bits in c
-    uint64_t qa, qb, qc;   // queued big-endian dwords, left-aligned (qa's high half first)
-    int qw;                // dwords queued (<= 6)
-    uint4 praw;            // the chunk loaded a step ahead (raw little-endian; converted when it joins the queue)
-    int pval;              // its bytes before the stream end (16 unless the chunk crosses it)
+    uint32_t p;            // next unread bit
+    uint32_t wr;           // dwords written to the ring
+    uint4 praw;            // the chunk loaded a fill ahead (raw little-endian)
+    int pval;              // its bytes before the stream end
     bool bad;
-    // The chunk at q as big-endian dword pairs, bytes at or past `end` zeroed.  Branch-free and unconditional: a guarded
-    // load compiled to a branch whose join waited for the load (vmcnt(0) at every chunk: no prefetch at all).  A chunk
-    // past the end re-reads the 16-byte-aligned chunk holding the last byte (never across a page) and is zeroed.
+    // The chunk at q, bytes at or past `end` counted in val.  Unconditional: a chunk past the end re-reads the
+    // 16-byte-aligned chunk holding the last byte (never across a page) and is zeroed by the fill.
     __device__ inline uint4 fetch(int64_t q, int &val) const {
         const int64_t lastq = (end - 1 + lead) & ~(int64_t)15;
         val = (int)max<int64_t>(0, min<int64_t>(16, end - (q - lead)));
         return *reinterpret_cast<const uint4 *>(abase + (q <= lastq ? q : lastq));
     }
-    __device__ static inline void convert(const uint4 &x, int val, uint64_t &a, uint64_t &b) {
-        auto keep = [&](uint32_t w, int d) -> uint32_t {  // dword d: bytes 4d..4d+3 (little-endian), zero past val
-            const int nb = val - 4 * d;
-            return nb >= 4 ? w : nb <= 0 ? 0u : (w & ((1u << (8 * nb)) - 1u));
+    __device__ inline void fill() {  // the prefetched chunk into the next four slots, the following chunk's load issued
+        auto be = [&](uint32_t w, int d) -> uint32_t {  // dword d as big-endian, zero past pval
+            const int nb = pval - 4 * d;
+            return __builtin_bswap32(nb >= 4 ? w : nb <= 0 ? 0u : (w & ((1u << (8 * nb)) - 1u)));
         };
-        a = ((uint64_t)__builtin_bswap32(keep(x.x, 0)) << 32) | __builtin_bswap32(keep(x.y, 1));
-        b = ((uint64_t)__builtin_bswap32(keep(x.z, 2)) << 32) | __builtin_bswap32(keep(x.w, 3));
+        const uint32_t d0 = be(praw.x, 0), d1 = be(praw.y, 1), d2 = be(praw.z, 2), d3 = be(praw.w, 3);
+        const uint32_t s = wr & (kRingSlots - 1);
+        uint32_t *a = col + (s << 6);
+        a[0] = d0;
+        a[64] = d1;
+        a[128] = d2;
+        a[192] = d3;
+        if (s == 0) col[kRingSlots << 6] = d0;
+        wr += 4;
+        praw = fetch(next, pval);
+        next += 16;
+        if (next - lead > end + 64) bad = true;  // runaway walk (corrupt data)
     }
-    __device__ inline void load_chunk(int64_t q, uint64_t &a, uint64_t &b) const {
-        int val;
-        const uint4 x = fetch(q, val);
-        convert(x, val, a, b);
+    // at least `need` unread dwords in the ring (fills leave at most need + 3, within the ring while need <= 13)
+    __device__ inline void ahead(int need) {
+        while ((int)(wr - (p >> 5)) < need && !bad) fill();
     }
-    // queue <- queue ++ prefetched chunk when at most two dwords are left (branch-free merge), next chunk in flight
-    __device__ inline void top_up() {
-        if (qw <= 2) {
-            uint64_t pa, pb;
-            convert(praw, pval, pa, pb);
-            const uint64_t a1 = (qa & 0xFFFFFFFF00000000ull) | (pa >> 32);
-            const uint64_t na = qw == 2 ? qa : qw == 1 ? a1 : pa;
-            const uint64_t nb = qw == 2 ? pa : qw == 1 ? ((pa << 32) | (pb >> 32)) : pb;
-            const uint64_t nc = qw == 2 ? pb : qw == 1 ? (pb << 32) : 0ull;
-            qa = na;
-            qb = nb;
-            qc = nc;
-            qw += 4;
-            praw = fetch(next, pval);
-            next += 16;
-            if (next - lead > end + 64) bad = true;  // runaway walk (corrupt data)
-        }
+    // a step's reads: up to eight codes of <= 32 bits read from windows at most 8 dwords on
+    __device__ inline void refill() { ahead(9); }
+    __device__ inline uint32_t window() const {  // bits [p, p + 32), MSB first (two dwords from p's in the ring)
+        const uint32_t *a = col + (((p >> 5) & (kRingSlots - 1)) << 6);
+        const uint64_t d = ((uint64_t)a[0] << 32) | a[64];
+        return (uint32_t)((d << (p & 31)) >> 32);
     }
-    __device__ inline void take(bool need) {  // branch-free: one dword into the cache when `need` (n <= 32)
-        const uint32_t w = (uint32_t)(qa >> 32);
-        c |= need ? ((uint64_t)w << (32 - n)) : 0ull;
-        n += need ? 32 : 0;
-        const uint64_t na = (qa << 32) | (qb >> 32), nb = (qb << 32) | (qc >> 32), nc = qc << 32;
-        qa = need ? na : qa;
-        qb = need ? nb : qb;
-        qc = need ? nc : qc;
-        qw -= need ? 1 : 0;
+    __device__ inline uint32_t peek32() {
+        ahead(2);
+        return window();
     }
-    __device__ inline void ensure() {
-        if (qw == 0) top_up();  // rare inside a step: the step used more than the queue held
-        take(n <= 32);
-    }
-    __device__ inline void init(const uint8_t *b, int64_t pos, int64_t e) {
+    __device__ inline void init(uint32_t *lane_col, const uint8_t *b, int64_t pos, int64_t e) {
+        col = lane_col;
         end = e;
         lead = (int64_t)(reinterpret_cast<uintptr_t>(b) & 15);
         abase = b - lead;
-        const int64_t q = (pos + lead) & ~(int64_t)15;
-        load_chunk(q, qa, qb);
-        qc = 0;
-        qw = 4;
-        praw = fetch(q + 16, pval);
-        next = q + 32;
+        q0 = (pos + lead) & ~(int64_t)15;
+        praw = fetch(q0, pval);
+        next = q0 + 16;
+        wr = 0;
         bad = false;
-        const int r = (int)((pos + lead) & 15);
-        c = 0;
-        n = 0;
-        for (int k = 0; k < (r >> 2); k++) take(true), c = 0, n = 0;  // skip whole dwords
-        top_up();
-        take(true);
-        top_up();
-        take(true);
-        c <<= 8 * (r & 3);
-        n -= 8 * (r & 3);
+        p = (uint32_t)((pos + lead) & 15) * 8u;
+        fill();
+        fill();
     }
     __device__ inline uint32_t bits(int k) {  // 0 <= k <= 32
-        const uint32_t v = k ? (uint32_t)(c >> (64 - k)) : 0u;
-        c = k ? c << k : c;
-        n -= k;
-        ensure();
-        return v;
+        const uint32_t w = peek32();
+        p += (uint32_t)k;
+        return k ? w >> (32 - k) : 0u;
     }
     __device__ inline int32_t sbits(int k) {
         const uint32_t v = bits(k);
         return (k == 0 || k == 32) ? (int32_t)v : ((int32_t)(v << (32 - k)) >> (32 - k));
     }
     __device__ inline uint32_t unary() {  // zeros before the next 1 (consumed)
-        uint32_t q = 0;
-        int z = c ? __builtin_clzll(c) : 64;
-        while (z >= n && !bad) {  // rare: a run longer than the cache
-            q += (uint32_t)n;
-            c = 0;
-            n = 0;
-            ensure();
-            z = c ? __builtin_clzll(c) : 64;
+        uint32_t q = 0, w;
+        for (;;) {
+            w = peek32();
+            if (w != 0 || bad) break;
+            q += 32;
+            p += 32;
         }
-        q += (uint32_t)z;
-        c = (z + 1 >= 64) ? 0 : (c << (z + 1));
-        n -= z + 1;
-        ensure();
-        return q;
+        const uint32_t z = w ? (uint32_t)__builtin_clz(w) : 0u;
+        p += z + 1;
+        return q + z;
     }
     __device__ inline uint32_t rice(int k) {  // Rice code, parameter k <= 30
-        const int z = c ? __builtin_clzll(c) : 64;
-        if (z + 1 + k > n) {  // rare: longer than the cached bits
-            const uint32_t q = unary();
-            return (q << k) | bits(k);
-        }
-        const uint32_t low = k ? (uint32_t)(((c << z) << 1) >> (64 - k)) : 0u;
-        const int used = z + 1 + k;
-        c = used >= 64 ? 0 : (c << used);
-        n -= used;
-        ensure();
-        return ((uint32_t)z << k) | low;
+        const uint32_t q = unary();
+        return (q << k) | bits(k);
     }
     __device__ inline int64_t pos() const {  // bit position of the next unread bit from the blob start
-        // loaded bytes end at next; the prefetched chunk (128 bits), the queued dwords and the cache are unread
-        return (next - lead) * 8 - 128 - (int64_t)qw * 32 - n;
+        return (q0 - lead) * 8 + (int64_t)p;
     }
 };
 
@@ -2614,12 +2587,11 @@ __device__ inline uint32_t dn_bits_t(const DecOut &o, int32_t pcm, float2 p) {
     } else if constexpr (OUT == kOutPlanar16) {
         return (uint32_t)pcm & 0xFFFFu;
     } else {
-        const float v = (float)(pcm >> o.shift) * (1.0f / 32768.0f);
-        float a = __fadd_rn(v, 1.0f);
-        a = __fmul_rn(a, 0.5f);  // == __fdiv_rn(a, 2.0f): scaling by a power of two
-        a = __fmul_rn(a, p.x);
-        a = __fadd_rn(a, p.y);
-        const int64_t r = (int64_t)rintf(a);
+        // ((v + 1) / 2) * rng + mn with v = h / 32768 (h = pcm >> shift, |h| < 2^24): (v + 1) / 2 = (h + 32768) 2^-16
+        // exactly, and scaling rng by 2^-16 instead is exact too, so one product and one sum round as in the
+        // reference's sequence; the rounded value is within the <= 16-bit output range, so an int32 conversion
+        const float a = __fadd_rn(__fmul_rn((float)((pcm >> o.shift) + 32768), p.x * (1.0f / 65536.0f)), p.y);
+        const int32_t r = (int32_t)rintf(a);
         if constexpr (OUT == kOutU8) return (uint32_t)(uint8_t)r;
         else return (uint32_t)(uint16_t)r;
     }
@@ -2711,7 +2683,8 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
     // stores -- one 16-byte store per step to 64 different lines had the L2 write each line back several times
     // (PMC: 5x the output bytes written)
     constexpr bool kStage = OUT == kOutI16 || OUT == kOutU16 || OUT == kOutU8 || OUT == kOutPlanar16;
-    __shared__ uint4 ostage[kStage ? 4 : 1][kStage ? 8 : 1][kStage ? 64 : 1];
+    __shared__ uint4 ostage[kStage ? 4 : 1][kStage ? kDecStageSlots : 1][kStage ? 64 : 1];
+    __shared__ uint32_t ring[4][kRingSlots + 1][64];  // the lanes' bit readers
     const int64_t fi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint8_t *obytes = MC ? reinterpret_cast<uint8_t *>(planar)
                          : OUT == kOutPcm ? reinterpret_cast<uint8_t *>(pcm) : static_cast<uint8_t *>(dout.out);
@@ -2733,8 +2706,8 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
             if (cd.ok && cd.frame_no == kk && cd.bs <= blocksize && first + cd.bs <= nsamp && take_all) {
                 const int bs = cd.bs;
                 const float2 dnp = OUT != kOutPcm && OUT != kOutPlanar16 ? dout.dn[s] : make_float2(0.f, 0.f);
-                LaneReader br;
-                br.init(blob, fpos + cd.hdr_len, send);
+                RingReader br;
+                br.init(&ring[threadIdx.x >> 6][0][threadIdx.x & 63], blob, fpos + cd.hdr_len, send);
                 for (int chn = 0; chn < (MC ? nch : 1) && take_all; chn++) {
                 const int64_t obase = MC ? (fi * nch + chn) * (int64_t)blocksize : poff[s] + first;
                 br.bits(1);
@@ -2805,7 +2778,7 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
                     auto flush = [&]() {
                         if constexpr (kStage) {
 #pragma unroll
-                            for (int u = 0; u < 8; u++) {
+                            for (int u = 0; u < kDecStageSlots; u++) {
                                 if (u < nst) {
                                     const uint4 v = st[u * 64 + ln];
                                     if constexpr (es == 2) reinterpret_cast<uint4 *>(rdst)[u] = v;
@@ -2816,31 +2789,29 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
                         }
                     };
                     for (int i0 = 0; i0 < bs && take; i0 += 8) {
-                        br.top_up();
+                        br.refill();
                         uint32_t ob[8];
                         // the general per-sample body only where some lane needs it: warm-up samples (step 0), the
                         // block's end, a partition boundary of a Rice-coded subframe inside this step
                         const bool gen = i0 == 0 || i0 + 8 > bs || (!raw && !cst && part_end < i0 + 8);
                         if (!__ballot(gen)) {
+                            // one code per sample: VERBATIM = sbps raw bits, Rice = unary run + stop bit + k low bits,
+                            // CONSTANT = nothing read.  Read from a 32-bit window at p: the unary run (zeroed for
+                            // VERBATIM / CONSTANT), then kk low bits; a Rice code longer than the window goes the
+                            // general way (rare)
+                            const uint32_t rmask = (raw || cst) ? 0u : ~0u, rbit = rmask & 1u;
+                            const uint32_t kk = raw ? (uint32_t)sbps : cst ? 0u : (uint32_t)k;
 #pragma unroll
                             for (int u = 0; u < 8; u++) {
-                                // one code per sample: VERBATIM = sbps raw bits, Rice = unary run + stop bit + k low
-                                // bits, CONSTANT = nothing read
-                                const int z = br.c ? __builtin_clzll(br.c) : 64;
-                                const int pre = (raw || cst) ? 0 : z + 1;
-                                const int kk = raw ? sbps : (cst ? 0 : k);
-                                const int used = pre + kk;
-                                uint32_t v;
-                                if (used > br.n) {  // (rare: a Rice code longer than the >= 33 cached bits)
-                                    const uint32_t q = br.unary();
-                                    v = (q << k) | br.bits(k);
-                                } else {
-                                    const uint64_t tb = pre >= 64 ? 0ull : (br.c << pre);
-                                    const uint32_t low = kk ? (uint32_t)(tb >> (64 - kk)) : 0u;
-                                    br.c = used >= 64 ? 0ull : (br.c << used);
-                                    br.n -= used;
-                                    br.ensure();
-                                    v = raw ? low : (((uint32_t)z << k) | low);
+                                const uint32_t win = br.window();
+                                const uint32_t zr = (win ? (uint32_t)__builtin_clz(win) : 32u) & rmask;
+                                const uint32_t used = zr + rbit + kk;
+                                uint32_t v = (zr << k) | __builtin_amdgcn_ubfe(win, 32u - used, kk);
+                                const bool longc = used > 32;
+                                br.p += longc ? 0u : used;
+                                if (__ballot(longc)) {  // (wave-uniform, rare)
+                                    if (longc) v = br.rice(k);
+                                    br.refill();
                                 }
                                 const int32_t r = raw ? ((int32_t)(v << (32 - sbps)) >> (32 - sbps))
                                                       : (int32_t)((v >> 1) ^ (uint32_t)(-(int32_t)(v & 1)));
@@ -2865,11 +2836,10 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
                             if (!cst && i >= o && i < bs) {
                                 // a partition boundary consumes the next Rice parameter (conditional shift)
                                 const bool bnd = i == part_end && !raw;
-                                const int kp = (int)(br.c >> (64 - pb));
+                                const int kp = (int)(br.peek32() >> (32 - pb));
                                 k = bnd ? kp : k;
                                 const int adv = bnd ? pb : 0;
-                                br.c <<= adv;
-                                br.n -= adv;
+                                br.p += (uint32_t)adv;
                                 part_end += bnd ? psz : 0;
                                 if (bnd && k == esc) take = false;
                                 int32_t r;
@@ -2906,7 +2876,7 @@ __global__ void __launch_bounds__(256) k_decode_frames_lane(const uint8_t *blob,
                                         st[nst * 64 + ln] = make_uint4(ob[0] | (ob[1] << 8) | (ob[2] << 16) | (ob[3] << 24),
                                                                  ob[4] | (ob[5] << 8) | (ob[6] << 16) | (ob[7] << 24), 0u,
                                                                  0u);
-                                    if (++nst == 8) flush();
+                                    if (++nst == kDecStageSlots) flush();
                                 } else if constexpr (es == 2) {
                                     *reinterpret_cast<uint4 *>(dst) =
                                         make_uint4(ob[0] | (ob[1] << 16), ob[2] | (ob[3] << 16), ob[4] | (ob[5] << 16),
