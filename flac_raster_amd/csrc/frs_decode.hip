@@ -2357,6 +2357,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
         // de-normalised 1- and 2-byte outputs: eight samples per lane and step, one 16-byte LDS read and one 16- (8-)
         // byte store (the per-sample loop issued 64 scattered 2-byte stores per lane: 13.6 of a frame's 137 us)
         const uint4 *x8 = reinterpret_cast<const uint4 *>(xout);
+        const float dnx = dnp.x * (1.0f / 65536.0f);
         for (int g = lane; g < (bs >> 3); g += 64) {
             const uint4 v = x8[g];
             const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
@@ -2364,12 +2365,9 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
 #pragma unroll
             for (int j = 0; j < 8; j++) {
                 const int32_t x = (int32_t)(int16_t)(wv[j >> 1] >> (16 * (j & 1)));
-                const float f = (float)((int32_t)((uint32_t)x << w)) * (1.0f / 32768.0f);
-                float a = __fadd_rn(f, 1.0f);
-                a = __fmul_rn(a, 0.5f);  // == __fdiv_rn(a, 2.0f): scaling by a power of two
-                a = __fmul_rn(a, dnp.x);
-                a = __fadd_rn(a, dnp.y);
-                ob[j] = (uint32_t)(int64_t)rintf(a);
+                // (dn_bits_t's exact rewrite of ((x / 32768 + 1) / 2) * rng + mn)
+                const float a = __fadd_rn(__fmul_rn((float)((int32_t)((uint32_t)x << w) + 32768), dnx), dnp.y);
+                ob[j] = (uint32_t)(int32_t)rintf(a);
             }
             if (dt == FRS_DT_U8) {
                 reinterpret_cast<uint2 *>(static_cast<uint8_t *>(dout.out) + obase)[g] =
