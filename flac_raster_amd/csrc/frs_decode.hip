@@ -17,6 +17,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -1791,13 +1792,19 @@ __device__ inline int32_t lds_poll(volatile int32_t *p) { return *p; }
 
 // OPT: the last work-group to finish (flags[8] counts them; re-armed to 0) copies the call's counters flags[0..7] to
 // page-locked host memory, so the host reads them after its stream synchronisation without a device-to-host copy
+// (system-scope fences: the work-group's output may be page-locked host memory, and the host takes hout[6] leaving -1
+// as the decode's completion -- it is written last, after every other counter)
 __device__ inline void pipe_wg_exit(int *flags, int64_t nframes, int *hout) {
-    __threadfence();
+    __threadfence_system();
     const int t = atomicAdd(&flags[8], 1);
     if (t == (int)nframes - 1) {
         flags[8] = 0;
         __threadfence();
-        for (int k = 0; k < 8; k++) hout[k] = __hip_atomic_load(&flags[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int k = 0; k < 8; k++)
+            if (k != 6) hout[k] = __hip_atomic_load(&flags[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int h6 = __hip_atomic_load(&flags[6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __threadfence_system();
+        __hip_atomic_store(&hout[6], h6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __threadfence_system();
     }
 }
@@ -3119,7 +3126,7 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     // batched mono decode (6241 streams of 8-KB frames) 2.16 -> 3.21 ms (the selection's CRC fold costs more than the
     // reading span check it replaces: 1 LDS table lookup per byte either way, at lower occupancy), so mono keeps the
     // reading form.  FRS_SPAN_READ=1 / 2 forces the reading / prefix form (tests).
-    const char *span_env = getenv("FRS_SPAN_READ");
+    const char *span_env = nblocks > kSelOnePassBlocks ? getenv("FRS_SPAN_READ") : nullptr;  // (no env walk per query)
     const int span_mode = span_env ? atoi(span_env) : 0;
     const bool pcrc_span = span_mode != 1 && (span_mode == 2 || mcl) && nblocks > kSelOnePassBlocks &&
                            (lane || !pipe) && max_frame < (int64_t)4096 * 256;
@@ -3195,7 +3202,22 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
                                                                      blocksize, nvalid, dout, ncand, ncand, hv);
         prof_end(ctx, "decode_frames", ev);
         FRS_HIP(hipGetLastError());
-        FRS_HIP(hipStreamSynchronize(st));
+        // completion = the last work-group's page-locked counters (hv[6] written last, after system-scope fences over
+        // every work-group's output): polled here, a few microseconds before the stream's completion signal; bounded,
+        // then the stream synchronisation decides.  FRS_C5_POLL=0: synchronise only
+        static const bool poll = !(getenv("FRS_C5_POLL") && atoi(getenv("FRS_C5_POLL")) == 0);
+        bool seen = false;
+        if (poll && !ctx->prof) {
+            const auto t0 = std::chrono::steady_clock::now();
+            for (uint32_t k = 0;; k++) {
+                if (__atomic_load_n(&hv[6], __ATOMIC_ACQUIRE) != -1) {
+                    seen = true;
+                    break;
+                }
+                if ((k & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+            }
+        }
+        if (!seen) FRS_HIP(hipStreamSynchronize(st));
         if (__atomic_load_n(&hv[6], __ATOMIC_ACQUIRE) == -1) {  // (not expected) the epilogue did not run: copy, re-arm
             FRS_HIP(hipMemcpyAsync(hv, ncand, sizeof(int) * 8, hipMemcpyDeviceToHost, st));
             FRS_HIP(hipMemsetAsync(ncand + 8, 0, sizeof(int), st));
