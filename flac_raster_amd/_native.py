@@ -25,12 +25,14 @@ STATUS = {-1: "FRS_E_ARG", -2: "FRS_E_HIP", -3: "FRS_E_NOSPACE", -4: "FRS_E_CORR
 DTYPE_CODES = {np.dtype(np.uint8): 1, np.dtype(np.uint16): 2, np.dtype(np.int16): 3,
                np.dtype(np.int32): 4, np.dtype(np.uint32): 5, np.dtype(np.float32): 6,
                np.dtype(np.float64): 7}
+_DT_CACHE = {}  # dtype argument -> (itemsize, DTYPE_CODES code): the bbox-query path skips np.dtype per call
 
 # names every build must export (tests check them against include/flac_raster_amd.h)
 EXPORTS = (
     "frs_abi_version", "frs_device_count", "frs_ctx_create", "frs_ctx_destroy", "frs_last_error",
     "frs_encode_arena_bound", "frs_encode_tiles_device", "frs_encode_tiles",
     "frs_decode_frames_device", "frs_decode_frames", "frs_decode_tiles_device", "frs_decode_tiles",
+    "frs_decode_tile_device",
     "frs_denormalize_device", "frs_denormalize",
     "frs_dev_malloc", "frs_dev_free", "frs_host_malloc", "frs_host_free", "frs_memcpy_h2d", "frs_memcpy_d2h", "frs_ctx_sync",
     "frs_synth_raster_device", "frs_ctx_stream", "frs_profile_enable", "frs_profile_avg_ms",
@@ -109,6 +111,9 @@ def load_library(path: Optional[os.PathLike] = None):
         L.frs_decode_tiles_device.argtypes = dect_args
         L.frs_decode_tiles.restype = i32
         L.frs_decode_tiles.argtypes = dect_args
+        L.frs_decode_tile_device.restype = i32
+        L.frs_decode_tile_device.argtypes = [ctxp, vp, i64, i64, i64, i32, i32, i32, ctypes.c_double, ctypes.c_double,
+                                             i32, vp]
         den_args = [ctxp, vp, i64, i32, ctypes.c_double, ctypes.c_double, i32, vp]
         L.frs_denormalize_device.restype = i32
         L.frs_denormalize_device.argtypes = den_args
@@ -442,19 +447,15 @@ class Context:
                            data_max: float, dtype, out, blocksize: int = 4096) -> None:
         """decode_tiles_device for ONE stream (blob bytes [start, end), `count` samples per channel) -- the latency
         path of a bbox query: argument tables are this context's reused ctypes arrays (no numpy per call)."""
-        dt = np.dtype(dtype)
-        if count * channels * dt.itemsize > out.nbytes:
+        dt = _DT_CACHE.get(dtype)
+        if dt is None:
+            dt = _DT_CACHE[dtype] = (np.dtype(dtype).itemsize, DTYPE_CODES[np.dtype(dtype)])
+        if count * channels * dt[0] > out.nbytes:
             raise ValueError("output buffer too small")
-        tabs = getattr(self, "_one_tabs", None)
-        if tabs is None:
-            tabs = self._one_tabs = ((ctypes.c_int64 * 2)(), (ctypes.c_int64 * 2)(), (ctypes.c_double * 1)(),
-                                     (ctypes.c_double * 1)())
-        soff, poff, mn, mx = tabs
-        soff[0], soff[1] = int(start), int(end)
-        poff[1] = int(count)
-        mn[0], mx[0] = float(data_min), float(data_max)
-        self._check(self.lib.frs_decode_tiles_device(self.handle, ctypes.c_void_p(blob.ptr), soff, 1, channels, bps,
-                                                     blocksize, poff, mn, mx, DTYPE_CODES[dt], ctypes.c_void_p(out.ptr)))
+        rc = self.lib.frs_decode_tile_device(self.handle, blob.ptr, int(start), int(end), int(count), channels, bps,
+                                             blocksize, float(data_min), float(data_max), dt[1], out.ptr)
+        if rc != FRS_OK:
+            raise FrsError(rc, self.last_error())
 
     def denormalize_host(self, pcm: np.ndarray, data_min: float, data_max: float, dtype, pcm_bps: int = 16) -> np.ndarray:
         p = np.ascontiguousarray(pcm, dtype=np.int32)

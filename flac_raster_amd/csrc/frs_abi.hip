@@ -431,6 +431,14 @@ int frs_decode_tiles_device(frs_ctx *ctx, const uint8_t *blob_dev, const int64_t
                         data_max, out_dtype, out_dev);
 }
 
+int frs_decode_tile_device(frs_ctx *ctx, const uint8_t *blob_dev, int64_t start, int64_t end, int64_t count,
+                           int32_t channels, int32_t bps, int32_t blocksize, double data_min, double data_max,
+                           int32_t out_dtype, void *out_dev) {
+    const int64_t soff[2] = {start, end}, poff[2] = {0, count};
+    return frs_decode_tiles_device(ctx, blob_dev, soff, 1, channels, bps, blocksize, poff, &data_min, &data_max,
+                                   out_dtype, out_dev);
+}
+
 int frs_decode_tiles(frs_ctx *ctx, const uint8_t *blob_host, const int64_t *stream_off, int32_t nstreams,
                      int32_t channels, int32_t bps, int32_t blocksize, const int64_t *pcm_off, const double *data_min,
                      const double *data_max, int32_t out_dtype, void *out_host) {

@@ -145,6 +145,12 @@ int frs_decode_tiles_device(frs_ctx *ctx, const uint8_t *blob_dev, const int64_t
 int frs_decode_tiles(frs_ctx *ctx, const uint8_t *blob_host, const int64_t *stream_off, int32_t nstreams,
                      int32_t channels, int32_t bps, int32_t blocksize, const int64_t *pcm_off, const double *data_min,
                      const double *data_max, int32_t out_dtype, void *out_host);
+/* frs_decode_tiles_device for ONE tile -- the bbox query of cli.py:984-1023 (extract-streaming decodes the single
+ * selected tile): its frames are blob_dev[start, end), `count` samples per channel, scalar arguments only (no
+ * per-call tables for the binding to marshal on the latency path).  Errors as frs_decode_tiles_device. */
+int frs_decode_tile_device(frs_ctx *ctx, const uint8_t *blob_dev, int64_t start, int64_t end, int64_t count,
+                           int32_t channels, int32_t bps, int32_t blocksize, double data_min, double data_max,
+                           int32_t out_dtype, void *out_dev);
 
 /* converter.py:88-110 after pyflac+soundfile's WAV round trip (sonos-pyflac.txt:1629, 1827-1852): the
  * decoder's int32 samples go into a PCM_16 WAV (16-bit streams unchanged; 32-bit streams keep x >> 16,

@@ -1,4 +1,5 @@
 """C5 query latency breakdown on the C4 arena: selection (host), decode call (device + sync), result download."""
+import ctypes
 import json
 import sys
 import time
@@ -31,7 +32,9 @@ def main():
     mode = sys.argv[2] if len(sys.argv) > 2 else ""
     prof = mode == "prof"  # kernel times (the profile's events add ~10 us per kernel)
     hostout = mode.startswith("hostout")
-    one = mode == "hostout1"  # + the single-stream call (decode_tile_device: reused ctypes tables)  # the decode kernels store straight into the page-locked host buffer (no D2H copy)
+    one = mode == "hostout1"
+    old1 = mode == "hostout1old"
+    tabs = ((ctypes.c_int64 * 2)(), (ctypes.c_int64 * 2)(), (ctypes.c_double * 1)(), (ctypes.c_double * 1)())  # + the single-stream call (decode_tile_device: reused ctypes tables)  # the decode kernels store straight into the page-locked host buffer (no D2H copy)
 
     class _HostOut:
         ptr, nbytes = int(host.ctypes.data), host.nbytes
@@ -56,7 +59,15 @@ def main():
         i = f["frame_id"]
         n = f["window"]["width"] * f["window"]["height"]
         t1 = time.perf_counter()
-        if one:
+        if old1:  # the round-5-before binding: per-call ctypes tables into frs_decode_tiles_device
+            soff, poff, dmn, dmx = tabs
+            soff[0], soff[1] = int(off[i]), int(off[i + 1])
+            poff[1] = int(n)
+            dmn[0], dmx[0] = float(mn[i]), float(mx[i])
+            ctx._check(ctx.lib.frs_decode_tiles_device(ctx.handle, ctypes.c_void_p(arena.ptr), soff, 1, 1, 16, 4096,
+                                                       poff, dmn, dmx, _native.DTYPE_CODES[np.dtype(np.int16)],
+                                                       ctypes.c_void_p(out.ptr)))
+        elif one:
             ctx.decode_tile_device(arena, off[i], off[i + 1], n, 1, 16, mn[i], mx[i], np.int16, out)
         else:
             ctx.decode_tiles_device(arena, np.array([off[i], off[i + 1]], dtype=np.int64), [n], channels=1, bps=16,
