@@ -649,7 +649,8 @@ __global__ void __launch_bounds__(1024) k_sync_scan(const int32_t *bcount, int64
     const int64_t c = (n + 1023) / 1024;
     const int64_t a = min(n, (int64_t)t * c), b = min(n, a + c);
     int64_t run = 0;
-    for (int64_t i = a; i < b; i++) run += bcount[i];
+#pragma unroll 8
+    for (int64_t i = a; i < b; i++) run += bcount[i];  // (unrolled: the loads of a thread's range issue together)
     int64_t x = run;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -664,6 +665,7 @@ __global__ void __launch_bounds__(1024) k_sync_scan(const int32_t *bcount, int64
         total += wsum[k];
     }
     int64_t acc = base + x - run;
+#pragma unroll 8
     for (int64_t i = a; i < b; i++) {
         bbase[i] = acc;
         acc += bcount[i];
@@ -1105,10 +1107,29 @@ __global__ void __launch_bounds__(1024) k_chain_lds(const int64_t *soff, int ns,
         if (tid == 0) atomicAdd(bad, 1);
         return;
     }
-    if (tid == 0) {
-        rng[0] = ns == 1 ? 0 : lower_bound_pos(cpos, nc, soff[s]);
-        rng[1] = ns == 1 ? nc : lower_bound_pos(cpos, nc, soff[s + 1]);
-        sbad = 0;
+    if (tid < 64) {  // the stream's candidate range: wave 0 narrows both bounds 64 ways per step (3 dependent loads for
+                     // 390 K candidates instead of 2 x 19 of a one-lane binary search)
+        for (int e = 0; e < 2; e++) {
+            const int64_t key = soff[s + e];
+            int lo = 0, hi = nc;  // first index with cpos >= key lies in [lo, hi]
+            if (ns == 1) {
+                lo = hi = e ? nc : 0;
+            }
+            while (hi - lo > 64) {
+                const int64_t span = hi - lo;
+                const int piv = lo + (int)(span * (tid + 1) / 65);  // 64 pivots inside (lo, hi)
+                const uint64_t below = __ballot(cpos[piv] < key);  // pivots with cpos < key: a prefix of the lanes
+                const int nb = __popcll(below);
+                const int nlo = nb ? lo + (int)(span * nb / 65) + 1 : lo;
+                const int nhi = nb < 64 ? lo + (int)(span * (nb + 1) / 65) : hi;
+                lo = nlo;
+                hi = nhi;
+            }
+            const int i = lo + tid;
+            const uint64_t below = __ballot(i < hi && cpos[i] < key);
+            if (tid == 0) rng[e] = lo + __popcll(below);
+        }
+        if (tid == 0) sbad = 0;
     }
     __syncthreads();
     const int c0 = rng[0], c1 = rng[1];
