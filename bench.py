@@ -43,8 +43,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E peak 8.0 TB/s
 VALU_PEAK_GINST_S = 1024 * 2.4 * 0.5
 METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"] if (ROOT / "BASELINE.json").exists() else \
     "Mpixels/sec encode (create-streaming) + bbox-extract ms, 1/2/4/8 GPU; bit-exact vs ref"
-KERNEL_SYMBOL = {"encode": "frs::k_encode_v4<3, false>", "analyze": "frs::k_analyze_v3<3, false, true>",
-                 "stats": "frs::k_tile_stats_vec<3>"}
+# bench kernel name -> the leading template arguments of its C4 instance in a rocprofv3 summary.  A template that
+# grows trailing parameters keeps matching (pmc_for takes the unique symbol that extends the prefix); a missing or
+# ambiguous match is reported on stderr, and tests/test_bench_pmc.py checks every entry against the committed summary.
+KERNEL_SYMBOL = {"encode": "frs::k_encode_v4<3, false", "analyze": "frs::k_analyze_v3<3, false, true"}
+# the kernels one C4 step launches (once each): their counter bytes per launch add up to the step's HBM traffic
+STEP_KERNELS = ("frs::k_analyze_v3<", "frs::k_encode_v4<", "frs::k_fast_finish")
+# achievable HBM rate (MI355X_MICROARCH.md: a streaming read+write kernel sustains ~6.29 TB/s of the 8 TB/s peak)
+HBM_ACHIEVABLE_GBS = 6290.0
 
 
 def parse():
@@ -60,6 +66,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the N = 1 extras (e2e, batched decode, ...)")
+    ap.add_argument("--legs", default="", help="comma-separated N = 1 extras to run (default: all of them)")
     ap.add_argument("--queries", type=int, default=1000, help="C5 bbox-extract queries (0: skip)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "pmc_traffic.json"),
                     help="tools/pmc_traffic.py output of a rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE pass of this bench")
@@ -196,7 +203,14 @@ def main():
                      "traffic": traffic_for(args.traffic_json, dom, px_rank),
                      # the north-star figure: the band's 2 B/px read once per step against the HBM read peak
                      "step_read": {"bytes": 2 * px_rank, "achieved": round(2 * px_rank / (ms_per_step * 1e-3) / 1e9, 1),
-                                   "frac": round(2 * px_rank / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}},
+                                   "frac": round(2 * px_rank / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+                     # the step's own traffic floor: algorithmic bytes (band read once + frames written once) at
+                     # the achievable HBM rate (~1.0 ms on C4)
+                     "step_floor": {"bytes": 2 * px_rank + comp_bytes,
+                                    "ms": round((2 * px_rank + comp_bytes) / (HBM_ACHIEVABLE_GBS * 1e9) * 1e3, 3),
+                                    "frac": round((2 * px_rank + comp_bytes) / (HBM_ACHIEVABLE_GBS * 1e9) * 1e3
+                                                  / ms_per_step, 4)},
+                     "step_traffic": step_traffic_for(args.traffic_json, px_rank, ms_per_step)},
     }
     if comm is not None:
         result["allgather_us"] = allgather_figures(comm, ag_s, np.diff(off), counts)
@@ -222,6 +236,8 @@ def main():
                           ("convert_2band", lambda: convert_2band(ctx)), ("raw_frames", lambda: raw_frames(ctx)),
                           ("convert_level8", lambda: convert_level8(ctx)),
                           ("end_to_end", lambda: end_to_end(ctx, raster, arena, off, rows, W, T, args))):
+            if args.legs and name not in args.legs.split(","):
+                continue
             progress(name)
             result[name] = leg()
     if rank == 0 and world == 1 and not args.no_cpu:  # (the CPU baseline is an N = 1 figure)
@@ -678,9 +694,20 @@ def loaded_lib_sha256() -> str:
     return hashlib.sha256(p.read_bytes()).hexdigest()
 
 
-def pmc_for(path, kernel, px, field):
-    """Per-launch PMC figure `field` of `kernel` from a committed summary (tools/pmc_traffic.py) measured on this
-    same workload (C4 slab of `px` pixels) AND this same library build (its sha256 stamp); None otherwise."""
+def resolve_symbol(kernels, kernel):
+    """The summary key of bench kernel `kernel`: the exact symbol, else the unique symbol extending its
+    KERNEL_SYMBOL prefix by further template arguments (`<3, false` matches `<3, false, false, false>`, not
+    `<3, falsey>`).  None when absent or ambiguous (two instances extend the prefix)."""
+    want = KERNEL_SYMBOL.get(kernel, kernel)
+    if want in kernels:
+        return want
+    hits = [k for k in kernels if k.startswith(want) and k[len(want):len(want) + 1] in (",", ">")]
+    return hits[0] if len(hits) == 1 else None
+
+
+def load_pmc(path, px):
+    """A committed counter summary (tools/pmc_traffic.py) measured on this same workload (C4 slab of `px`
+    pixels) AND this same library build (its sha256 stamp); None otherwise."""
     try:
         d = json.loads(Path(path).read_text())
     except (OSError, ValueError):
@@ -688,9 +715,41 @@ def pmc_for(path, kernel, px, field):
     if d.get("pixels_per_launch") not in (None, px):
         return None
     if d.get("lib_sha256") != loaded_lib_sha256():
+        print(f"bench.py: {path} was measured on another library build: no counter figures", file=sys.stderr)
         return None
-    k = d.get("kernels", {}).get(KERNEL_SYMBOL.get(kernel, kernel))
-    return None if k is None or field not in k else k[field]
+    return d
+
+
+def pmc_for(path, kernel, px, field):
+    """Per-launch PMC figure `field` of bench kernel `kernel` (see load_pmc); None otherwise.  A summary of this
+    library whose symbols do not resolve is a bug (a renamed template): reported on stderr."""
+    d = load_pmc(path, px)
+    if d is None:
+        return None
+    kernels = d.get("kernels", {})
+    sym = resolve_symbol(kernels, kernel)
+    if sym is None:
+        print(f"bench.py: no unique counter entry for {kernel!r} ({KERNEL_SYMBOL.get(kernel, kernel)}) in {path}",
+              file=sys.stderr)
+        return None
+    return kernels[sym].get(field)
+
+
+def step_traffic_for(path, px, ms_per_step):
+    """HBM bytes one C4 step moves by the counters: the FETCH x2 + WRITE bytes per launch of every kernel the
+    step launches (STEP_KERNELS), against the step time and the achievable HBM rate; None without a summary."""
+    d = load_pmc(path, px)
+    if d is None:
+        return None
+    parts = {k: v["bytes"] for k, v in d.get("kernels", {}).items()
+             if "bytes" in v and any(k.startswith(p) for p in STEP_KERNELS)}
+    if not parts:
+        return None
+    total = sum(parts.values())
+    rate = total / (ms_per_step * 1e-3) / 1e9
+    return {"bytes": round(total), "kernels": {k: round(v) for k, v in parts.items()},
+            "achieved": round(rate, 1), "achievable": HBM_ACHIEVABLE_GBS,
+            "frac_achievable": round(rate / HBM_ACHIEVABLE_GBS, 4), "frac_peak": round(rate / HBM_PEAK_GBS, 4)}
 
 
 def traffic_for(path, kernel, px):

@@ -543,6 +543,7 @@ void *frs_host_malloc(frs_ctx *ctx, int64_t bytes) {
         ctx->err = std::string("hipHostMalloc: ") + hipGetErrorString(e);
         return nullptr;
     }
+    ctx->host_allocs.emplace_back(reinterpret_cast<uintptr_t>(p), (size_t)bytes);
     return p;
 }
 
@@ -551,6 +552,12 @@ void frs_host_free(frs_ctx *ctx, void *ptr) {
     if (ctx) {
         hipSetDevice(ctx->device);
         hipDeviceSynchronize();  // (copies on the context's side streams may still read or write it)
+        ctx->unsynced = false;
+        for (size_t k = 0; k < ctx->host_allocs.size(); k++)
+            if (ctx->host_allocs[k].first == reinterpret_cast<uintptr_t>(ptr)) {
+                ctx->host_allocs.erase(ctx->host_allocs.begin() + (long)k);
+                break;
+            }
     }
     hipHostFree(ptr);  // (ctx may be null: a buffer that outlived its context; its streams are gone)
 }
@@ -575,6 +582,7 @@ int frs_memcpy_d2h(frs_ctx *ctx, void *dst_host, const void *src_dev, int64_t by
 
 int frs_ctx_sync(frs_ctx *ctx) {
     if (!ctx) return FRS_E_ARG;
+    ctx->unsynced = false;
     FRS_HIP(hipStreamSynchronize(ctx->stream));
     return FRS_OK;
 }

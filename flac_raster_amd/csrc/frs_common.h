@@ -56,6 +56,7 @@ struct SubAnalysis {
 constexpr int kFlagConstant = 1;  // CONSTANT subframe (all samples equal and fixed bits[1] == 0)
 constexpr int kFlagFixedOk = 2;   // fixed estimate < subframe bps -> evaluate FIXED
 constexpr int kFlagLpcOk = 4;     // LPC estimate < subframe bps and quantisation succeeded
+constexpr int kFlagZero = 8;      // every sample of the coded signal is 0 (k_zero_subframes: raw-frames tiles)
 
 // Encode job parameters passed to kernels by value.
 struct EncodeParams {

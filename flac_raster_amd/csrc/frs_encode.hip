@@ -528,8 +528,10 @@ template <int DT, bool WIDE, bool ST = false>
 __global__ void __launch_bounds__(128) k_analyze(const typename Elem<DT>::T *raster, EncodeParams P,
                                                 const TileGeom *tiles, const TileNorm *norms,
                                                 const float *__restrict__ window, SubAnalysis *out,
-                                                const int64_t *__restrict__ flist, int64_t nlist) {
+                                                const int64_t *__restrict__ flist, int64_t nlist,
+                                                const uint8_t *__restrict__ skip = nullptr) {
     // flist: the frames to analyse (the fast path's partial last frames), nullptr = every frame of the job.
+    // skip: subframes already analysed (k_zero_subframes), nullptr = none.
     // One lane per coded signal: (frame, channel), or (frame, L/R/M/S) for a two-channel stream (ST).
     using T = typename Elem<DT>::T;
     // sample type: 32 bits except the 33-bit side signal of a 32-bit stereo stream
@@ -537,11 +539,13 @@ __global__ void __launch_bounds__(128) k_analyze(const typename Elem<DT>::T *ras
     using UA = std::make_unsigned_t<XA>;
     const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t nsub = (flist ? nlist : P.nframes) * P.nvch;
-    const bool live = li < nsub;
-    const int64_t fi = live ? li / P.nvch : 0;
-    const int ch = live ? (int)(li - fi * P.nvch) : 0;
+    const bool inrange = li < nsub;
+    const int64_t fi = inrange ? li / P.nvch : 0;
+    const int ch = inrange ? (int)(li - fi * P.nvch) : 0;
     const int64_t f = flist ? flist[fi] : fi;
     const int64_t sub = f * P.nvch + ch;
+    const bool live = inrange && !(skip && skip[sub]);
+    if (skip && __ballot(live) == 0) return;  // (wave-uniform: a wave of skipped subframes walks nothing)
     const int t = tile_of_frame(tiles, P.ntiles, f);
     const TileGeom g = tiles[t];
     const int64_t s0 = (f - g.frame_base) * P.blocksize;
@@ -906,17 +910,55 @@ __global__ void __launch_bounds__(kPartThreads) k_analyze_partial(const typename
     }
 }
 
+// libFLAC 1.4.3 FLAC__fixed_compute_best_predictor_limit_residual's choice from the totals tt / validity of orders
+// 0..4 (CHECK_ORDER_IS_VALID: the estimate of a best-so-far order uses total_error_0, the others are 34.0f), then
+// process_subframe_'s constant test (fixed bits[1] == 0 and `is_constant()`: every sample equal) and the FIXED
+// estimate test against subframe_bps.  Updates A's fixed_order and kFlagConstant / kFlagFixedOk.
+template <typename IsConstant>
+__device__ inline void fixed_wide_decide(SubAnalysis &A, const uint64_t *tt, const bool *valid, int n, int sbps,
+                                         IsConstant is_constant) {
+    uint64_t smallest = UINT64_MAX;
+    int order = 0;
+    float fb[5];
+    const double dn = (double)(n - 4);
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        if (valid[k] && tt[k] < smallest) {
+            order = k;
+            smallest = tt[k];
+            fb[k] = (float)(tt[0] > 0 ? log(M_LN2 * (double)tt[0] / dn) / M_LN2 : 0.0);
+        } else {
+            fb[k] = 34.0f;
+        }
+    }
+    int flags = A.flags & ~(kFlagConstant | kFlagFixedOk);
+    const bool constant = fb[1] == 0.0f && is_constant();
+    if (constant) {
+        A.flags = (flags & ~kFlagLpcOk) | kFlagConstant;
+    } else {
+        A.fixed_order = order;
+        float fg = fb[0];
+#pragma unroll
+        for (int k = 1; k < 5; k++)
+            if (k == order) fg = fb[k];
+        if (!(fg >= (float)sbps)) flags |= kFlagFixedOk;
+        A.flags = flags;
+    }
+}
+
 // 32-bit streams (bits_per_sample 24 -> pyflac bps 32) use libFLAC's limit_residual fixed estimator;
 // it needs 64-bit errors and validity tracking, done in a separate exact pass per lane.
 template <int DT, bool ST = false>
 __global__ void __launch_bounds__(128) k_analyze_fixed_wide(const typename Elem<DT>::T *raster, EncodeParams P,
                                                            const TileGeom *tiles, const TileNorm *norms,
-                                                           SubAnalysis *out) {
+                                                           SubAnalysis *out, const uint8_t *__restrict__ skip = nullptr) {
     // ST: two-channel stream, lanes per (frame, L/R/M/S); the side signal has 33 bits
     // (FLAC__fixed_compute_best_predictor_limit_residual_33bit: the same arithmetic on int64 samples)
+    // skip: subframes already analysed (k_zero_subframes)
     using T = typename Elem<DT>::T;
     const int64_t sub = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (sub >= P.nframes * P.nvch) return;
+    if (skip && skip[sub]) return;
     const int64_t f = sub / P.nvch;
     const int ch = (int)(sub - f * P.nvch);
     const int t = tile_of_frame(tiles, P.ntiles, f);
@@ -967,51 +1009,75 @@ __global__ void __launch_bounds__(128) k_analyze_fixed_wide(const typename Elem<
         h2 = h1;
         h1 = x;
     }
-    // CHECK_ORDER_IS_VALID (fixed.c, limit_residual): estimate uses total_error_0 for every order
-    uint64_t smallest = UINT64_MAX;
-    int order = 0;
-    float fb[5];
-    const double dn = (double)(n - 4);
-#pragma unroll
-    for (int k = 0; k < 5; k++) {
-        if (valid[k] && tt[k] < smallest) {
-            order = k;
-            smallest = tt[k];
-            fb[k] = (float)(tt[0] > 0 ? log(M_LN2 * (double)tt[0] / dn) / M_LN2 : 0.0);
-        } else {
-            fb[k] = 34.0f;
-        }
-    }
-    int flags = A.flags & ~(kFlagConstant | kFlagFixedOk);
-    bool constant = false;
-    if (fb[1] == 0.0f) {
+    fixed_wide_decide(A, tt, valid, n, sbps, [&]() {
         // all samples equal?  (rare; re-walk)
         row = s0 / g.w;
         col = (int)(s0 - row * g.w);
         rowp = tbase + (g.r0 + row) * P.row_stride + g.c0;
         int64_t first = 0;
-        constant = true;
         for (int i = 0; i < n; i++) {
             const int64_t x = next();
             if (i == 0) first = x;
-            else if (x != first) {
-                constant = false;
-                break;
+            else if (x != first) return false;
+        }
+        return true;
+    });
+    out[sub] = A;
+}
+
+// Raw-frames tiles (`convert --spatial`: 32-bit streams of pyflac's truncated floats): a DEM's samples
+// normalise to 0 almost everywhere, and k_analyze / k_analyze_fixed_wide would still walk every such subframe one
+// sample at a time on one lane.  One wave per coded signal (frame, channel) ORs its normalised samples instead (each
+// lane a contiguous run, rows walked by a cursor); an all-zero subframe gets its SubAnalysis here -- the decisions
+// those two kernels make on all-zero sums (generic_decide: no wasted bits, fixed guess 0, no LPC since autoc[0] == 0;
+// the limit_residual estimator: order 0, bits 0), flagged kFlagZero -- and zero[sub] = 1 makes them skip it.
+template <int DT>
+__global__ void __launch_bounds__(256) k_zero_subframes(const typename Elem<DT>::T *raster, EncodeParams P,
+                                                       const TileGeom *tiles, const TileNorm *norms, SubAnalysis *out,
+                                                       uint8_t *zero) {
+    using T = typename Elem<DT>::T;
+    const int64_t sub = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (sub >= P.nframes * P.nvch) return;
+    const int64_t f = sub / P.nvch;
+    const int ch = (int)(sub - f * P.nvch);
+    const int t = tile_of_frame(tiles, P.ntiles, f);
+    const TileGeom g = tiles[t];
+    const int64_t s0 = (f - g.frame_base) * P.blocksize;
+    const int64_t tile_px = (int64_t)g.h * g.w;
+    const int n = (int)((tile_px - s0) < P.blocksize ? (tile_px - s0) : P.blocksize);
+    const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits, P.norm_mode);
+    const int per = (n + 63) / 64;
+    int i = lane * per;
+    const int iend = min(n, i + per);
+    uint32_t o = 0;
+    if (i < iend) {
+        const int64_t q = s0 + i, r = q / g.w;
+        int col = (int)(q - r * g.w);
+        const T *rowp = raster + (int64_t)(P.band0 + ch) * P.band_stride + (g.r0 + r) * P.row_stride + g.c0;
+        for (; i < iend; i++) {
+            o |= (uint32_t)nz(rowp[col]);
+            if (++col == g.w) {
+                col = 0;
+                rowp += P.row_stride;
             }
         }
     }
-    if (constant) {
-        A.flags = (flags & ~kFlagLpcOk) | kFlagConstant;
-    } else {
-        A.fixed_order = order;
-        float fg = fb[0];
+    const bool z = __ballot(o != 0) == 0;
+    if (lane == 0) {
+        zero[sub] = z ? 1 : 0;
+        if (z) {
+            double acc[kMaxLpc + 1];
 #pragma unroll
-        for (int k = 1; k < 5; k++)
-            if (k == order) fg = fb[k];
-        if (!(fg >= (float)sbps)) flags |= kFlagFixedOk;
-        A.flags = flags;
+            for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
+            const uint64_t tt[5] = {0, 0, 0, 0, 0};
+            const bool valid[5] = {true, true, true, true, true};
+            SubAnalysis A = generic_decide<true>(acc, tt, 0, 0, n, P, 0);
+            if (n > 4) fixed_wide_decide(A, tt, valid, n, P.bps - A.wasted, []() { return true; });
+            A.flags |= kFlagZero;
+            out[sub] = A;
+        }
     }
-    out[sub] = A;
 }
 
 // ------------------------------------------------------------------------------ k_encode_frames
@@ -1429,7 +1495,17 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
         const SubAnalysis A = ana[f * P.nvch + v];
         const int w = A.wasted;
         const int sbps = P.bps - w + ((ST && v == 3) ? 1 : 0);
-        load(v, w);
+        // an all-zero subframe (k_zero_subframes: raw-frames tiles) needs no sample load: the signal is zeros, and
+        // decide() runs unchanged on them; its residual codes are written as runs below (WG-uniform)
+        const bool zsub = !ST && (A.flags & kFlagZero) && !cand;
+        if (zsub) {
+            for (int i = tid; i < n; i += kEncThreads) S.xs[xsi(i)] = 0;
+            if (tid < (2 << kMaxPo)) S.psum[tid >> kMaxPo][tid & ((1 << kMaxPo) - 1)] = 0;
+            if (tid == 0) S.lpc_bad = 0;
+            __syncthreads();
+        } else {
+            load(v, w);
+        }
         int type;
         const RiceChoice *rcp;
         const LpcCand *lcp;
@@ -1487,6 +1563,23 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
             const int pbits = rc.rice2 ? 5 : 4;
             const int po = rc.order;
             const int ps = n >> po;
+            bool k0 = zsub;
+            for (int p = 0; p < (1 << po) && k0; p++) k0 = rc.k[p] == 0;
+            if (k0) {
+                // all residuals 0 with parameter 0 in every partition: each code is the single stop bit '1' and the
+                // parameter fields are zeros, so partition p is one run of ones after its field
+                for (int p = 0; p < (1 << po); p++) {
+                    const uint64_t before = p ? (uint64_t)p * ps - o : 0;  // codes of the earlier partitions
+                    const uint64_t a = pos + (uint64_t)pbits * (p + 1) + before;
+                    const uint64_t b = a + (uint64_t)(ps - (p ? 0 : o));
+                    for (uint64_t wd = (a >> 5) + tid; wd <= ((b - 1) >> 5) && b > a; wd += kEncThreads) {
+                        const uint64_t lo = a > wd * 32 ? a : wd * 32, hi = b < wd * 32 + 32 ? b : wd * 32 + 32;
+                        const uint32_t nb = (uint32_t)(hi - lo), sh = (uint32_t)(wd * 32 + 32 - hi);
+                        atomicOr(&S.bits[wd], (nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1u)) << sh);
+                    }
+                }
+                sub_end = pos + (uint64_t)pbits * (1 << po) + (uint64_t)(n - o);
+            } else {
             // per-thread code lengths of its chunk, then block exclusive scan
             uint64_t my = 0;
             for (int i = max(i_beg, o); i < i_end; i++) {
@@ -1536,6 +1629,7 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
             __syncthreads();
             for (int p = tid; p < (1 << po); p += kEncThreads)
                 put_bits(S.bits, pos + (uint64_t)pbits * p + pstart[p], rc.k[p], pbits);
+            }
         }
         __syncthreads();
         // ---- flush complete words of S.bits to the slot, keep the partial word
@@ -4585,9 +4679,16 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                 k_analyze_lpc_hi<DT, true, true><<<agrid, 128, 0, st>>>(raster, P, dtiles, dnorms,
                                                                         ctx->window_hi.as<float>(), dana, dcand, lv.parts);
         } else {
+            // raw-frames tiles: all-zero subframes analysed by a coalesced pass, skipped by the lane walks
+            uint8_t *zero = nullptr;
+            if (!dcand) {
+                FRS_HIP(ctx->zero_sub.ensure((size_t)nsub + 64));
+                zero = ctx->zero_sub.as<uint8_t>();
+                k_zero_subframes<DT><<<(unsigned)((nsub + 3) / 4), 256, 0, st>>>(raster, Pa, dtiles, dnorms, dana, zero);
+            }
             k_analyze<DT, true><<<agrid, 128, 0, st>>>(raster, Pa, dtiles, dnorms, ctx->window.as<float>(), dana,
-                                                         nullptr, 0);
-            k_analyze_fixed_wide<DT><<<agrid, 128, 0, st>>>(raster, Pa, dtiles, dnorms, dana);
+                                                         nullptr, 0, zero);
+            k_analyze_fixed_wide<DT><<<agrid, 128, 0, st>>>(raster, Pa, dtiles, dnorms, dana, zero);
             if (dcand)
                 k_analyze_lpc_hi<DT, true><<<agrid, 128, 0, st>>>(raster, P, dtiles, dnorms, ctx->window_hi.as<float>(),
                                                                   dana, dcand, lv.parts);
@@ -4690,6 +4791,7 @@ static int run_encode_any(frs_ctx *ctx, const frs_encode_desc *d, const void *ra
 int encode_job(frs_ctx *ctx, const frs_encode_desc *d, const void *raster_dev, void *arena_dev, int64_t arena_cap,
                int64_t *tile_off, double *tile_min, double *tile_max, int32_t *stream_bps) {
     if (stream_bps) *stream_bps = stream_bps_of(d);
+    if (const int rc = check_unsynced(ctx)) return rc;
 #ifdef FRS_PROBE_I16  // (register probes: tools/kernel_regs.py --probe compiles the int16 kernels only)
     return run_encode_any<FRS_DT_I16>(ctx, d, raster_dev, arena_dev, arena_cap, tile_off, tile_min, tile_max);
 #else

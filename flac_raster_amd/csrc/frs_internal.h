@@ -102,6 +102,18 @@ struct frs_ctx {
     DevBuf lpc_cand, window_hi, loose_assign, loose_lead;
     int window_hi_bs = 0, window_hi_parts = 0;
     DevBuf sub_est, st_pick;  // two-channel fast path: subframe estimates (L, R, M, S), the assignment per frame
+    DevBuf zero_sub;          // raw-frames tiles: all-zero subframe flags (k_zero_subframes)
+    // page-locked host allocations of this context (frs_host_malloc): a C5 decode whose output lies in one returns
+    // when the kernel's last work-group has published it, before the stream's completion signal (`unsynced` then
+    // makes the next call check the stream for an asynchronous fault first)
+    std::vector<std::pair<uintptr_t, size_t>> host_allocs;
+    bool unsynced = false;
+    bool is_host_alloc(const void *p, size_t n) const {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+        for (const auto &r : host_allocs)
+            if (a >= r.first && a + n <= r.first + r.second) return true;
+        return false;
+    }
 };
 
 #define FRS_HIP(call)                                                                  \
@@ -114,6 +126,18 @@ struct frs_ctx {
     } while (0)
 
 namespace frs {
+// A call after an early-returning C5 decode (frs_ctx::unsynced): a fault of that kernel surfaces here, in the next
+// call on the context, instead of in some later unrelated HIP call.
+inline int check_unsynced(frs_ctx *ctx) {
+    if (!ctx->unsynced) return FRS_OK;
+    ctx->unsynced = false;
+    const hipError_t e = hipStreamQuery(ctx->stream);
+    if (e != hipSuccess && e != hipErrorNotReady) {
+        ctx->err = std::string("an earlier decode's kernel failed: ") + hipGetErrorString(e);
+        return FRS_E_HIP;
+    }
+    return FRS_OK;
+}
 // Kernel timing helpers (no-ops unless ctx->prof).
 void prof_begin(frs_ctx *ctx, const char *name, hipEvent_t *start, hipStream_t s = nullptr);
 void prof_end(frs_ctx *ctx, const char *name, hipEvent_t start, hipStream_t s = nullptr);

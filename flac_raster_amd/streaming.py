@@ -349,25 +349,35 @@ def select_frame(index: Dict, tile_id: Optional[int] = None, last: bool = False,
     raise ValueError("Must specify --tile-id, --bbox, --center, or --last")
 
 
-_GRID_CACHE: List[Tuple[Dict, int, Optional[tuple]]] = []  # (index, len(frames), grid) of recently queried indexes
+_GRID_CACHE: List[Tuple[tuple, Optional[tuple]]] = []  # (fingerprint, grid) of recently queried indexes
+
+
+def _grid_key(index: Dict) -> tuple:
+    """What the derived grid depends on, besides the frames' bboxes (read live at query time): the index object,
+    its frame count and the tile geometry.  No reference to the index is kept (a dropped index is not pinned in
+    memory); an index whose geometry or frame list length changes in place gets a new grid."""
+    t = index.get("transform")
+    return (id(index), id(index["frames"]), len(index["frames"]), index.get("tile_size"), index.get("width"),
+            index.get("height"), tuple(t) if t else None)
 
 
 def _grid_of(index: Dict) -> Optional[tuple]:
     """The row-major tile grid of an index as create-streaming writes it (tile size, columns, rows, the transform's
-    scale/offset terms, the frames' bboxes as tuples), or None when the index is not that grid.  Derived once per
-    index object (a bbox query is latency-bound: the per-query dict walks cost more than the tests themselves)."""
+    scale/offset terms), or None when the index is not that grid.  Derived once per index geometry (a bbox query
+    is latency-bound: the per-query dict walks cost more than the tests themselves).  The frames' bboxes are not
+    cached: first_intersecting reads them from the index on every query."""
     frames = index["frames"]
-    for idx, n, g in _GRID_CACHE:
-        if idx is index and n == len(frames):
+    key = _grid_key(index)
+    for k, g in _GRID_CACHE:
+        if k == key:
             return g
     T, W, H, t = index.get("tile_size"), index.get("width"), index.get("height"), index.get("transform")
     g = None
     if T and W and H and t and len(t) >= 6 and t[1] == 0 and t[3] == 0 and t[0] != 0 and t[4] != 0:
         tc, tr = -(-int(W) // int(T)), -(-int(H) // int(T))
         if len(frames) == tc * tr and all(fr["frame_id"] == k for k, fr in enumerate(frames)):
-            g = (int(T), tc, tr, float(t[0]), float(t[2]), float(t[4]), float(t[5]),
-                 [tuple(fr["bbox"]) for fr in frames])
-    _GRID_CACHE.insert(0, (index, len(frames), g))
+            g = (int(T), tc, tr, float(t[0]), float(t[2]), float(t[4]), float(t[5]))
+    _GRID_CACHE.insert(0, (key, g))
     del _GRID_CACHE[8:]
     return g
 
@@ -380,7 +390,8 @@ def first_intersecting(index: Dict, bbox: Sequence[float]) -> Optional[Dict]:
     if g is None:
         hits = intersecting(index, bbox)
         return hits[0] if hits else None
-    T, tc, tr, a, c, e, f, boxes = g
+    T, tc, tr, a, c, e, f = g
+    frames = index["frames"]
     x0, y0, x1, y1 = bbox
     ca, cb = (x0 - c) / a, (x1 - c) / a
     if cb < ca:
@@ -394,9 +405,10 @@ def first_intersecting(index: Dict, bbox: Sequence[float]) -> Optional[Dict]:
     for r in range(rt0, rt1 + 1):
         k = r * tc
         for cc in range(ct0, ct1 + 1):
-            b = boxes[k + cc]
+            fr = frames[k + cc]
+            b = fr["bbox"]
             if x0 < b[2] and x1 > b[0] and y0 < b[3] and y1 > b[1]:
-                return index["frames"][k + cc]
+                return fr
     return None
 
 

@@ -113,6 +113,16 @@ def test_first_intersecting_matches_linear_scan():
         hits = streaming.intersecting(index, bbox)
         got = streaming.first_intersecting(index, bbox)
         assert (got is None and not hits) or (hits and got is hits[0]), bbox
+    # an index mutated in place after its first query: a bbox rewritten, then the tile size changed --
+    # the grid accelerator follows the live index, never a cached copy of it
+    bbox = list(frames[5]["bbox"])
+    assert streaming.first_intersecting(index, bbox) is frames[5]
+    frames[5]["bbox"] = [b + 1e7 for b in frames[5]["bbox"]]
+    hits = streaming.intersecting(index, bbox)
+    assert streaming.first_intersecting(index, bbox) is (hits[0] if hits else None) and frames[5] not in hits
+    index["tile_size"] = 1024
+    assert streaming._grid_of(index) is None  # no longer the 1024-px grid of these 24 frames: linear scan
+    assert streaming.first_intersecting(index, bbox) is (hits[0] if hits else None)
 
 
 @pytest.mark.parametrize("crs,dtype,tr", [

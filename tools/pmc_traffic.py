@@ -33,7 +33,11 @@ def per_dispatch(d, counter):
     out = defaultdict(list)
     for k, v in vals.items():
         out[names[k]].append(v)
+    CALLS.update({k: len(v) for k, v in out.items()})
     return {k: sum(v) / len(v) for k, v in out.items()}
+
+
+CALLS = {}  # dispatches per kernel in the last pass read
 
 
 def main():
@@ -46,7 +50,7 @@ def main():
     for k in sorted(set(fr) | set(wr)):
         rd = 2 * fr.get(k, 0.0) * 1024
         wb = wr.get(k, 0.0) * 1024
-        kernels[k] = {"read_bytes": rd, "write_bytes": wb, "bytes": rd + wb}
+        kernels[k] = {"read_bytes": rd, "write_bytes": wb, "bytes": rd + wb, "calls": CALLS.get(k, 0)}
     if "--valu" in sys.argv:
         for k, v in per_dispatch(sys.argv[sys.argv.index("--valu") + 1], "SQ_INSTS_VALU").items():
             kernels.setdefault(k, {})["valu_insts"] = v
