@@ -2324,16 +2324,15 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     int i = head;
     // whole 64-sample groups, fully unrolled, two samples per step on pair-aligned history: Q[m] = (x[2m+1] << 16 |
     // x[2m] & 0xffff), the output layout, in a four-register ring renamed by the unroll (no per-sample shifting of the
-    // history).  x[2m] = r + (sum q.x >> shift): the pairs Q[m-2..m-4] against C'[k] = (q[2k] << 16 | q[2k+1]) by
-    // dot2, the newest pair's two samples x[2m-2], x[2m-1] by 24-bit multiply-adds (q1, q0); x[2m+1] the same pairs
-    // against D'[k] = (q[2k+1] << 16 | q[2k+2]) and q2 x[2m-2] + q1 x[2m-1] + q0 x[2m].  Only q0 x[i-1], the add and
-    // the shift wait on the previous sample (round 5 took the newest pair through a dot2 after re-packing it: perm,
-    // dot2, shift, mul24, add, shift per pair on the chain; tools/micro/restore_chain.hip measures both).  Integer
-    // sums in wrapping int32 (the pipe path is 32-bit-safe: prec + sbps + log2(order) <= 31), so the regrouping is
-    // exact.  Residual j of the group by v_readlane with an immediate lane index.
+    // history).  x[2m] = r + (sum_k dot2(Q[m-1-k], C'[k]) >> shift), C'[k] = (q[2k] << 16 | q[2k+1]); x[2m+1] adds
+    // q[0] x[2m] to dot2s of the same pairs against D'[k] = (q[2k+1] << 16 | q[2k+2]).  Residual j of the group by
+    // v_readlane with an immediate lane index.  (Per sample ~8.5 instructions instead of ~12: the lone consumer wave
+    // issues one every ~8 cycles.)  Round 6: taking the newest pair's two samples off the dot2 (24-bit multiply-adds,
+    // four dependent operations per pair instead of six) is not faster: tools/micro/restore_chain.hip 25.6 (this
+    // form) / 27.9 / 26.9 ns per sample, C5 decode_frames 0.104 ms either way (one box, one call).
     if (!failed && i + 64 <= bs) {
         auto pk = [](int32_t hi, int32_t lo) { return ((uint32_t)hi << 16) | ((uint32_t)lo & 0xFFFFu); };
-        const int32_t q0 = info.cq[0], q1 = info.cq[1], q2 = info.cq[2];
+        const int32_t q0 = info.cq[0];
         uint32_t Ce[4], Co[4], Qr[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
@@ -2343,7 +2342,6 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
         __builtin_amdgcn_s_waitcnt(0xC07F);  // the head's pairs are in xout
 #pragma unroll
         for (int k = 0; k < 4; k++) Qr[3 - k] = i ? xout[(i >> 1) - 1 - k] : 0u;  // Qr[3] = Q[m-1] .. Qr[0] = Q[m-4]
-        int32_t xe_p = (int32_t)(int16_t)(Qr[3] & 0xFFFFu), xo_p = (int32_t)(int16_t)(Qr[3] >> 16);
         for (; i + 64 <= bs; i += 64) {
             if (!wait_for(i + 64)) {
                 failed = true;
@@ -2358,23 +2356,20 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
                 // and seed the dot2 accumulators (no per-sample v_readlane + v_mov)
                 if (!(p2 & 1)) rr = rp[p2 >> 1];
                 const int32_t Re = (p2 & 1) ? rr.z : rr.x, Ro = (p2 & 1) ? rr.w : rr.y;
-                const uint32_t B = Qr[(p2 + 2) & 3], Cc = Qr[(p2 + 1) & 3], Dd = Qr[p2 & 3];
+                const uint32_t A = Qr[(p2 + 3) & 3], B = Qr[(p2 + 2) & 3], Cc = Qr[(p2 + 1) & 3], Dd = Qr[p2 & 3];
                 int32_t pe = dec_dot2(Dd, Ce[3], Re);
                 pe = dec_dot2(Cc, Ce[2], pe);
                 pe = dec_dot2(B, Ce[1], pe);
                 int32_t po = dec_dot2(Dd, Co[3], Ro);
                 po = dec_dot2(Cc, Co[2], po);
                 po = dec_dot2(B, Co[1], po);
-                pe = __mul24(q1, xe_p) + pe;
-                po = __mul24(q2, xe_p) + po;
-                po = __mul24(q1, xo_p) + po;
-                const int32_t xe = (__mul24(q0, xo_p) + pe) >> shift;
+                po = dec_dot2(A, Co[0], po);
+                pe = dec_dot2(A, Ce[0], pe);
+                const int32_t xe = pe >> shift;
                 const int32_t xo = (__mul24(q0, xe) + po) >> shift;
                 const uint32_t qn = __builtin_amdgcn_perm((uint32_t)xo, (uint32_t)xe, 0x05040100u);
                 xp[p2] = qn;
                 Qr[p2 & 3] = qn;
-                xe_p = xe;
-                xo_p = xo;
             }
         }
 #pragma unroll

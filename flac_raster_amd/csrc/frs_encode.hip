@@ -1025,61 +1025,6 @@ __global__ void __launch_bounds__(128) k_analyze_fixed_wide(const typename Elem<
     out[sub] = A;
 }
 
-// Raw-frames tiles (`convert --spatial`: 32-bit streams of pyflac's truncated floats, SURVEY Q1): a DEM's samples
-// normalise to 0 almost everywhere, and k_analyze / k_analyze_fixed_wide would still walk every such subframe one
-// sample at a time on one lane.  One wave per coded signal (frame, channel) ORs its normalised samples instead (each
-// lane a contiguous run, rows walked by a cursor); an all-zero subframe gets its SubAnalysis here -- the decisions
-// those two kernels make on all-zero sums (generic_decide: no wasted bits, fixed guess 0, no LPC since autoc[0] == 0;
-// the limit_residual estimator: order 0, bits 0), flagged kFlagZero -- and zero[sub] = 1 makes them skip it.
-template <int DT>
-__global__ void __launch_bounds__(256) k_zero_subframes(const typename Elem<DT>::T *raster, EncodeParams P,
-                                                       const TileGeom *tiles, const TileNorm *norms, SubAnalysis *out,
-                                                       uint8_t *zero) {
-    using T = typename Elem<DT>::T;
-    const int64_t sub = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (sub >= P.nframes * P.nvch) return;
-    const int64_t f = sub / P.nvch;
-    const int ch = (int)(sub - f * P.nvch);
-    const int t = tile_of_frame(tiles, P.ntiles, f);
-    const TileGeom g = tiles[t];
-    const int64_t s0 = (f - g.frame_base) * P.blocksize;
-    const int64_t tile_px = (int64_t)g.h * g.w;
-    const int n = (int)((tile_px - s0) < P.blocksize ? (tile_px - s0) : P.blocksize);
-    const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits, P.norm_mode);
-    const int per = (n + 63) / 64;
-    int i = lane * per;
-    const int iend = min(n, i + per);
-    uint32_t o = 0;
-    if (i < iend) {
-        const int64_t q = s0 + i, r = q / g.w;
-        int col = (int)(q - r * g.w);
-        const T *rowp = raster + (int64_t)(P.band0 + ch) * P.band_stride + (g.r0 + r) * P.row_stride + g.c0;
-        for (; i < iend; i++) {
-            o |= (uint32_t)nz(rowp[col]);
-            if (++col == g.w) {
-                col = 0;
-                rowp += P.row_stride;
-            }
-        }
-    }
-    const bool z = __ballot(o != 0) == 0;
-    if (lane == 0) {
-        zero[sub] = z ? 1 : 0;
-        if (z) {
-            double acc[kMaxLpc + 1];
-#pragma unroll
-            for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
-            const uint64_t tt[5] = {0, 0, 0, 0, 0};
-            const bool valid[5] = {true, true, true, true, true};
-            SubAnalysis A = generic_decide<true>(acc, tt, 0, 0, n, P, 0);
-            if (n > 4) fixed_wide_decide(A, tt, valid, n, P.bps - A.wasted, []() { return true; });
-            A.flags |= kFlagZero;
-            out[sub] = A;
-        }
-    }
-}
-
 // ------------------------------------------------------------------------------ k_encode_frames
 constexpr int kEncThreads = 256;
 constexpr int kBitWords = 4096 + 64;  // one 32-bit subframe (4096 x 32 bits) + headers + carry
@@ -1207,6 +1152,70 @@ template <typename XT> struct EncShared {
     int assign;          // FLAC__ChannelAssignment: 0 independent, 1 left-side, 2 right-side, 3 mid-side
 };
 
+// Frame header of a generic-path frame (RFC 9639 9.1; libFLAC FLAC__frame_add_header) into h: fixed blocksize,
+// frame number fk (UTF-8), sample rate and bps codes, channel assignment code cac, CRC-8; returns its bytes
+__device__ inline int generic_frame_header(uint8_t *h, int n, const EncodeParams &P, int cac, uint32_t fk) {
+    int hb = 0;
+    int bsc, bsx = 0;
+    switch (n) {
+    case 192: bsc = 1; break;
+    case 576: bsc = 2; break;
+    case 1152: bsc = 3; break;
+    case 2304: bsc = 4; break;
+    case 4608: bsc = 5; break;
+    case 256: bsc = 8; break;
+    case 512: bsc = 9; break;
+    case 1024: bsc = 10; break;
+    case 2048: bsc = 11; break;
+    case 4096: bsc = 12; break;
+    case 8192: bsc = 13; break;
+    case 16384: bsc = 14; break;
+    case 32768: bsc = 15; break;
+    default: bsc = bsx = (n <= 256 ? 6 : 7); break;
+    }
+    int src, srx = 0;
+    const int sr = P.sample_rate;
+    switch (sr) {
+    case 88200: src = 1; break;
+    case 176400: src = 2; break;
+    case 192000: src = 3; break;
+    case 8000: src = 4; break;
+    case 16000: src = 5; break;
+    case 22050: src = 6; break;
+    case 24000: src = 7; break;
+    case 32000: src = 8; break;
+    case 44100: src = 9; break;
+    case 48000: src = 10; break;
+    case 96000: src = 11; break;
+    default:
+        if (sr <= 255000 && sr % 1000 == 0) src = srx = 12;
+        else if (sr % 10 == 0 && sr / 10 <= 65535) src = srx = 14;
+        else src = srx = 13;
+    }
+    int bpc = P.bps == 8 ? 1 : P.bps == 12 ? 2 : P.bps == 16 ? 4 : P.bps == 20 ? 5 : P.bps == 24 ? 6 : P.bps == 32 ? 7 : 0;
+    // channel assignment: nch - 1 (independent), 8 left-side, 9 right-side, 10 mid-side
+    h[hb++] = 0xFF;
+    h[hb++] = 0xF8;
+    h[hb++] = (uint8_t)((bsc << 4) | src);
+    h[hb++] = (uint8_t)((cac << 4) | (bpc << 1));
+    const uint32_t v = fk;
+    if (v < 0x80) h[hb++] = (uint8_t)v;
+    else if (v < 0x800) { h[hb++] = (uint8_t)(0xC0 | (v >> 6)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+    else if (v < 0x10000) { h[hb++] = (uint8_t)(0xE0 | (v >> 12)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+    else if (v < 0x200000) { h[hb++] = (uint8_t)(0xF0 | (v >> 18)); h[hb++] = (uint8_t)(0x80 | ((v >> 12) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+    else if (v < 0x4000000) { h[hb++] = (uint8_t)(0xF8 | (v >> 24)); h[hb++] = (uint8_t)(0x80 | ((v >> 18) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 12) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+    else { h[hb++] = (uint8_t)(0xFC | (v >> 30)); h[hb++] = (uint8_t)(0x80 | ((v >> 24) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 18) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 12) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
+    if (bsx == 6) h[hb++] = (uint8_t)(n - 1);
+    else if (bsx == 7) { h[hb++] = (uint8_t)((n - 1) >> 8); h[hb++] = (uint8_t)(n - 1); }
+    if (srx == 12) h[hb++] = (uint8_t)(sr / 1000);
+    else if (srx == 13) { h[hb++] = (uint8_t)(sr >> 8); h[hb++] = (uint8_t)sr; }
+    else if (srx == 14) { h[hb++] = (uint8_t)((sr / 10) >> 8); h[hb++] = (uint8_t)(sr / 10); }
+    uint8_t c = 0;
+    for (int i = 0; i < hb; i++) c = c_crc8[c ^ h[i]];
+    h[hb++] = c;
+    return hb;
+}
+
 // workgroup = frame.  ST: a two-channel stream -- the four signals L, R, M, S are evaluated (process_subframe_ each),
 // the assignment with the fewest estimated bits wins (stream_encoder.c process_subframes_, do_mid_side_stereo &&
 // !loose: independent, left-side, right-side, mid-side; a later one only if strictly smaller) and its two subframes
@@ -1245,6 +1254,13 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
     const int max_po_block = min(P.max_po, __builtin_ctz((unsigned)n));  // level 5: kMaxPartOrder
     const int chunk = (n + kEncThreads - 1) / kEncThreads;
     const int i_beg = tid * chunk, i_end = min(n, i_beg + chunk);
+    if constexpr (!ST) {
+        if (!flist && !cand && n > 4) {  // every subframe all-zero: k_zero_frames_emit writes this frame
+            bool all0 = true;
+            for (int c = 0; c < P.nch; c++) all0 = all0 && (ana[f * P.nvch + c].flags & kFlagZero);
+            if (all0) return;
+        }
+    }
 
     for (int i = tid; i < kWords; i += kEncThreads) S.bits[i] = 0;
     __syncthreads();
@@ -1419,65 +1435,9 @@ __global__ void __launch_bounds__(kEncThreads) k_encode_frames(const typename El
         __shared__ int hdr_bits;
         if (tid == 0) {
             uint8_t h[16];
-            int hb = 0;
-            int bsc, bsx = 0;
-            switch (n) {
-            case 192: bsc = 1; break;
-            case 576: bsc = 2; break;
-            case 1152: bsc = 3; break;
-            case 2304: bsc = 4; break;
-            case 4608: bsc = 5; break;
-            case 256: bsc = 8; break;
-            case 512: bsc = 9; break;
-            case 1024: bsc = 10; break;
-            case 2048: bsc = 11; break;
-            case 4096: bsc = 12; break;
-            case 8192: bsc = 13; break;
-            case 16384: bsc = 14; break;
-            case 32768: bsc = 15; break;
-            default: bsc = bsx = (n <= 256 ? 6 : 7); break;
-            }
-            int src, srx = 0;
-            const int sr = P.sample_rate;
-            switch (sr) {
-            case 88200: src = 1; break;
-            case 176400: src = 2; break;
-            case 192000: src = 3; break;
-            case 8000: src = 4; break;
-            case 16000: src = 5; break;
-            case 22050: src = 6; break;
-            case 24000: src = 7; break;
-            case 32000: src = 8; break;
-            case 44100: src = 9; break;
-            case 48000: src = 10; break;
-            case 96000: src = 11; break;
-            default:
-                if (sr <= 255000 && sr % 1000 == 0) src = srx = 12;
-                else if (sr % 10 == 0 && sr / 10 <= 65535) src = srx = 14;
-                else src = srx = 13;
-            }
-            int bpc = P.bps == 8 ? 1 : P.bps == 12 ? 2 : P.bps == 16 ? 4 : P.bps == 20 ? 5 : P.bps == 24 ? 6 : P.bps == 32 ? 7 : 0;
             // channel assignment: nch - 1 (independent), 8 left-side, 9 right-side, 10 mid-side
-            const int cac = ST ? (S.assign == 0 ? 1 : 7 + S.assign) : P.nch - 1;
-            h[hb++] = 0xFF;
-            h[hb++] = 0xF8;
-            h[hb++] = (uint8_t)((bsc << 4) | src);
-            h[hb++] = (uint8_t)((cac << 4) | (bpc << 1));
-            const uint32_t v = (uint32_t)fk;
-            if (v < 0x80) h[hb++] = (uint8_t)v;
-            else if (v < 0x800) { h[hb++] = (uint8_t)(0xC0 | (v >> 6)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
-            else if (v < 0x10000) { h[hb++] = (uint8_t)(0xE0 | (v >> 12)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
-            else if (v < 0x200000) { h[hb++] = (uint8_t)(0xF0 | (v >> 18)); h[hb++] = (uint8_t)(0x80 | ((v >> 12) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
-            else if (v < 0x4000000) { h[hb++] = (uint8_t)(0xF8 | (v >> 24)); h[hb++] = (uint8_t)(0x80 | ((v >> 18) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 12) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
-            else { h[hb++] = (uint8_t)(0xFC | (v >> 30)); h[hb++] = (uint8_t)(0x80 | ((v >> 24) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 18) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 12) & 0x3F)); h[hb++] = (uint8_t)(0x80 | ((v >> 6) & 0x3F)); h[hb++] = (uint8_t)(0x80 | (v & 0x3F)); }
-            if (bsx == 6) h[hb++] = (uint8_t)(n - 1);
-            else if (bsx == 7) { h[hb++] = (uint8_t)((n - 1) >> 8); h[hb++] = (uint8_t)(n - 1); }
-            if (srx == 12) h[hb++] = (uint8_t)(sr / 1000);
-            else if (srx == 13) { h[hb++] = (uint8_t)(sr >> 8); h[hb++] = (uint8_t)sr; }
-            else if (srx == 14) { h[hb++] = (uint8_t)((sr / 10) >> 8); h[hb++] = (uint8_t)(sr / 10); }
-            uint8_t c = 0;
-            for (int i = 0; i < hb; i++) c = c_crc8[c ^ h[i]];
-            h[hb++] = c;
+            const int hb = generic_frame_header(h, n, P, ST ? (S.assign == 0 ? 1 : 7 + S.assign) : P.nch - 1,
+                                                (uint32_t)fk);
             for (int i = 0; i < hb; i++) put_bits(S.bits, (uint64_t)i * 8, h[i], 8);
             hdr_bits = hb * 8;
         }
@@ -2054,6 +2014,122 @@ template <int DT, int N> struct ChunkN {
         else load_gather(base, row_stride, width, row, col, nvalid);
     }
 };
+
+// Raw-frames tiles (`convert --spatial`: 32-bit streams of pyflac's truncated floats, SURVEY Q1): a DEM's samples
+// normalise to 0 almost everywhere, and k_analyze / k_analyze_fixed_wide would still walk every such subframe one
+// sample at a time on one lane.  One wave per coded signal (frame, channel) ORs its normalised samples instead (each
+// lane 64 consecutive samples, vector loads when the tile width is a multiple of 64 and the rows are aligned); an
+// all-zero subframe gets its SubAnalysis here -- the decisions those two kernels make on all-zero sums
+// (generic_decide: no wasted bits, fixed guess 0, no LPC since autoc[0] == 0; the limit_residual estimator: order 0,
+// bits 0), flagged kFlagZero -- and zero[sub] = 1 makes them skip it.
+template <int DT>
+__global__ void __launch_bounds__(256) k_zero_subframes(const typename Elem<DT>::T *raster, EncodeParams P,
+                                                       const TileGeom *tiles, const TileNorm *norms, SubAnalysis *out,
+                                                       uint8_t *zero) {
+    using T = typename Elem<DT>::T;
+    const int64_t sub = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (sub >= P.nframes * P.nvch) return;
+    const int64_t f = sub / P.nvch;
+    const int ch = (int)(sub - f * P.nvch);
+    const int t = tile_of_frame(tiles, P.ntiles, f);
+    const TileGeom g = tiles[t];
+    const int64_t s0 = (f - g.frame_base) * P.blocksize;
+    const int64_t tile_px = (int64_t)g.h * g.w;
+    const int n = (int)((tile_px - s0) < P.blocksize ? (tile_px - s0) : P.blocksize);
+    const Normalizer<DT> nz = make_norm<DT>(norms[t], P.scale_bits, P.norm_mode);
+    const T *band = raster + (int64_t)(P.band0 + ch) * P.band_stride + g.r0 * P.row_stride + g.c0;
+    uint32_t o = 0;
+    for (int i0 = 64 * lane; i0 < n; i0 += 64 * 64) {  // (blocksize 4096: one pass)
+        const int64_t q = s0 + i0, r = q / g.w;
+        const int col = (int)(q - r * g.w);
+        const int cnt = n - i0 < 64 ? n - i0 : 64;
+        const int vec = (cnt == 64 && (g.w % 64) == 0) ? P.vec_ok : 0;
+        if constexpr (sizeof(T) <= 4) {
+            if (vec) {
+                Chunk64<DT> chk;
+                chk.load(band, P.row_stride, g.w, r, col, vec, 64);
+#pragma unroll
+                for (int j = 0; j < 64; j++) o |= (uint32_t)nz(chk.get(j));
+                continue;
+            }
+        }
+        int c = col;
+        const T *rowp = band + r * P.row_stride;
+        for (int j = 0; j < cnt; j++) {
+            o |= (uint32_t)nz(rowp[c]);
+            if (++c == g.w) {
+                c = 0;
+                rowp += P.row_stride;
+            }
+        }
+    }
+    const bool z = __ballot(o != 0) == 0;
+    if (lane == 0) {
+        zero[sub] = z ? 1 : 0;
+        if (z) {
+            double acc[kMaxLpc + 1];
+#pragma unroll
+            for (int l = 0; l <= kMaxLpc; l++) acc[l] = 0.0;
+            const uint64_t tt[5] = {0, 0, 0, 0, 0};
+            const bool valid[5] = {true, true, true, true, true};
+            SubAnalysis A = generic_decide<true>(acc, tt, 0, 0, n, P, 0);
+            if (n > 4) fixed_wide_decide(A, tt, valid, n, P.bps - A.wasted, []() { return true; });
+            A.flags |= kFlagZero;
+            out[sub] = A;
+        }
+    }
+}
+
+// A frame whose every subframe is all-zero (kFlagZero, more than 4 samples): what k_encode_frames writes for it,
+// without its work-group per frame -- decide() on all-zero sums keeps FIXED order 0 (the verbatim, LPC and constant
+// candidates are out: no LPC since autoc[0] == 0, and the limit_residual estimator's bits[1] is 34), and libFLAC's
+// Rice estimate (set_partitioned_rice_) is 4 + ceil(ns / 2) bits per partition at parameter 0, so partition order 0
+// wins.  Subframe: 8 header bits (0x10: FIXED, order 0, no wasted bits), RICE method and partition order (6 zero bits),
+// the parameter 0 (4 bits), then n codes of the single stop bit '1'.  One wave per frame writes the frame's words to
+// its slot (byte order, as k_encode_frames' flush) and its byte count incl. the CRC-16 footer (k_compact adds it).
+__global__ void __launch_bounds__(256) k_zero_frames_emit(EncodeParams P, const TileGeom *tiles,
+                                                         const SubAnalysis *ana, uint32_t *slots,
+                                                         int64_t *frame_bytes) {
+    const int64_t f = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (f >= P.nframes) return;
+    bool all0 = true;
+    for (int c = 0; c < P.nch; c++) all0 = all0 && (ana[f * P.nvch + c].flags & kFlagZero);
+    const int t = tile_of_frame(tiles, P.ntiles, f);
+    const TileGeom g = tiles[t];
+    const int64_t fk = f - g.frame_base;
+    const int64_t tile_px = (int64_t)g.h * g.w;
+    const int n = (int)((tile_px - fk * P.blocksize) < P.blocksize ? (tile_px - fk * P.blocksize) : P.blocksize);
+    if (!all0 || n <= 4) return;  // (k_encode_frames codes it)
+    uint8_t h[16];
+    const int hb = generic_frame_header(h, n, P, P.nch - 1, (uint32_t)fk);
+    const uint32_t hbits = (uint32_t)hb * 8, sbits = 18u + (uint32_t)n;
+    const uint32_t bits = hbits + (uint32_t)P.nch * sbits;
+    const uint32_t nwords = (bits + 31) >> 5;
+    uint32_t *slot = slots + (size_t)f * P.slot_words;
+    for (uint32_t wi = (uint32_t)lane; wi < nwords; wi += 64) {
+        uint32_t v = 0;  // MSB-first bits [32 wi, 32 wi + 32)
+        for (int k = 0; k < 4; k++) {
+            const uint32_t byte = 4 * wi + (uint32_t)k;
+            if (byte < (uint32_t)hb) v |= (uint32_t)h[byte] << (24 - 8 * k);
+        }
+        for (int c = 0; c < P.nch; c++) {
+            const uint32_t b0 = hbits + (uint32_t)c * sbits;
+            // 0x10 at [b0, b0 + 8): its one bit at b0 + 3; ones at [b0 + 18, b0 + sbits)
+            const uint32_t one = b0 + 3;
+            if (one >= 32 * wi && one < 32 * wi + 32) v |= 0x80000000u >> (one - 32 * wi);
+            const uint32_t a = b0 + 18, e = b0 + sbits;
+            const uint32_t lo = a > 32 * wi ? a : 32 * wi, hi = e < 32 * wi + 32 ? e : 32 * wi + 32;
+            if (hi > lo) {
+                const uint32_t nb = hi - lo, sh = 32 * wi + 32 - hi;
+                v |= (nb == 32 ? 0xFFFFFFFFu : ((1u << nb) - 1u)) << sh;
+            }
+        }
+        slot[wi] = __builtin_bswap32(v);
+    }
+    if (lane == 0) frame_bytes[f] = (int64_t)((bits + 7) >> 3) + 2;
+}
 
 // normalise elements [8b, 8b + 8) of a chunk (b compile-time after unrolling)
 template <int DT>
@@ -4670,6 +4746,7 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
         }
     }
     prof_begin(ctx, "analyze", &ev);
+    uint8_t *zero = nullptr;  // raw-frames tiles: all-zero subframe flags (k_zero_subframes)
     if (P.bps > 16) {
         if (stereo) {
             k_analyze<DT, true, true><<<agrid, 128, 0, st>>>(raster, Pa, dtiles, dnorms, ctx->window.as<float>(), dana,
@@ -4680,11 +4757,18 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
                                                                         ctx->window_hi.as<float>(), dana, dcand, lv.parts);
         } else {
             // raw-frames tiles: all-zero subframes analysed by a coalesced pass, skipped by the lane walks
-            uint8_t *zero = nullptr;
             if (!dcand) {
                 FRS_HIP(ctx->zero_sub.ensure((size_t)nsub + 64));
                 zero = ctx->zero_sub.as<uint8_t>();
-                k_zero_subframes<DT><<<(unsigned)((nsub + 3) / 4), 256, 0, st>>>(raster, Pa, dtiles, dnorms, dana, zero);
+                EncodeParams Pz = Pa;  // 64-sample row segments: the widest load every band's rows allow
+                const int es = (int)sizeof(T);
+                const uintptr_t b0 = reinterpret_cast<uintptr_t>(raster_dev) + (size_t)d->band0 * d->band_stride * es;
+                Pz.vec_ok = 0;
+                for (int a : {16, 8, 4})
+                    if (Pz.vec_ok == 0 && (d->row_stride * es) % a == 0 && (d->band_stride * es) % a == 0 &&
+                        b0 % a == 0 && ((int64_t)d->tile_w * es) % a == 0)
+                        Pz.vec_ok = a;
+                k_zero_subframes<DT><<<(unsigned)((nsub + 3) / 4), 256, 0, st>>>(raster, Pz, dtiles, dnorms, dana, zero);
             }
             k_analyze<DT, true><<<agrid, 128, 0, st>>>(raster, Pa, dtiles, dnorms, ctx->window.as<float>(), dana,
                                                          nullptr, 0, zero);
@@ -4743,6 +4827,8 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
     else
         k_encode_frames<DT><<<(unsigned)nframes, kEncThreads, 0, st>>>(raster, P, dtiles, dnorms, dana, dslots, dfb,
                                                                        err_flag, nullptr, dcand, nullptr, 0);
+    if (zero)  // the all-zero frames k_encode_frames left
+        k_zero_frames_emit<<<(unsigned)((nframes + 3) / 4), 256, 0, st>>>(P, dtiles, dana, dslots, dfb);
     prof_end(ctx, "encode", ev);
     // 4. offsets (frame_off[nframes] = total)
     k_scan_sizes<<<1, kScanThreads, 0, st>>>(ctx->frame_bytes.as<int64_t>(), ctx->frame_off.as<int64_t>(), nframes);
