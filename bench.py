@@ -232,6 +232,7 @@ def main():
             result["bbox_extract"] = bx
     if world == 1 and not args.no_extras:
         for name, leg in (("batched_decode", lambda: batched_decode(ctx, arena, off, mn, mx, rows, W, T)),
+                          ("c3_streaming", lambda: c3_streaming(ctx)),
                           ("sentinel2", lambda: sentinel2(ctx)), ("convert_multiband", lambda: convert_multiband(ctx)),
                           ("convert_2band", lambda: convert_2band(ctx)), ("raw_frames", lambda: raw_frames(ctx)),
                           ("convert_level8", lambda: convert_level8(ctx)),
@@ -379,6 +380,41 @@ def batched_decode(ctx, arena, off, tmin, tmax, rows, W, T):
     px = rows * W
     return {"tiles": len(counts), "ms": round(dt * 1e3, 2), "Mpixels_s": round(px / dt / 1e6, 1),
             "GB_s": round((int(off[-1]) + 2 * px) / dt / 1e9, 1), "kernels_ms": kern}
+
+
+def c3_streaming(ctx, steps=10):
+    """BASELINE config C3: create-streaming of a synthetic 16384 x 16384 x 4 int16 multispectral raster at tile 512
+    (band 1, cli.py:699; 1024 tiles), device-resident, with the encoder's algorithmic-bytes roofline (the same
+    recipe as the C4 line: 2 B/px read + the frames written, over the encoder's HIP-event time)."""
+    H = W = 16384
+    B, T = 4, 512
+    buf = ctx.alloc(B * H * W * 2)
+    ctx.synth_raster(buf, B, H, W, seed=1234)
+    d = ctx.make_desc(H, W, np.int16, nbands=1, band0=0, tile_h=T, tile_w=T, sample_rate=44100, bits_per_sample=16)
+    arena = ctx.alloc(ctx.arena_bound(d))
+    for _ in range(3):
+        ctx.encode_tiles_device(buf.ptr, d, arena)
+    ctx.profile(True)
+    ctx.profile_reset()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        off, _, _, _ = ctx.encode_tiles_device(buf.ptr, d, arena)
+    ctx.sync()
+    dt = (time.perf_counter() - t0) / steps
+    ctx.profile(False)
+    kern = {k: round(ctx.profile_avg_ms(k), 4) for k in ("stats", "analyze", "partial", "encode", "compact")}
+    kern = {k: v for k, v in kern.items() if v > 0}
+    comp = int(off[-1])
+    enc_gbs = (2 * H * W + comp) / (kern["encode"] * 1e-3) / 1e9 if "encode" in kern else None
+    arena.close()
+    buf.close()
+    return {"raster": f"{H}x{W}x{B} int16", "tile_size": T, "tiles": (H // T) * (W // T), "band": 1,
+            "ms_per_step": round(dt * 1e3, 3), "Mpixels_s": round(H * W / dt / 1e6, 1), "compressed_bytes": comp,
+            "kernels_ms": kern,
+            "roofline": None if enc_gbs is None else {"kernel": "encode", "achieved": round(enc_gbs, 1),
+                                                       "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                                       "frac": round(enc_gbs / HBM_PEAK_GBS, 4)}}
 
 
 def sentinel2(ctx, steps=5):

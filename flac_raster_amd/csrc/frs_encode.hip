@@ -2283,6 +2283,9 @@ __device__ inline SubAnalysis analysis_finish(const double *acc, uint32_t or_acc
 }
 
 // ------------------------------------------------------------------------------ k_analyze_v3
+// the prefetching analysis (PF) below this many 64-frame groups (waves) with fused stats: C3's 1024 tiles take it, C4's
+// 6241 keep occupancy 4
+constexpr int kPfMaxWaves = 1536;
 // Lane = frame (libFLAC's sequential fp64 autocorrelation per lane), laid
 // out for occupancy and memory-level parallelism: a wave takes up to 64 frames of ONE tile (host wave table),
 // so the normaliser is wave-uniform and chosen once (LUT in LDS read by ds_read / zeros / fast division /
@@ -2318,7 +2321,8 @@ __device__ inline uint32_t ana_sad(uint32_t a, uint32_t b, uint32_t c) {  // |a 
 // mid = (L + R) >> 1, side = L - R (converter.py:185-194 interleaves the bands; libFLAC process_subframes_ forms mid
 // and side from the normalised samples)
 // SIG >= 0 (ST): the signal fixed at compile time, so a wave loads and normalises only the bands it needs
-template <int DT, int KIND, int kAnaChunk, bool ST = false, int SIG = -1>
+// PF (small jobs, k_analyze_v3<..., PF>): the next chunk's loads are issued before the current chunk is summed
+template <int DT, int KIND, int kAnaChunk, bool ST = false, int SIG = -1, bool PF = false>
 __device__ inline void ana_autoc(const typename Elem<DT>::T *base, const EncodeParams &P, const TileGeom &g,
                                  int64_t s0, const TileNorm &tn, const int16_t *slut, const int16_t *glut,
                                  const float *__restrict__ swin, int vec, double *acc, uint32_t &or_acc, uint32_t *ft,
@@ -2333,11 +2337,26 @@ __device__ inline void ana_autoc(const typename Elem<DT>::T *base, const EncodeP
     for (int j = 0; j < 8; j++) prev[j] = 0.0;
     // (the fixed-predictor totals of fixed.c are the encoder's: encode_frame_v4 forms them lane-parallel from the
     // samples it has loaded anyway, which takes ~12 integer ops per sample out of this fp64-bound pass)
+    static_assert(!(PF && ST), "prefetch: single-band signals");
+    Ch pf;  // PF: the chunk whose loads are in flight
+    if constexpr (PF) {
+        pf.template load<true>(base, P.row_stride, g.w, crow, ccol, vec, kAnaChunk);
+        ccol += kAnaChunk;
+        while (ccol >= g.w) {
+            ccol -= g.w;
+            crow++;
+        }
+    }
     for (int c = 0; c < kMaxBlock / kAnaChunk; c++) {
         const int i0 = c * kAnaChunk;
         Ch ch, ch1;
-        if (!ST || sig != 1) ch.template load<true>(base, P.row_stride, g.w, crow, ccol, vec, kAnaChunk);
-        if (ST && sig >= 1) ch1.template load<true>(base + P.band_stride, P.row_stride, g.w, crow, ccol, vec, kAnaChunk);
+        if constexpr (PF) {
+            ch = pf;
+            if (c + 1 < kMaxBlock / kAnaChunk) pf.template load<true>(base, P.row_stride, g.w, crow, ccol, vec, kAnaChunk);
+        } else {
+            if (!ST || sig != 1) ch.template load<true>(base, P.row_stride, g.w, crow, ccol, vec, kAnaChunk);
+            if (ST && sig >= 1) ch1.template load<true>(base + P.band_stride, P.row_stride, g.w, crow, ccol, vec, kAnaChunk);
+        }
         ccol += kAnaChunk;
         while (ccol >= g.w) {
             ccol -= g.w;
@@ -2432,12 +2451,16 @@ __device__ inline void wave_tile_minmax(const typename Elem<DT>::T *base, int64_
 // and normalisation parameters (k_tile_stats_vec + k_tile_finalize) and builds the tile's LUT (k_build_lut) in
 // LDS and in global memory for the encoder -- the tile is read twice, but the separate stats pass and its
 // launches are gone.  A slow-class tile only gets its parameters written here; the SLOW launch analyses it.
-template <int DT, bool SLOW, bool STATS = false, bool ST = false>
+// PF (small fused-stats jobs: fewer 64-frame groups than about 1.5 waves per SIMD, e.g. C3's 1024 tiles): a lone wave
+// per SIMD waits on each chunk's loads in turn, so the next chunk's loads are issued before the current one is
+// summed.  136 instead of 127 VGPRs (occupancy 3 instead of 4): the large jobs (C4) keep the plain form.
+template <int DT, bool SLOW, bool STATS = false, bool ST = false, bool PF = false>
 __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *raster, EncodeParams P,
                                                    const TileGeom *tiles, TileNorm *norms,
                                                    int16_t *luts, const float *__restrict__ window,
                                                    SubAnalysis *out, const int2 *__restrict__ wtab, int nwaves) {
     static_assert(!(SLOW && STATS), "stats are fused into the lean launch only");
+    static_assert(!(PF && (SLOW || ST)), "prefetch: the lean mono / multi-channel launch");
     __shared__ int16_t slut[SLOW ? 1 : 4][SLOW ? 1 : kLutCap];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wv = blockIdx.x * 4 + wave;
@@ -2490,7 +2513,8 @@ __global__ void __launch_bounds__(256) k_analyze_v3(const typename Elem<DT>::T *
             else                                                                                                        \
                 ana_autoc<DT, KIND, kChunkMS, true, 3>(base, P, g, s0, tn, SLUT, glut, window, vec, acc, or_acc, ft);   \
         } else {                                                                                                        \
-            ana_autoc<DT, KIND, kChunk, false>(base, P, g, s0, tn, SLUT, glut, window, vec, acc, or_acc, ft, chn);      \
+            ana_autoc<DT, KIND, kChunk, false, -1, PF>(base, P, g, s0, tn, SLUT, glut, window, vec, acc, or_acc, ft,  \
+                                                       chn);                                                            \
         }                                                                                                               \
     } while (0)
     constexpr int kChunkMS = kChunk > 16 ? kChunk / 2 : kChunk;
@@ -4471,7 +4495,21 @@ static int run_encode(frs_ctx *ctx, const frs_encode_desc *d, const void *raster
             prof_begin(ctx, "analyze", &ev);
             const unsigned wgrid = (unsigned)((nwaves + 3) / 4);
             const int2 *wtab = ctx->wave_tab.as<int2>();
-            if (fuse_stats) {
+            // small jobs with fused stats (C3): the prefetching form (FRS_ANA_PF=0/1 forces either).  Measured (round 6,
+            // one box): C3 analysis 0.348 -> 0.322 ms; the Sentinel-2 example's separate-stats launch 0.529 -> 0.620 ms
+            // and C4 1.30 -> 1.31-1.33 ms, so those keep the plain form
+            const char *pf_env = getenv("FRS_ANA_PF");
+            const bool pf = !st2 && (pf_env ? atoi(pf_env) == 1 : fuse_stats && nwaves <= kPfMaxWaves);
+            if (pf) {
+                if (fuse_stats) {
+                    if constexpr (sizeof(T) == 2)
+                        k_analyze_v3<DT, false, true, false, true><<<wgrid, 256, 0, st>>>(
+                            raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(), ctx->window.as<float>(), dana, wtab, nwaves);
+                } else {
+                    k_analyze_v3<DT, false, false, false, true><<<wgrid, 256, 0, st>>>(
+                        raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(), ctx->window.as<float>(), dana, wtab, nwaves);
+                }
+            } else if (fuse_stats) {
                 if constexpr (sizeof(T) == 2)
                     k_analyze_v3<DT, false, true><<<wgrid, 256, 0, st>>>(raster, P, dtiles, dnorms, ctx->luts.as<int16_t>(),
                                                                          ctx->window.as<float>(), dana, wtab, nwaves);

@@ -121,8 +121,10 @@ int frs_encode_tiles(frs_ctx *ctx, const frs_encode_desc *desc, const void *rast
  * and must start at its first frame (the caller skips the metadata blocks; container.py parses them).
  * channels/bps describe every stream (STREAMINFO); samples are written interleaved as int32 at
  * pcm_out + pcm_off[s] * channels, pcm_off has nstreams+1 entries (per-stream sample counts known
- * from the tile windows).  Frames are located by sync code + CRC-8/CRC-16 and decoded one work-group
- * per frame.  Ranges of any size are accepted (64-bit positions); a stream with more sync-code
+ * from the tile windows).  Frames are located by sync code + CRC-8/CRC-16 and decoded in parallel: one lane per
+ * frame for large calls (thousands of frames), two waves per frame (a Rice-decoding and a restoring wave) for a
+ * single tile, one wave per frame for 32-bit / wide streams.  Ranges of any size are accepted (64-bit positions);
+ * a stream with more sync-code
  * candidates than the capacity (2 x frames + bytes / 1024 + 4096) is rejected with FRS_E_CORRUPT before
  * anything is written past it. */
 int frs_decode_frames_device(frs_ctx *ctx, const uint8_t *blob_dev, const int64_t *stream_off, int32_t nstreams,
@@ -138,7 +140,10 @@ int frs_decode_frames(frs_ctx *ctx, const uint8_t *blob_host, const int64_t *str
  * interleaved as out_dtype at out + (pcm_off[s] + i) * channels + c -- the int32 PCM never reaches memory for
  * mono 16-bit streams (create-streaming tiles).  out_dev is device memory, or page-locked host memory from
  * frs_host_malloc: the kernels then store the result straight into host memory (no separate D2H copy; a C5 query
- * returns one tile this way).  Errors as frs_decode_frames. */
+ * returns one tile this way).  On FRS_OK the result is complete and visible to the host: a device-memory out_dev
+ * after the call has synchronised the context stream; page-locked host memory from frs_host_malloc as soon as the
+ * kernels have published it (system-scope fences), possibly before the stream has retired -- a fault of those kernels
+ * is then reported by the next call on the context.  Errors as frs_decode_frames. */
 int frs_decode_tiles_device(frs_ctx *ctx, const uint8_t *blob_dev, const int64_t *stream_off, int32_t nstreams,
                             int32_t channels, int32_t bps, int32_t blocksize, const int64_t *pcm_off,
                             const double *data_min, const double *data_max, int32_t out_dtype, void *out_dev);

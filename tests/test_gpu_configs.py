@@ -228,3 +228,24 @@ def test_partial_frame_tiles_take_the_fast_path(gpu_ctx, shape, tile, dtype):
     assert np.array_equal(off, o_off)
     assert arena.tobytes() == o_arena.tobytes()
     assert np.array_equal(mn, o_mn) and np.array_equal(mx, o_mx)
+
+
+@pytest.mark.parametrize("shape,tile", [((4096, 6000), 512), ((3000, 3100), 1024), ((700, 900), 200)])
+def test_prefetch_analysis_equals_plain_form(gpu_ctx, monkeypatch, shape, tile):
+    """k_analyze_v3's prefetching launch (small jobs: the next chunk's loads in flight while one is summed) and the
+    plain launch give the same frames, both equal to the oracle (fused stats at tile 512; separate stats and partial
+    last frames at 1024 and 200)."""
+    H, W = shape
+    raster, band = _device_raster(gpu_ctx, H, W, bands=1, seed=77)
+    outs = []
+    for force in ("1", "0"):
+        monkeypatch.setenv("FRS_ANA_PF", force)
+        desc = gpu_ctx.make_desc(H, W, np.int16, tile_h=tile, tile_w=tile, sample_rate=44100, bits_per_sample=16)
+        arena = gpu_ctx.alloc(gpu_ctx.arena_bound(desc))
+        off, mn, mx, _ = gpu_ctx.encode_tiles_device(raster.ptr, desc, arena)
+        outs.append((off.copy(), arena.download(int(off[-1]), 0).tobytes()))
+        arena.close()
+    assert np.array_equal(outs[0][0], outs[1][0]) and outs[0][1] == outs[1][1]
+    o_arena, o_off, _, _ = O.encode_tiles(band, tile, threads=workloads.oracle_threads())
+    assert np.array_equal(outs[0][0], o_off) and outs[0][1] == o_arena.tobytes()
+    raster.close()
