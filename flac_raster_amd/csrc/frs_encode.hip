@@ -2765,8 +2765,8 @@ struct EncV3Shared {
     uint16_t xlo[64];       // x^(8m) mod P, m = 0..63
     uint16_t xhi[kXpowHi];  // x^(8*64*m) mod P
     uint8_t crc8[256];
-    int ticket;
-    int want;
+    int ticket[2];
+    int want[2];
     int lut_tile;
 };
 // lut_gather_pairs forms LUT byte addresses mod 2^16: the LUT (the only LDS object of k_encode_v3 is this struct)
@@ -3908,21 +3908,27 @@ __global__ void __launch_bounds__(256, sizeof(typename Elem<DT>::T) <= 2 ? (ST ?
     if (threadIdx.x == 0) S.lut_tile = -1;
     PendingFrame prev;
     uint32_t *fbuf = S.bits[wave];
+    // one barrier per ticket: the ticket and the tile it wants are double-buffered (slot = iteration & 1), so thread 0
+    // may write the next ticket while slower waves still read this one; every wave still meets the others once per
+    // ticket, after the atomic, so the LUT is never rewritten under a wave that encodes with it (round 6: encode
+    // 3.88-3.89 -> 3.84 ms, step 5.27-5.29 -> 5.22-5.24 ms, three alternations on one box; tools/r6/enc_variants.py)
+    int it = 0;
     while (true) {
-        __syncthreads();  // previous ticket's readers of S.ticket / S.lut are done
+        const int sl = it & 1;  // (slot sl is read after this iteration's barrier; the previous one's slot is sl ^ 1)
+        it++;
         constexpr int kUpfSt = WIDE ? 1 : 3;  // units per frame of a two-channel launch
         const int upf = ST ? kUpfSt : P.nch;
         const int64_t nunits = SUB ? P.nframes * upf : P.nframes;
         if (threadIdx.x == 0) {
             const int tk = atomicAdd(ticket_ctr, 1);
-            S.ticket = tk;
+            S.ticket[sl] = tk;
             const int64_t u0 = (int64_t)tk * 4;
-            S.want = (u0 < nunits) ? ftile[SUB ? u0 / upf : u0] : -1;
+            S.want[sl] = (u0 < nunits) ? ftile[SUB ? u0 / upf : u0] : -1;
         }
         __syncthreads();
-        const int64_t fbase = (int64_t)S.ticket * 4;
+        const int64_t fbase = (int64_t)S.ticket[sl] * 4;
         if (fbase >= nunits) break;
-        const int want = S.want;
+        const int want = S.want[sl];
         if (want != S.lut_tile) {  // WG-uniform
             const TileNorm tw = norms[want];
             if (tw.mode == kNormLut) {

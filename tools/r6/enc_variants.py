@@ -37,6 +37,96 @@ def one_barrier(src):
     return src
 
 
+def no_barrier(src):
+    """eB (on the tree's eA form): no barrier per ticket.  Thread 0 fills a ring of four ticket slots, each once the
+    four waves have read its previous use (an LDS read counter); every wave waits (LDS poll) for its iteration's slot
+    and reads it; the work-group meets only when the LUT's tile changes (all waves are then past their frames of the
+    old tile).  Spins are bounded (err |= 32, the wave returns: an ended wave no longer counts at a barrier)."""
+    subs = [
+        ("""    int ticket[2];
+    int want[2];
+    int lut_tile;""", """    int ticket[4];
+    int want[4];
+    int seq[4];
+    int nread[4];
+    int lut_tile;"""),
+        ("""    if (threadIdx.x == 0) S.lut_tile = -1;
+    PendingFrame prev;""", """    if (threadIdx.x == 0) S.lut_tile = -1;
+    if (threadIdx.x < 4) {
+        S.seq[threadIdx.x] = 0;
+        S.nread[threadIdx.x] = 4;
+    }
+    __syncthreads();
+    PendingFrame prev;"""),
+        ("""    int it = 0;
+    while (true) {
+        const int sl = it & 1;  // (slot sl is read after this iteration's barrier; the previous one's slot is sl ^ 1)
+        it++;
+        constexpr int kUpfSt = WIDE ? 1 : 3;  // units per frame of a two-channel launch
+        const int upf = ST ? kUpfSt : P.nch;
+        const int64_t nunits = SUB ? P.nframes * upf : P.nframes;
+        if (threadIdx.x == 0) {
+            const int tk = atomicAdd(ticket_ctr, 1);
+            S.ticket[sl] = tk;
+            const int64_t u0 = (int64_t)tk * 4;
+            S.want[sl] = (u0 < nunits) ? ftile[SUB ? u0 / upf : u0] : -1;
+        }
+        __syncthreads();
+        const int64_t fbase = (int64_t)S.ticket[sl] * 4;
+        if (fbase >= nunits) break;
+        const int want = S.want[sl];
+        if (want != S.lut_tile) {  // WG-uniform
+            const TileNorm tw = norms[want];""", """    int it = 0;
+    volatile int *vseq = S.seq, *vnread = S.nread;
+    while (true) {
+        const int sl = it & 3;
+        it++;
+        constexpr int kUpfSt = WIDE ? 1 : 3;  // units per frame of a two-channel launch
+        const int upf = ST ? kUpfSt : P.nch;
+        const int64_t nunits = SUB ? P.nframes * upf : P.nframes;
+        if (threadIdx.x == 0) {
+            long spins = 0;
+            while (vnread[sl] < 4) {  // the slot's previous use read by every wave
+                if (++spins > (1l << 24)) {
+                    atomicOr(err, 32);
+                    return;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            vnread[sl] = 0;
+            const int tk = atomicAdd(ticket_ctr, 1);
+            S.ticket[sl] = tk;
+            const int64_t u0 = (int64_t)tk * 4;
+            S.want[sl] = (u0 < nunits) ? ftile[SUB ? u0 / upf : u0] : -1;
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // the slot's words have landed before its sequence number
+            vseq[sl] = it;
+        }
+        {
+            long spins = 0;
+            while (vseq[sl] != it) {
+                if (++spins > (1l << 24)) {
+                    if (lane == 0) atomicOr(err, 32);
+                    return;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __asm__ volatile("" ::: "memory");
+        const int64_t fbase = (int64_t)S.ticket[sl] * 4;
+        const int want = S.want[sl];
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // (the reads above have returned before the read count moves)
+        if (lane == 0) atomicAdd(&S.nread[sl], 1);
+        if (fbase >= nunits) break;
+        if (want != S.lut_tile) {  // WG-uniform
+            __syncthreads();  // every wave is past its frames of the previous tile
+            const TileNorm tw = norms[want];"""),
+    ]
+    for a, b in subs:
+        assert src.count(a) == 1, a
+        src = src.replace(a, b)
+    return src
+
+
 if __name__ == "__main__":
     for name in sys.argv[1:] or ["eA"]:
-        print(build_variant(name, {"eA": one_barrier}[name]))
+        print(build_variant(name, {"eA": one_barrier, "eB": no_barrier}[name]))
