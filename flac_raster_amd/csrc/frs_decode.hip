@@ -291,10 +291,9 @@ __device__ inline uint32_t sel_point_crc(const SelCrcLds *cx, int wv, int k, int
 // `nxt` = the following 16 bytes: the bits whose header parses (header_ok_regs on the 32-byte window; the global
 // parse when the window does not hold the next 16 bytes).  Out of line: the rare path must not keep the caller's
 // step loop from unrolling (a rolled loop indexed the 16 loaded chunks dynamically, i.e. through scratch memory).
-__device__ __attribute__((noinline)) uint32_t sel_check_candidates(uint4 cur, uint4 nxt, uint32_t raw, int64_t p0,
-                                                                   int64_t nbytes, const uint8_t *blob,
-                                                                   const int64_t *soff, int ns, int channels,
-                                                                   int stream_bps, bool regs_ok) {
+__device__ inline uint32_t sel_check_body(uint4 cur, uint4 nxt, uint32_t raw, int64_t p0, int64_t nbytes,
+                                          const uint8_t *blob, const int64_t *soff, int ns, int channels,
+                                          int stream_bps, bool regs_ok) {
     uint32_t mask = 0;
     while (raw) {
         const int j = __builtin_ctz(raw);
@@ -322,6 +321,13 @@ __device__ __attribute__((noinline)) uint32_t sel_check_candidates(uint4 cur, ui
     return mask;
 }
 
+__device__ __attribute__((noinline)) uint32_t sel_check_candidates(uint4 cur, uint4 nxt, uint32_t raw, int64_t p0,
+                                                                   int64_t nbytes, const uint8_t *blob,
+                                                                   const int64_t *soff, int ns, int channels,
+                                                                   int stream_bps, bool regs_ok) {
+    return sel_check_body(cur, nxt, raw, p0, nbytes, blob, soff, ns, channels, stream_bps, regs_ok);
+}
+
 // Coalesced candidate flags: wave w of a 64 KB block takes the contiguous 16 KB at qw = block base + 16 KB w; step k
 // of it is the 1 KB at qw + 1024 k, lane L its 16 bytes at + 16 L (one fully coalesced 16-byte load per lane and
 // step).  Bit j of m[k] marks a sync code with a parseable, CRC-8-correct header at qw + 1024 k + 16 L + j, so
@@ -331,7 +337,9 @@ __device__ __attribute__((noinline)) uint32_t sel_check_candidates(uint4 cur, ui
 // Only a header starting in the wave's last 16 bytes takes the global parse.  Headers are bounded by the blob end
 // (not the stream end: a header straddling a stream boundary becomes a candidate whose CRC span never verifies).
 // Returns the lane's candidate count.
-template <int STEPS = kSelSteps, bool CRC = false>
+// FULL: the caller knows the wave's 16 KB lie inside the range: no per-lane guards.  (A separate kernel instance:
+// with both load forms in one kernel the compiler keeps a second register set live -- 116 instead of 87 VGPRs.)
+template <int STEPS = kSelSteps, bool CRC = false, bool FULL = false>
 __device__ inline int sel_masks_co(const uint8_t *blob, int64_t nbytes, const int64_t *soff, int ns, int channels,
                                    int stream_bps, int64_t qw, int lane, uint32_t *m, SelCrcLds *cx = nullptr,
                                    int wv = 0, uint32_t bsteps = 0) {
@@ -342,18 +350,33 @@ __device__ inline int sel_masks_co(const uint8_t *blob, int64_t nbytes, const in
     // all 16 loads in flight at once: unconditional (a chunk past the end re-reads chunk 0 and is zeroed after) --
     // a guarded load per step compiled to 16 load/wait round trips
     uint4 v[kSelSteps];
+    if constexpr (FULL) {
+        const uint8_t *wb = base + qw;
 #pragma unroll
-    for (int k = 0; k < kSelSteps; k++) {
-        const int64_t q = qw + 1024 * k + 16 * lane;
-        v[k] = *reinterpret_cast<const uint4 *>(base + (q < qend ? q : 0));
+        for (int k = 0; k < kSelSteps; k++)
+            v[k] = *reinterpret_cast<const uint4 *>(wb + (uint32_t)(1024 * k + 16 * lane));
+    } else {
+#pragma unroll
+        for (int k = 0; k < kSelSteps; k++) {
+            const int64_t q = qw + 1024 * k + 16 * lane;
+            v[k] = *reinterpret_cast<const uint4 *>(base + (q < qend ? q : 0));
+        }
+#pragma unroll
+        for (int k = 0; k < kSelSteps; k++)
+            if (qw + 1024 * k + 16 * lane >= qend) v[k] = make_uint4(0, 0, 0, 0);
     }
-#pragma unroll
-    for (int k = 0; k < kSelSteps; k++)
-        if (qw + 1024 * k + 16 * lane >= qend) v[k] = make_uint4(0, 0, 0, 0);
     const int64_t qlast = qw + 1024 * kSelSteps;  // the byte after the wave's 16 KB
     const uint32_t after = (lane == 63 && qlast < qend) ? base[qlast] : 0u;
     int cnt = 0;
     uint32_t acc = 0;  // CRC: Horner state of this lane's pieces over the steps so far
+    // no CRC fold (round 6; the one-pass selection and the placement pass's re-scan -- k_sync_count has its own
+    // queue form, sel_count_queue): the header checks wait until every step is flagged -- the steps keep only their
+    // patterns (16 bits each, two steps per register) and the steps holding one (rsteps), so the call to the
+    // rare-path check no longer sits between the 16 loaded chunks and the steps that read them
+    uint32_t rp[(kSelSteps + 1) / 2];
+#pragma unroll
+    for (int i = 0; i < (kSelSteps + 1) / 2; i++) rp[i] = 0;
+    uint32_t rsteps = 0;
 #pragma unroll
     for (int k = 0; k < kSelSteps; k++) {
         // first byte of the next 16 bytes: lane L + 1's word 0 (lane 63: next step's lane 0)
@@ -362,12 +385,22 @@ __device__ inline int sel_masks_co(const uint8_t *blob, int64_t nbytes, const in
                                               : after;
         if (lane == 63) nx = n0;
         const uint32_t w[5] = {v[k].x, v[k].y, v[k].z, v[k].w, nx & 0xFFu};
-        // sync patterns (0xFF then 0xF8 / 0xF9) of this lane's 16 bytes
-        uint32_t raw = 0;
+        // sync patterns (0xFF then 0xF8 / 0xF9) of this lane's 16 bytes.  Branch-free test first (round 6): per dword
+        // t = ~x | ((x >> 8 | next byte << 24) & 0xFE..FE ^ 0xF8..F8) has a zero byte exactly where a pattern starts,
+        // and haszero(t) is exact as a boolean; a 0xFF alone (1.6 % of dwords, so nearly every step of some lane) no
+        // longer sends the whole wave through the per-byte test, which runs only on steps with a pattern (~3 %)
+        uint32_t hit = 0;
 #pragma unroll
         for (int i = 0; i < 4; i++) {
-            const uint32_t x = w[i];
-            if (((~x) - 0x01010101u) & x & 0x80808080u) {  // some byte is 0xFF
+            const uint32_t sh = __builtin_amdgcn_alignbyte(w[i + 1], w[i], 1u);
+            const uint32_t t = ~w[i] | ((sh & 0xFEFEFEFEu) ^ 0xF8F8F8F8u);
+            hit |= (t - 0x01010101u) & ~t & 0x80808080u;
+        }
+        uint32_t raw = 0;
+        if (__ballot(hit != 0)) {  // (wave-uniform, rare) the exact per-byte flags
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const uint32_t x = w[i];
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const uint32_t b0 = (x >> (8 * j)) & 0xFF;
@@ -375,6 +408,11 @@ __device__ inline int sel_masks_co(const uint8_t *blob, int64_t nbytes, const in
                     if (b0 == 0xFF && (b1 & 0xFE) == 0xF8) raw |= 1u << (4 * i + j);
                 }
             }
+        }
+        if constexpr (!CRC) {
+            rp[k >> 1] |= raw << (16 * (k & 1));
+            if (__ballot(raw != 0)) rsteps |= 1u << k;
+            continue;
         }
         uint32_t mask = 0;
         if (__ballot(raw != 0)) {  // (wave-uniform, ~3 % of steps) the successor 16 bytes of every lane
@@ -417,6 +455,27 @@ __device__ inline int sel_masks_co(const uint8_t *blob, int64_t nbytes, const in
     if constexpr (CRC) {
         const uint32_t w = lane_reduce_crc(acc, lane, cx->ML);
         if (lane == 0) cx->W[wv] = w;
+    } else {
+        // the header checks of the flagged steps: the lane's 16 bytes and the next 16 read again (L2-hot; the next
+        // 16 zero past the range end, as the in-register window had them)
+#pragma unroll
+        for (int k = 0; k < kSelSteps; k++) {
+            uint32_t mask = 0;
+            if ((rsteps >> k) & 1u) {  // (wave-uniform)
+                const uint32_t raw = (rp[k >> 1] >> (16 * (k & 1))) & 0xFFFFu;
+                if (raw) {
+                    const int64_t q0 = qw + 1024 * k + 16 * lane;
+                    const uint4 cur = *reinterpret_cast<const uint4 *>(base + q0);
+                    const uint4 nxt = q0 + 16 < qend ? *reinterpret_cast<const uint4 *>(base + q0 + 16)
+                                                     : make_uint4(0, 0, 0, 0);
+                    const bool regs_ok = k + 1 < kSelSteps || lane < 63;  // the window holds the next 16 bytes
+                    mask = sel_check_candidates(cur, nxt, raw, q0 - lead, nbytes, blob, soff, ns, channels,
+                                                stream_bps, regs_ok);
+                }
+            }
+            m[k] = mask;
+            cnt += __builtin_popcount(mask);
+        }
     }
     return cnt;
 }
@@ -441,6 +500,7 @@ __device__ inline void sel_emit_co(const uint32_t *m, int64_t qw, int lane, int 
     constexpr int kSelSteps = STEPS;
 #pragma unroll
     for (int k = 0; k < kSelSteps; k++) {
+        if (__ballot(m[k] != 0) == 0) continue;  // (wave-uniform) most steps hold no candidate: no scan
         int tot;
         const int ex = wave_excl_scan_i32(__builtin_popcount(m[k]), lane, tot);
         if (tot) {
@@ -459,6 +519,118 @@ __device__ inline void sel_emit_co(const uint32_t *m, int64_t qw, int lane, int 
                 }
                 idx++;
             }
+        }
+        base += tot;
+    }
+}
+
+// Two-pass selection count without the CRC fold (round 6, the batched mono decode): the steps only flag sync patterns
+// (a branch-free test per dword, sel_masks_co) and append each lane holding one to the wave's queue in LDS -- entry =
+// step << 22 | lane << 16 | pattern bits, appended in (step, lane) order; then the queue's header checks run 64 at a
+// time, one entry per lane (the entry's 32-byte window read again, L2-hot), each entry's low 16 bits replaced by its
+// candidate bits.  Round 5 checked each flagged step for the whole wave in turn with the 16 chunks still in registers
+// (a call holding them live: 124 VGPRs) -- per wave ~2 K VALU, most of it the per-byte test that any 0xFF byte in
+// any lane triggered.  Candidates keep the (k, lane, j) order of sel_masks_co / sel_emit_co (the queue's order), so the
+// placement pass's re-scan of an overflowing block agrees.  Returns the lane's candidate count; qn = queue length.
+constexpr int kSelQueue = kSelSteps * 64;  // entries per wave (every lane of every step)
+template <bool FULL>
+__device__ inline int sel_count_queue(const uint8_t *blob, int64_t nbytes, const int64_t *soff, int ns, int channels,
+                                      int stream_bps, int64_t qw, int lane, uint32_t *q, int &qn_out) {
+    const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
+    const uint8_t *base = blob - lead;
+    const int64_t qend = nbytes + lead;
+    uint4 v[kSelSteps];
+    if constexpr (FULL) {
+        const uint8_t *wb = base + qw;
+#pragma unroll
+        for (int k = 0; k < kSelSteps; k++)
+            v[k] = *reinterpret_cast<const uint4 *>(wb + (uint32_t)(1024 * k + 16 * lane));
+    } else {
+#pragma unroll
+        for (int k = 0; k < kSelSteps; k++) {
+            const int64_t qq = qw + 1024 * k + 16 * lane;
+            v[k] = *reinterpret_cast<const uint4 *>(base + (qq < qend ? qq : 0));
+        }
+#pragma unroll
+        for (int k = 0; k < kSelSteps; k++)
+            if (qw + 1024 * k + 16 * lane >= qend) v[k] = make_uint4(0, 0, 0, 0);
+    }
+    const int64_t qlast = qw + 1024 * kSelSteps;  // the byte after the wave's 16 KB
+    const uint32_t after = (lane == 63 && qlast < qend) ? base[qlast] : 0u;
+    int qn = 0;  // (wave-uniform)
+#pragma unroll
+    for (int k = 0; k < kSelSteps; k++) {
+        uint32_t nx = (uint32_t)__shfl_down((int)v[k].x, 1);
+        const uint32_t n0 = k + 1 < kSelSteps ? (uint32_t)__builtin_amdgcn_readlane((int)v[k + 1 < kSelSteps ? k + 1 : k].x, 0)
+                                              : after;
+        if (lane == 63) nx = n0;
+        const uint32_t w[5] = {v[k].x, v[k].y, v[k].z, v[k].w, nx & 0xFFu};
+        uint32_t hit = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t sh = __builtin_amdgcn_alignbyte(w[i + 1], w[i], 1u);
+            const uint32_t t = ~w[i] | ((sh & 0xFEFEFEFEu) ^ 0xF8F8F8F8u);
+            hit |= (t - 0x01010101u) & ~t & 0x80808080u;
+        }
+        const uint64_t bm = __ballot(hit != 0);
+        if (bm) {  // (wave-uniform, ~3 % of steps) the exact per-byte flags of the lanes with one, queued
+            if (hit) {
+                uint32_t raw = 0;
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const uint32_t b0 = (w[i] >> (8 * j)) & 0xFF;
+                        const uint32_t b1 = j < 3 ? (w[i] >> (8 * j + 8)) & 0xFF : w[i + 1] & 0xFF;
+                        if (b0 == 0xFF && (b1 & 0xFE) == 0xF8) raw |= 1u << (4 * i + j);
+                    }
+                }
+                const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+                q[qn + below] = ((uint32_t)k << 22) | ((uint32_t)lane << 16) | raw;  // (hit exact: raw != 0)
+            }
+            qn += __builtin_popcountll(bm);
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // the queue's LDS writes have landed (one wave: in order)
+    __builtin_amdgcn_wave_barrier();
+    int cnt = 0;
+    for (int r0 = 0; r0 < qn; r0 += 64) {  // (wave-uniform) the header checks, one queue entry per lane
+        const int i = r0 + lane;
+        if (i < qn) {
+            const uint32_t e = q[i];
+            const int k = (int)(e >> 22), ln = (int)((e >> 16) & 63);
+            const int64_t q0 = qw + 1024 * k + 16 * ln;
+            const uint4 cur = *reinterpret_cast<const uint4 *>(base + q0);
+            const uint4 nxt = q0 + 16 < qend ? *reinterpret_cast<const uint4 *>(base + q0 + 16) : make_uint4(0, 0, 0, 0);
+            const bool regs_ok = k + 1 < kSelSteps || ln < 63;  // as sel_masks_co: the window holds the next 16 bytes
+            const uint32_t mask = sel_check_body(cur, nxt, e & 0xFFFFu, q0 - lead, nbytes, blob, soff, ns, channels,
+                                                 stream_bps, regs_ok);
+            q[i] = (e & 0xFFFF0000u) | mask;
+            cnt += __builtin_popcount(mask);
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_wave_barrier();
+    qn_out = qn;
+    return cnt;
+}
+
+// the candidate positions of sel_count_queue's checked queue, from output index `base` (past `cap` only counted)
+__device__ inline void sel_emit_queue(const uint32_t *q, int qn, int64_t qw, int lane, int lead, int64_t base,
+                                      int64_t *cpos, int64_t cap) {
+    for (int r0 = 0; r0 < qn; r0 += 64) {  // (wave-uniform)
+        const int i = r0 + lane;
+        const uint32_t e = i < qn ? q[i] : 0u;
+        uint32_t mask = e & 0xFFFFu;
+        int tot;
+        const int ex = wave_excl_scan_i32(__builtin_popcount(mask), lane, tot);
+        int64_t idx = base + ex;
+        const int64_t q0 = qw + 1024 * (int)(e >> 22) + 16 * (int)((e >> 16) & 63) - lead;
+        while (mask) {
+            const int j = __builtin_ctz(mask);
+            mask &= mask - 1;
+            if (idx < cap) cpos[idx] = q0 + j;
+            idx++;
         }
         base += tot;
     }
@@ -571,20 +743,23 @@ __device__ inline uint32_t sel_crc_block(SelCrcLds *cx) {
 // CRC (prefix-CRC span check): the block's CRC to bcrc[b], each kept candidate's CRC from the block start to bipc
 // (beside bpos), and each stream boundary inside the block (bfirst[b]: the first such stream index, soff[s] + lead
 // past the block start) to sbib[s]
-template <bool CRC = false>
+// FULL: blocks [blk0, blk0 + grid) lie inside the range (the host launches the range's last block apart)
+template <bool CRC = false, bool FULL = false>
 __global__ void __launch_bounds__(kSelThreads) k_sync_count(const uint8_t *blob, int64_t nbytes, const int64_t *soff,
                                                           int ns, int channels, int stream_bps, int32_t *bcount,
                                                           int64_t *bpos, uint16_t *bcrc = nullptr,
                                                           uint16_t *bipc = nullptr, const uint32_t *bfirst = nullptr,
-                                                          uint16_t *sbib = nullptr) {
+                                                          uint16_t *sbib = nullptr, int64_t blk0 = 0) {
+    const int64_t blk = blk0 + blockIdx.x;
     __shared__ int s_wsum[kSelThreads / 64];
     __shared__ typename std::conditional<CRC, SelCrcLds, char>::type cxs;
+    __shared__ uint32_t s_queue[CRC ? 1 : kSelThreads / 64][CRC ? 1 : kSelQueue];  // sel_count_queue's queues
     SelCrcLds *cx = CRC ? reinterpret_cast<SelCrcLds *>(&cxs) : nullptr;
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);  // (wave-uniform: scalar)
     const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
-    const int64_t qw = (int64_t)blockIdx.x * kSelBytes + (int64_t)(kSelBytes / 4) * wv;
+    const int64_t qw = blk * kSelBytes + (int64_t)(kSelBytes / 4) * wv;
     uint32_t bsteps = 0;  // this wave's steps holding a stream boundary
-    const int sb0 = CRC ? (int)bfirst[blockIdx.x] : -1;
+    const int sb0 = CRC ? (int)bfirst[blk] : -1;
     if constexpr (CRC) {
         sel_crc_load_tables(cx, t, kSelThreads);
         for (int sidx = sb0; sidx >= 0 && sidx <= ns; sidx++) {
@@ -595,7 +770,12 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_count(const uint8_t *blob,
         __syncthreads();
     }
     uint32_t m[kSelSteps];
-    int c = sel_masks_co<kSelSteps, CRC>(blob, nbytes, soff, ns, channels, stream_bps, qw, lane, m, cx, wv, bsteps);
+    int qn = 0;
+    int c;
+    if constexpr (CRC)
+        c = sel_masks_co<kSelSteps, CRC, FULL>(blob, nbytes, soff, ns, channels, stream_bps, qw, lane, m, cx, wv, bsteps);
+    else
+        c = sel_count_queue<FULL>(blob, nbytes, soff, ns, channels, stream_bps, qw, lane, &s_queue[wv][0], qn);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
     if (lane == 0) s_wsum[wv] = c;
@@ -606,10 +786,10 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_count(const uint8_t *blob,
         wbase += k < wv ? s_wsum[k] : 0;
         tot += s_wsum[k];
     }
-    if (t == 0) bcount[blockIdx.x] = tot;
-    const int64_t slot = (int64_t)blockIdx.x * kSelBlkCap;
+    if (t == 0) bcount[blk] = tot;
+    const int64_t slot = blk * kSelBlkCap;
     if constexpr (CRC) {
-        if (t == 0) bcrc[blockIdx.x] = (uint16_t)sel_crc_block(cx);
+        if (t == 0) bcrc[blk] = (uint16_t)sel_crc_block(cx);
         __syncthreads();
         const uint8_t *abase = blob - lead;
         if (tot <= kSelBlkCap)
@@ -626,7 +806,7 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_count(const uint8_t *blob,
                                                       lead));
         }
     } else if (tot <= kSelBlkCap) {  // (block-uniform) keep the positions: the placement pass copies them
-        sel_emit_co(m, qw, lane, lead, slot + wbase, bpos, slot + kSelBlkCap);
+        sel_emit_queue(&s_queue[wv][0], qn, qw, lane, lead, slot + wbase, bpos, slot + kSelBlkCap);
     }
 }
 
@@ -3178,6 +3358,8 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         int32_t *bcount = ctx->dec_sel.as<int32_t>();
         int64_t *bbase = ctx->dec_sel.as<int64_t>() + (nblocks + 1) / 2 + 1;
         int64_t *bpos = bbase + nblocks + 1;
+        // blocks whose 64 KB lie inside the range take the unguarded instance; the last, partial block its own launch
+        const int64_t nfull = std::min<int64_t>(nblocks, lead_bytes / kSelBytes);
         if (pcrc_span) {
             // [BP u32 (nblocks + 1) | bfirst u32 nblocks | bcrc u16 nblocks | bipc u16 32 nblocks | sbib u16 ns + 1 |
             //  pcrc u16 cand_cap]
@@ -3194,16 +3376,25 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
             const int lead = (int)(reinterpret_cast<uintptr_t>(blob_dev) & 15);
             FRS_HIP(hipMemsetAsync(bfirst, 0xFF, 4 * nb, st));
             k_bound_mark<<<(unsigned)((nstreams + 255) / 256), 256, 0, st>>>(dsoff, nstreams, lead, bfirst);
-            k_sync_count<true><<<(unsigned)nblocks, kSelThreads, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams,
-                                                                          channels, bps, bcount, bpos, bcrc, bipc,
-                                                                          bfirst, sbibv);
+            if (nfull)
+                k_sync_count<true, true><<<(unsigned)nfull, kSelThreads, 0, st>>>(
+                    blob_dev, blob_bytes, dsoff, nstreams, channels, bps, bcount, bpos, bcrc, bipc, bfirst, sbibv, 0);
+            if (nblocks > nfull)
+                k_sync_count<true, false><<<(unsigned)(nblocks - nfull), kSelThreads, 0, st>>>(
+                    blob_dev, blob_bytes, dsoff, nstreams, channels, bps, bcount, bpos, bcrc, bipc, bfirst, sbibv, nfull);
             k_sync_scan<<<1, 1024, 0, st>>>(bcount, bbase, nblocks, ncand, bcrc, BPv);
             k_sync_scatter<true><<<(unsigned)nblocks, kSelThreads, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams,
                                                                             channels, bps, bbase, cpos, cand_cap,
                                                                             bcount, bpos, pcrcv, BPv, bipc);
         } else {
-            k_sync_count<<<(unsigned)nblocks, kSelThreads, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams, channels,
-                                                                    bps, bcount, bpos);
+            if (nfull)
+                k_sync_count<false, true><<<(unsigned)nfull, kSelThreads, 0, st>>>(
+                    blob_dev, blob_bytes, dsoff, nstreams, channels, bps, bcount, bpos, nullptr, nullptr, nullptr,
+                    nullptr, 0);
+            if (nblocks > nfull)
+                k_sync_count<false, false><<<(unsigned)(nblocks - nfull), kSelThreads, 0, st>>>(
+                    blob_dev, blob_bytes, dsoff, nstreams, channels, bps, bcount, bpos, nullptr, nullptr, nullptr,
+                    nullptr, nfull);
             k_sync_scan<<<1, 1024, 0, st>>>(bcount, bbase, nblocks, ncand);
             k_sync_scatter<<<(unsigned)nblocks, kSelThreads, 0, st>>>(blob_dev, blob_bytes, dsoff, nstreams, channels,
                                                                       bps, bbase, cpos, cand_cap, bcount, bpos);
