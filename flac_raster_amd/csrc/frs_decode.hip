@@ -533,9 +533,12 @@ __device__ inline void sel_emit_co(const uint32_t *m, int64_t qw, int lane, int 
 // any lane triggered.  Candidates keep the (k, lane, j) order of sel_masks_co / sel_emit_co (the queue's order), so the
 // placement pass's re-scan of an overflowing block agrees.  Returns the lane's candidate count; qn = queue length.
 constexpr int kSelQueue = kSelSteps * 64;  // entries per wave (every lane of every step)
-template <bool FULL>
+// CRC (the prefix-CRC span check): also the lanes' CRC fold of sel_masks_co<CRC> -- a step is a point step (E / SW
+// recorded) when some lane holds a sync pattern (a superset of the candidate steps) or a stream boundary.
+template <bool FULL, bool CRC = false>
 __device__ inline int sel_count_queue(const uint8_t *blob, int64_t nbytes, const int64_t *soff, int ns, int channels,
-                                      int stream_bps, int64_t qw, int lane, uint32_t *q, int &qn_out) {
+                                      int stream_bps, int64_t qw, int lane, uint32_t *q, int &qn_out,
+                                      SelCrcLds *cx = nullptr, int wv = 0, uint32_t bsteps = 0) {
     const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
     const uint8_t *base = blob - lead;
     const int64_t qend = nbytes + lead;
@@ -558,6 +561,7 @@ __device__ inline int sel_count_queue(const uint8_t *blob, int64_t nbytes, const
     const int64_t qlast = qw + 1024 * kSelSteps;  // the byte after the wave's 16 KB
     const uint32_t after = (lane == 63 && qlast < qend) ? base[qlast] : 0u;
     int qn = 0;  // (wave-uniform)
+    uint32_t acc = 0;  // CRC: Horner state of this lane's pieces over the steps so far
 #pragma unroll
     for (int k = 0; k < kSelSteps; k++) {
         uint32_t nx = (uint32_t)__shfl_down((int)v[k].x, 1);
@@ -590,6 +594,28 @@ __device__ inline int sel_count_queue(const uint8_t *blob, int64_t nbytes, const
             }
             qn += __builtin_popcountll(bm);
         }
+        if constexpr (CRC) {
+            uint4 cv = v[k];
+            if (qw + 1024 * k + 16 * lane == 0 && lead) {  // bytes before the blob start count as zeros
+                auto keep = [&](uint32_t x, int d) -> uint32_t {
+                    const int nb = lead - 4 * d;  // leading bytes of this dword to clear
+                    return nb >= 4 ? 0u : nb <= 0 ? x : (x & ~((1u << (8 * nb)) - 1u));
+                };
+                cv = make_uint4(keep(cv.x, 0), keep(cv.y, 1), keep(cv.z, 2), keep(cv.w, 3));
+            }
+            const uint32_t c = chunk_crc16(cv, cx->T);
+            if (bm || ((bsteps >> k) & 1u)) {  // (wave-uniform) a point step
+                const uint32_t sw = lane_reduce_crc(acc, lane, cx->ML);
+                const uint32_t e = lane_excl_scan_crc(c, lane, cx->ML);
+                cx->E[wv][k][lane] = (uint16_t)e;
+                if (lane == 0) cx->SW[wv][k] = sw;
+            }
+            acc = crc_mul_tab(acc, cx->MK) ^ c;
+        }
+    }
+    if constexpr (CRC) {
+        const uint32_t wc = lane_reduce_crc(acc, lane, cx->ML);
+        if (lane == 0) cx->W[wv] = wc;
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // the queue's LDS writes have landed (one wave: in order)
     __builtin_amdgcn_wave_barrier();
@@ -615,9 +641,13 @@ __device__ inline int sel_count_queue(const uint8_t *blob, int64_t nbytes, const
     return cnt;
 }
 
-// the candidate positions of sel_count_queue's checked queue, from output index `base` (past `cap` only counted)
+// the candidate positions of sel_count_queue's checked queue, from output index `base` (past `cap` only counted);
+// CRC: ccrc[idx] = CRC of [origin, candidate) as sel_emit_co<CRC> forms it (`pre` = CRC of [origin, wave start))
+template <bool CRC = false>
 __device__ inline void sel_emit_queue(const uint32_t *q, int qn, int64_t qw, int lane, int lead, int64_t base,
-                                      int64_t *cpos, int64_t cap) {
+                                      int64_t *cpos, int64_t cap, uint16_t *ccrc = nullptr,
+                                      const SelCrcLds *cx = nullptr, int wv = 0, const uint8_t *abase = nullptr,
+                                      uint32_t pre = 0) {
     for (int r0 = 0; r0 < qn; r0 += 64) {  // (wave-uniform)
         const int i = r0 + lane;
         const uint32_t e = i < qn ? q[i] : 0u;
@@ -625,11 +655,17 @@ __device__ inline void sel_emit_queue(const uint32_t *q, int qn, int64_t qw, int
         int tot;
         const int ex = wave_excl_scan_i32(__builtin_popcount(mask), lane, tot);
         int64_t idx = base + ex;
-        const int64_t q0 = qw + 1024 * (int)(e >> 22) + 16 * (int)((e >> 16) & 63) - lead;
+        const int ek = (int)(e >> 22), eln = (int)((e >> 16) & 63);
+        const int64_t qc = qw + 1024 * ek + 16 * eln;
         while (mask) {
             const int j = __builtin_ctz(mask);
             mask &= mask - 1;
-            if (idx < cap) cpos[idx] = q0 + j;
+            if (idx < cap) {
+                cpos[idx] = qc - lead + j;
+                if constexpr (CRC)
+                    ccrc[idx] = (uint16_t)(crc_xpow(pre, (uint32_t)(qc + j - qw)) ^
+                                           sel_point_crc(cx, wv, ek, eln, j, abase, qc, lead));
+            }
             idx++;
         }
         base += tot;
@@ -753,7 +789,7 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_count(const uint8_t *blob,
     const int64_t blk = blk0 + blockIdx.x;
     __shared__ int s_wsum[kSelThreads / 64];
     __shared__ typename std::conditional<CRC, SelCrcLds, char>::type cxs;
-    __shared__ uint32_t s_queue[CRC ? 1 : kSelThreads / 64][CRC ? 1 : kSelQueue];  // sel_count_queue's queues
+    __shared__ uint32_t s_queue[kSelThreads / 64][kSelQueue];  // sel_count_queue's queues
     SelCrcLds *cx = CRC ? reinterpret_cast<SelCrcLds *>(&cxs) : nullptr;
     const int t = threadIdx.x, lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);  // (wave-uniform: scalar)
     const int lead = (int)(reinterpret_cast<uintptr_t>(blob) & 15);
@@ -769,13 +805,9 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_count(const uint8_t *blob,
         }
         __syncthreads();
     }
-    uint32_t m[kSelSteps];
     int qn = 0;
-    int c;
-    if constexpr (CRC)
-        c = sel_masks_co<kSelSteps, CRC, FULL>(blob, nbytes, soff, ns, channels, stream_bps, qw, lane, m, cx, wv, bsteps);
-    else
-        c = sel_count_queue<FULL>(blob, nbytes, soff, ns, channels, stream_bps, qw, lane, &s_queue[wv][0], qn);
+    int c = sel_count_queue<FULL, CRC>(blob, nbytes, soff, ns, channels, stream_bps, qw, lane, &s_queue[wv][0], qn, cx,
+                                       wv, bsteps);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
     if (lane == 0) s_wsum[wv] = c;
@@ -793,8 +825,8 @@ __global__ void __launch_bounds__(kSelThreads) k_sync_count(const uint8_t *blob,
         __syncthreads();
         const uint8_t *abase = blob - lead;
         if (tot <= kSelBlkCap)
-            sel_emit_co<kSelSteps, true>(m, qw, lane, lead, slot + wbase, bpos, slot + kSelBlkCap, bipc, cx, wv, abase,
-                                         cx->WP[wv]);
+            sel_emit_queue<true>(&s_queue[wv][0], qn, qw, lane, lead, slot + wbase, bpos, slot + kSelBlkCap, bipc, cx, wv,
+                                 abase, cx->WP[wv]);
         for (int sidx = sb0; sidx >= 0 && sidx <= ns; sidx++) {  // (wave-uniform loop) stream boundaries
             const int64_t q = soff[sidx] + lead;
             if (q >= qw + kSelBytes / 4) break;
@@ -3333,7 +3365,8 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     // stream of 65536 32-KB frames: the lane span check has few, long spans) select + span 2.49 -> 1.94 ms; the C4
     // batched mono decode (6241 streams of 8-KB frames) 2.16 -> 3.21 ms (the selection's CRC fold costs more than the
     // reading span check it replaces: 1 LDS table lookup per byte either way, at lower occupancy), so mono keeps the
-    // reading form.  FRS_SPAN_READ=1 / 2 forces the reading / prefix form (tests).
+    // reading form.  Round 6 (both counts in the queue form): select + span 1.73 (reading) vs 1.84 ms (prefix) on C4,
+    // the 4-band stream's decode 5.35 -> 4.91 ms.  FRS_SPAN_READ=1 / 2 forces the reading / prefix form (tests).
     const char *span_env = nblocks > kSelOnePassBlocks ? getenv("FRS_SPAN_READ") : nullptr;  // (no env walk per query)
     const int span_mode = span_env ? atoi(span_env) : 0;
     const bool pcrc_span = span_mode != 1 && (span_mode == 2 || mcl) && nblocks > kSelOnePassBlocks &&
