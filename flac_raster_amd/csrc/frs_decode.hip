@@ -2562,11 +2562,18 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
             int4 rr = make_int4(0, 0, 0, 0);
             const int4 *rp = reinterpret_cast<const int4 *>(&resbuf[i]);  // (base pointers: immediate ds offsets)
             uint32_t *xp = xout + (i >> 1);
+            // the group's 64 (pre-shifted) residuals read up front, every lane the same 16 bytes per read: they
+            // arrive in VGPRs and seed the dot2 accumulators (no per-sample v_readlane + v_mov).  Round 6: reading
+            // four at a time every second pair put an LDS round trip (s_waitcnt lgkmcnt(0)) on the lone wave's chain
+            // every 4 samples -- tools/micro/restore_chain.hip 25.6 -> 19.7 ns per sample, C5 decode_frames 104.4 ->
+            // 102.7 us: the restore (~80 us a frame) now runs behind the producer's Rice windows (a build with the
+            // restore skipped: 95 vs 97.6 us into device memory)
+            int4 rall[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) rall[j] = rp[j];
 #pragma unroll
             for (int p2 = 0; p2 < 32; p2++) {
-                // four (pre-shifted) residuals at a time, every lane reading the same 16 bytes: they arrive in VGPRs
-                // and seed the dot2 accumulators (no per-sample v_readlane + v_mov)
-                if (!(p2 & 1)) rr = rp[p2 >> 1];
+                if (!(p2 & 1)) rr = rall[p2 >> 1];
                 const int32_t Re = (p2 & 1) ? rr.z : rr.x, Ro = (p2 & 1) ? rr.w : rr.y;
                 const uint32_t A = Qr[(p2 + 3) & 3], B = Qr[(p2 + 2) & 3], Cc = Qr[(p2 + 1) & 3], Dd = Qr[p2 & 3];
                 int32_t pe = dec_dot2(Dd, Ce[3], Re);

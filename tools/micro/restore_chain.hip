@@ -5,7 +5,11 @@
 //   B  the newest two samples as 24-bit multiplies (the compiler sums them with v_add3: chain per pair mul -> add3 ->
 //      ashr -> mul -> add3 -> ashr), the older pairs by dot2 one step ahead
 //   C  B with v_mad_i32_i24 forced on the chain (mad -> ashr -> mad -> ashr)
-// Both outputs are checked against a host restore.
+//   D  A with the 64-sample group's residuals read from LDS up front (16 ds_read_b128 back to back): A reads four
+//      residuals every second pair and waits for them at once (s_waitcnt lgkmcnt(0): an LDS round trip per 4 samples
+//      on the lone wave's chain)
+//   E, F  B and C with the group's residuals read up front as in D
+// The outputs are checked against a host restore.
 // build: hipcc --offload-arch=gfx950 -O3 -o restore_chain restore_chain.hip
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -46,17 +50,23 @@ __global__ void __launch_bounds__(64) k_restore(const int32_t *R, const int32_t 
             int4 rr = make_int4(0, 0, 0, 0);
             const int4 *rp = reinterpret_cast<const int4 *>(&res[i]);
             uint32_t *xp = xout + (i >> 1);
+            int4 rall[FORM >= 3 ? 16 : 1];
+            if constexpr (FORM >= 3) {
+#pragma unroll
+                for (int j = 0; j < 16; j++) rall[j] = rp[j];
+            }
 #pragma unroll
             for (int p2 = 0; p2 < 32; p2++) {
                 if (i + 2 * p2 >= N) break;
                 if (!(p2 & 1)) {
-                    rr = rp[p2 >> 1];
+                    if constexpr (FORM >= 3) rr = rall[p2 >> 1];
+                    else rr = rp[p2 >> 1];
                     asm volatile("" : "+v"(rr.x), "+v"(rr.y), "+v"(rr.z), "+v"(rr.w));
                 }
                 const int32_t Re = (p2 & 1) ? rr.z : rr.x, Ro = (p2 & 1) ? rr.w : rr.y;
                 const uint32_t A = Qr[(p2 + 3) & 3], B = Qr[(p2 + 2) & 3], Cc = Qr[(p2 + 1) & 3], Dd = Qr[p2 & 3];
                 uint32_t qn;
-                if constexpr (FORM == 0) {
+                if constexpr (FORM == 0 || FORM == 3) {
                     int32_t pe = dot2(Dd, Ce[3], Re);
                     pe = dot2(Cc, Ce[2], pe);
                     pe = dot2(B, Ce[1], pe);
@@ -68,7 +78,7 @@ __global__ void __launch_bounds__(64) k_restore(const int32_t *R, const int32_t 
                     const int32_t xe = pe >> shift;
                     const int32_t xo = (__mul24(q0, xe) + po) >> shift;
                     qn = __builtin_amdgcn_perm((uint32_t)xo, (uint32_t)xe, 0x05040100u);
-                } else if constexpr (FORM == 2) {
+                } else if constexpr (FORM == 2 || FORM == 5) {
                     // B with explicit v_mad_i32_i24 on the chain: x[i-1] -> mad -> ashr -> mad -> ashr
                     int32_t pe = dot2(Dd, Ce[3], Re);
                     pe = dot2(Cc, Ce[2], pe);
@@ -139,12 +149,15 @@ int main(int argc, char **argv) {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    for (int form = 0; form < 3; form++) {
+    for (int form = 0; form < 6; form++) {
         for (int pass = 0; pass < 2; pass++) {
             hipEventRecord(a);
             if (form == 0) k_restore<0><<<1, 64>>>(dR, dq, shift, reps, dout);
             else if (form == 1) k_restore<1><<<1, 64>>>(dR, dq, shift, reps, dout);
-            else k_restore<2><<<1, 64>>>(dR, dq, shift, reps, dout);
+            else if (form == 2) k_restore<2><<<1, 64>>>(dR, dq, shift, reps, dout);
+            else if (form == 3) k_restore<3><<<1, 64>>>(dR, dq, shift, reps, dout);
+            else if (form == 4) k_restore<4><<<1, 64>>>(dR, dq, shift, reps, dout);
+            else k_restore<5><<<1, 64>>>(dR, dq, shift, reps, dout);
             hipEventRecord(b);
             hipEventSynchronize(b);
         }
@@ -157,7 +170,7 @@ int main(int argc, char **argv) {
             const int16_t g = (int16_t)(o[i >> 1] >> (16 * (i & 1)));
             bad += g != (int16_t)x[i];
         }
-        printf("form %c: %.2f ns/sample (%d reps), mismatches %d\n", "ABC"[form], ms * 1e6 / ((double)reps * (N - 8)),
+        printf("form %c: %.2f ns/sample (%d reps), mismatches %d\n", "ABCDEF"[form], ms * 1e6 / ((double)reps * (N - 8)),
                reps, bad);
     }
     return 0;
