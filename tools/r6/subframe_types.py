@@ -58,6 +58,7 @@ def main():
     ctx.sync()
     types = Counter()
     orders = Counter()
+    pords = Counter()
     step = max(1, (len(off) - 1) // ntiles)
     for t in range(0, len(off) - 1, step):
         buf = arena.download(int(off[t + 1] - off[t]), int(off[t])).tobytes()
@@ -70,10 +71,22 @@ def main():
                     "LPC" if st >= 32 else "other"
                 types[kind] += 1
                 orders[f"{kind}{(st - 8) if kind == 'FIXED' else (st - 31) if kind == 'LPC' else ''}"] += 1
+                if kind in ("FIXED", "LPC"):  # the residual's partition order (16-bit stream, no wasted bits)
+                    o = (st - 8) if kind == "FIXED" else (st - 31)
+                    v = int.from_bytes(buf[p + h:p + h + 64], "big")
+                    nb = 64 * 8
+                    pos = 8 + (buf[p + h] & 1)  # (a wasted-bits flag would add a unary count: C4 has none)
+                    pos += o * 16
+                    if kind == "LPC":
+                        prec = ((v >> (nb - pos - 4)) & 15) + 1
+                        pos += 4 + 5 + o * prec
+                    pos += 2
+                    po = (v >> (nb - pos - 4)) & 15
+                    pords[f"{kind}-po{po}"] += 1
                 p += h + 1000  # (frames are > 1 KB: skip ahead, then find the next sync)
             else:
                 p += 1
-    print(json.dumps({"tiles": len(range(0, len(off) - 1, step)), "types": dict(types), "orders": dict(orders)}),
+    print(json.dumps({"tiles": len(range(0, len(off) - 1, step)), "types": dict(types), "orders": dict(orders), "partition_orders": dict(pords)}),
           flush=True)
 
 
