@@ -2001,6 +2001,56 @@ struct WaveBits {
 // chain over the eight newest samples held as packed int16 pairs -- and writes them to LDS, copied to the PCM
 // output at the end.  Mono 16-bit FIXED / LPC (order <= 8, 32-bit-safe prediction) / CONSTANT / VERBATIM
 // subframes; anything else falls back to decode_one_frame on wave 0, lane 0.
+// The jump tables of one Rice window (kRiceWinBits candidate bit positions from stage bit P, parameter k1 - 1) by
+// one wave: jt[0][c] = 2 x the start of the code after a code starting at candidate c (absorbing -- c itself -- when
+// that code's stop bit lies more than 64 bits past its lane's first candidate), jt[k+1][c] = jt[k][jt[k][c]].  Entries
+// are BYTE offsets into a row (2 c), so a lookup's address is the entry itself plus the row's immediate offset.  Lane
+// j owns the kRiceWinQ consecutive candidates c = kRiceWinQ j + t: their 64-bit windows lie in four stage words, and
+// the lane's entries are one contiguous run (16-byte LDS stores).  The entries past the window (fixed points) are
+// the caller's.
+__device__ inline void rice_window_tables(const uint32_t *stage, uint32_t P, int k1, uint16_t (*jt)[kRiceWinBits + 128],
+                                          int lane) {
+    const uint32_t b = P + (uint32_t)(kRiceWinQ * lane), wi = b >> 5, sh = b & 31u;
+    const uint64_t wA = ((uint64_t)stage[wi] << 32) | stage[wi + 1];
+    const uint64_t wB = ((uint64_t)stage[wi + 2] << 32) | stage[wi + 3];
+    int jq[kRiceWinQ];
+    {
+        // the lane's 64 bits from its first candidate; candidate t's code ends k1 bits after the first set bit at or
+        // after t: those first-set positions by a backward select chain over the top 16 bits (one 64-bit clz for the
+        // rest) instead of a shift + clz per candidate.  A code whose stop bit lies past these 64 bits is left
+        // absorbing (the chain's long-code path decodes it).
+        const uint64_t X = sh ? (wA << sh) | (wB >> (64u - sh)) : wA;
+        const uint64_t X16 = X << 16;
+        int f = (X16 ? __builtin_clzll(X16) : 64) + 16;  // 80: no set bit in [16, 64)
+        const uint32_t top = (uint32_t)(X >> 48);
+        const int c0 = kRiceWinQ * lane;
+#pragma unroll
+        for (int t = kRiceWinQ - 1; t >= 0; t--) {
+            f = ((top >> (15 - t)) & 1u) ? t : f;
+            jq[t] = 2 * (f + k1 - t <= 64 ? c0 + f + k1 : c0 + t);
+        }
+    }
+    auto store_run = [&](uint16_t *row) {  // jq -> row[kRiceWinQ * lane ...], 16 bytes at a time
+#pragma unroll
+        for (int v = 0; v < kRiceWinQ / 8; v++) {
+            uint4 u;
+            u.x = (uint32_t)jq[8 * v] | ((uint32_t)jq[8 * v + 1] << 16);
+            u.y = (uint32_t)jq[8 * v + 2] | ((uint32_t)jq[8 * v + 3] << 16);
+            u.z = (uint32_t)jq[8 * v + 4] | ((uint32_t)jq[8 * v + 5] << 16);
+            u.w = (uint32_t)jq[8 * v + 6] | ((uint32_t)jq[8 * v + 7] << 16);
+            reinterpret_cast<uint4 *>(row + kRiceWinQ * lane)[v] = u;
+        }
+    };
+    store_run(jt[0]);
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+#pragma unroll
+        for (int q = 0; q < kRiceWinQ; q++)
+            jq[q] = *reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(jt[k]) + jq[q]);
+        store_run(jt[k + 1]);
+    }
+}
+
 typedef short dec_v2s16 __attribute__((ext_vector_type(2)));
 __device__ inline int32_t dec_dot2(uint32_t a, uint32_t b, int32_t c) {  // v_dot2_i32_i16
     return __builtin_amdgcn_sdot2(__builtin_bit_cast(dec_v2s16, a), __builtin_bit_cast(dec_v2s16, b), c, false);
@@ -2015,6 +2065,12 @@ struct PipeInfo {
     int32_t o, shift, w, bs;
     int32_t cq[8];
     int32_t wu[8];
+    // grid tables (one-partition Rice residuals): the producer publishes gstate = 1 with (gk1, gbase, glim), or -1;
+    // wave 2 builds the tables of grid window j (bits gbase + kRiceWinBits j ...) into slot j & 1 and publishes
+    // gready = j + 1; the producer publishes gused = the windows it has left behind, and gstop when it is done
+    int32_t gstate, gready, gused, gstop;
+    int32_t gk1;
+    uint32_t gbase, glim;
 };
 
 __device__ inline void lds_publish(volatile int32_t *p, int32_t v) {
@@ -2048,7 +2104,7 @@ __device__ inline void pipe_wg_exit(int *flags, int64_t nframes, int *hout) {
 // its end both verify.  Anything else (a false sync, a frame the producer would hand to the one-lane decoder) sets
 // flags[6], and the host runs the span check, chain and the non-optimistic decoder after all.
 template <bool OPT = false>
-__global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob, const int64_t *soff, int ns,
+__global__ void __launch_bounds__(192) k_decode_frames_pipe(const uint8_t *blob, const int64_t *soff, int ns,
                                                            const int64_t *poff, const int64_t *cpos,
                                                            const int64_t *ends, const int64_t *fbase,
                                                            const int64_t *frame_cand, int64_t nframes, int channels,
@@ -2064,13 +2120,13 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     union PipeU {
         struct {
             uint32_t xout[kDecResMax / 2];
-            uint16_t jt[6][kJumpN];
+            uint16_t jt[2][6][kJumpN];  // (the grid path's two slots; the partition-by-partition path slot 0)
         } p;
         int32_t fb[kDecResMax];
     };
     __shared__ __attribute__((aligned(16))) PipeU pu;
     uint32_t *xout = pu.p.xout;
-    uint16_t(*jt)[kJumpN] = pu.p.jt;
+    uint16_t(*jt)[kJumpN] = pu.p.jt[0];
     const int64_t fi = blockIdx.x;
     if (fi >= nframes) return;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -2111,13 +2167,17 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
     const int64_t wb = fpos >> 2, we = (fend_known + 3) >> 2;
     const bool staged = we - wb <= kDecStageWords;
     if (staged)  // big-endian words: the scalar bit reader needs no byte swap
-        stage_words<128, true>(stage, blob, wb, we - wb + 2 * kRiceWinQ + 4, send, (int)threadIdx.x);
+        stage_words<192, true>(stage, blob, wb, we - wb + 2 * kRiceWinQ + 4, send, (int)threadIdx.x);
     if (threadIdx.x == 0) {
         info.state = 0;
         info.progress = 0;
         info.finished = 0;
         info.valid = 0;
         info.crc_ok = 0;
+        info.gstate = 0;
+        info.gready = 0;
+        info.gused = 0;
+        info.gstop = 0;
     }
     __syncthreads();
     const int64_t nsamp = poff[s + 1] - poff[s];
@@ -2166,6 +2226,7 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
             }
         };
         auto finish = [&](int st, int valid) {
+            if (lane == 0) lds_publish(&vi->gstate, -1);  // (every early end: the grid builder leaves)
             if (st == kPipeDone) span_crc();
             // OPT: a CONSTANT / VERBATIM frame's samples were stored by this wave; the consumer's exit (and the last
             // work-group's completion word the host takes as the decode's end) must not pass them, and a fence
@@ -2314,12 +2375,102 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
         auto publish = [&]() {
             if (lane == 0) lds_publish(&vi->progress, i);
         };
+        // ---- one-partition residuals (C4: 97 % of the frames): the Rice parameter is the frame's, so the windows'
+        //      jump tables do not depend on where the chain enters them -- wave 2 builds them on a fixed bit grid
+        //      (window j = bits base + kRiceWinBits j ..), two windows ahead of this wave, which only walks the chain
+        //      (round 6: the table levels were ~half of each window's dependent LDS round trips)
+        bool grid = false;
+        if (po == 0) {
+            br.seek(P);
+            const int kp = (int)br.bits(pb);
+            if (kp != esc) {
+                grid = true;
+                const uint32_t base = br.pos();
+                if (lane == 0) {
+                    info.gk1 = kp + 1;
+                    info.gbase = base;
+                    info.glim = lim;
+                    lds_publish(&vi->gstate, 1);
+                }
+                uint32_t Pg = base;
+                int left = bs - o, jdone = 0;
+                while (left > 0) {
+                    if (Pg > lim) {
+                        bad = true;
+                        break;
+                    }
+                    const uint32_t rel = Pg - base;
+                    const int j = (int)(rel / (uint32_t)kRiceWinBits), e = (int)(rel % (uint32_t)kRiceWinBits);
+                    if (j > jdone) {  // windows < j are left behind: their slots may be rebuilt
+                        jdone = j;
+                        if (lane == 0) lds_publish(&vi->gused, j);
+                    }
+                    while (lds_poll(&vi->gready) <= j) __builtin_amdgcn_s_sleep(1);
+                    __asm__ volatile("" ::: "memory");  // table reads stay behind the poll
+                    const uint16_t(*tb)[kJumpN] = pu.p.jt[j & 1];
+                    auto tb_at = [&](int k, int byteoff) -> int {
+                        return *reinterpret_cast<const uint16_t *>(reinterpret_cast<const char *>(tb[k]) + byteoff);
+                    };
+                    const uint32_t wbits = base + (uint32_t)j * (uint32_t)kRiceWinBits;
+                    const int cap = left < 64 ? left : 64;
+                    int posv = 2 * e;  // (byte offset) lane m: the m-th code from the entry point
+#pragma unroll
+                    for (int k = 0; k < 6; k++) {
+                        const int nx = tb_at(k, posv);
+                        posv = ((lane >> k) & 1) ? nx : posv;
+                    }
+                    const int nxt = tb_at(0, posv);
+                    const uint64_t chain = __ballot(posv < 2 * kRiceWinBits && nxt != posv && lane < cap);
+                    const int cnt = __builtin_popcountll(chain);
+                    int cur;
+                    bool lng = false;
+                    if (cnt < cap) {  // stopped at a long code (inside the window) or past the window
+                        cur = __builtin_amdgcn_readlane(posv, cnt) >> 1;
+                        lng = cur < kRiceWinBits;
+                    } else {
+                        cur = __builtin_amdgcn_readlane(nxt, cnt - 1) >> 1;
+                    }
+                    {
+                        const uint32_t bc = wbits + (uint32_t)(posv >> 1), wc = bc >> 5;
+                        const uint32_t sft = bc & 31u, x0 = stage[wc], x1 = stage[wc + 1], x2 = stage[wc + 2];
+                        const uint32_t hi = sft ? __builtin_amdgcn_alignbit(x0, x1, 32u - sft) : x0;
+                        const uint32_t lo = sft ? __builtin_amdgcn_alignbit(x1, x2, 32u - sft) : x1;
+                        const uint64_t win = ((uint64_t)hi << 32) | lo;
+                        const int z = win ? __builtin_clzll(win) : 64;
+                        const uint32_t low = kp ? (uint32_t)((win << (z + 1)) >> (64 - kp)) : 0u;
+                        const uint32_t u = ((uint32_t)z << kp) | low;
+                        if (lane < cnt) resbuf[i + lane] = (int32_t)(((u >> 1) ^ (uint32_t)(-(int32_t)(u & 1))) << shift);
+                    }
+                    const int i0 = i;
+                    i += cnt;
+                    left -= cnt;
+                    Pg = wbits + (uint32_t)cur;
+                    if (lng) {  // a long unary run: one code through the scalar reader
+                        br.seek(Pg);
+                        uint32_t q;
+                        if (!br.unary(q, lim)) {
+                            bad = true;
+                            break;
+                        }
+                        const uint32_t uu = (q << kp) | br.bits(kp);
+                        if (lane == 0) resbuf[i] = (int32_t)(((uu >> 1) ^ (uint32_t)(-(int32_t)(uu & 1))) << shift);
+                        i++;
+                        left--;
+                        Pg = br.pos();
+                    }
+                    if ((i0 >> 6) != (i >> 6) || left == 0) publish();  // per 64-sample group (and the end)
+                }
+                P = Pg;
+                if (lane == 0) lds_publish(&vi->gstop, 1);
+            }
+        }
+        if (!grid && lane == 0) lds_publish(&vi->gstate, -1);
 #pragma unroll
         for (int k = 0; k < 6; k++) {  // jump-table entries past the window are fixed points
             jt[k][kRiceWinBits + lane] = (uint16_t)(2 * (kRiceWinBits + lane));
             jt[k][kRiceWinBits + 64 + lane] = (uint16_t)(2 * (kRiceWinBits + 64 + lane));
         }
-        for (int p = 0; p < (1 << po) && !bad; p++) {
+        for (int p = 0; p < (1 << po) && !bad && !grid; p++) {
             br.seek(P);
             const int kp = (int)br.bits(pb);
             int left = psz - (p == 0 ? o : 0);
@@ -2453,6 +2604,33 @@ __global__ void __launch_bounds__(128) k_decode_frames_pipe(const uint8_t *blob,
         if (lane == 0) {
             info.valid = ok;
             lds_publish(&vi->finished, 1);
+        }
+        return;
+    }
+    if (wave == 2) {
+        // ================= grid table builder (one-partition residuals, see the producer)
+        int gs;
+        while ((gs = lds_poll(&vi->gstate)) == 0) __builtin_amdgcn_s_sleep(1);
+        if (gs < 0) return;
+        __asm__ volatile("" ::: "memory");
+        const int k1 = vi->gk1;
+        const uint32_t base = vi->gbase, glim = vi->glim;
+#pragma unroll
+        for (int sl = 0; sl < 2; sl++)
+#pragma unroll
+            for (int k = 0; k < 6; k++) {  // entries past the window are fixed points
+                pu.p.jt[sl][k][kRiceWinBits + lane] = (uint16_t)(2 * (kRiceWinBits + lane));
+                pu.p.jt[sl][k][kRiceWinBits + 64 + lane] = (uint16_t)(2 * (kRiceWinBits + 64 + lane));
+            }
+        for (int j = 0;; j++) {
+            const uint32_t B = base + (uint32_t)j * (uint32_t)kRiceWinBits;
+            if (B > glim) break;  // (the producer stops at glim)
+            if (j >= 2)  // slot j & 1 held window j - 2: the producer has entered window j - 1
+                while (lds_poll(&vi->gused) < j - 1 && !lds_poll(&vi->gstop)) __builtin_amdgcn_s_sleep(1);
+            if (lds_poll(&vi->gstop)) break;
+            __asm__ volatile("" ::: "memory");
+            rice_window_tables(stage, B, k1, pu.p.jt[j & 1], lane);
+            if (lane == 0) lds_publish(&vi->gready, j + 1);
         }
         return;
     }
@@ -3456,7 +3634,7 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
         // the last work-group copies the counters into hv (page-locked) itself: no device-to-host copy to wait for
         hv[6] = -1;
         prof_begin(ctx, "decode_frames", &ev);
-        k_decode_frames_pipe<true><<<(unsigned)frames, 128, 0, st>>>(blob_dev, dsoff, nstreams, dpoff, cpos, ends,
+        k_decode_frames_pipe<true><<<(unsigned)frames, 192, 0, st>>>(blob_dev, dsoff, nstreams, dpoff, cpos, ends,
                                                                      dfbase, dchain, frames, channels, bps, pcm_dev,
                                                                      blocksize, nvalid, dout, ncand, ncand, hv);
         prof_end(ctx, "decode_frames", ev);
@@ -3569,7 +3747,7 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
             blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase, dchain, channels, bps, pcm_dev, blocksize, nvalid,
             dout, fbl, fbc);
     } else if (pipe) {
-        k_decode_frames_pipe<<<(unsigned)frames, 128, 0, st>>>(blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase,
+        k_decode_frames_pipe<<<(unsigned)frames, 192, 0, st>>>(blob_dev, dsoff, nstreams, dpoff, cpos, ends, dfbase,
                                                                dchain, frames, channels, bps, pcm_dev, blocksize, nvalid,
                                                                dout);
     } else
