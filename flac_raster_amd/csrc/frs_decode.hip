@@ -2720,6 +2720,19 @@ __global__ void __launch_bounds__(192) k_decode_frames_pipe(const uint8_t *blob,
     // issues one every ~8 cycles.)  Round 6: taking the newest pair's two samples off the dot2 (24-bit multiply-adds,
     // four dependent operations per pair instead of six) is not faster: tools/micro/restore_chain.hip 25.6 (this
     // form) / 27.9 / 26.9 ns per sample, C5 decode_frames 0.104 ms either way (one box, one call).
+    // OPT, de-normalised 1- / 2-byte output: each restored 64-sample group leaves (one 2-byte store per lane) while the
+    // next group is restored, instead of all 4096 samples after the restore; a declined frame is decoded again by the
+    // non-optimistic path, which rewrites its output
+    const int dt = fused ? dout.dtype : -1;
+    const bool dfast = (dt == FRS_DT_I16 || dt == FRS_DT_U16 || dt == FRS_DT_U8) && dout.shift == 0 &&
+                       (obase & 7) == 0 && (bs & 7) == 0;
+    const bool early = OPT && dfast;
+    const float dnx = dnp.x * (1.0f / 65536.0f);
+    auto dn1 = [&](int32_t x) -> uint32_t {  // (dn_bits_t's exact rewrite of ((x / 32768 + 1) / 2) * rng + mn)
+        const float a = __fadd_rn(__fmul_rn((float)((int32_t)((uint32_t)x << w) + 32768), dnx), dnp.y);
+        return (uint32_t)(int32_t)rintf(a);
+    };
+    int stored = 0;  // samples [0, stored) already stored (wave-uniform)
     if (!failed && i + 64 <= bs) {
         auto pk = [](int32_t hi, int32_t lo) { return ((uint32_t)hi << 16) | ((uint32_t)lo & 0xFFFFu); };
         const int32_t q0 = info.cq[0];
@@ -2749,6 +2762,10 @@ __global__ void __launch_bounds__(192) k_decode_frames_pipe(const uint8_t *blob,
             int4 rall[16];
 #pragma unroll
             for (int j = 0; j < 16; j++) rall[j] = rp[j];
+            // the previous 64 samples (the last group, or the head) leave after this group's restore: read now
+            const bool st_now = early && i - stored >= 64;
+            int32_t xprev = 0;
+            if (st_now) xprev = reinterpret_cast<const int16_t *>(xout)[stored + lane];
 #pragma unroll
             for (int p2 = 0; p2 < 32; p2++) {
                 if (!(p2 & 1)) rr = rall[p2 >> 1];
@@ -2768,6 +2785,12 @@ __global__ void __launch_bounds__(192) k_decode_frames_pipe(const uint8_t *blob,
                 xp[p2] = qn;
                 Qr[p2 & 3] = qn;
             }
+            if (st_now) {
+                const uint32_t ob = dn1(xprev);
+                if (dt == FRS_DT_U8) static_cast<uint8_t *>(dout.out)[obase + stored + lane] = (uint8_t)ob;
+                else static_cast<uint16_t *>(dout.out)[obase + stored + lane] = (uint16_t)ob;
+                stored += 64;
+            }
         }
 #pragma unroll
         for (int k = 0; k < 4; k++) H[k] = __builtin_amdgcn_alignbit(Qr[3 - k], Qr[3 - k], 16);  // for the tail
@@ -2782,14 +2805,12 @@ __global__ void __launch_bounds__(192) k_decode_frames_pipe(const uint8_t *blob,
         return;
     }
     const int16_t *x16 = reinterpret_cast<const int16_t *>(xout);
-    const int dt = fused ? dout.dtype : -1;
-    if ((dt == FRS_DT_I16 || dt == FRS_DT_U16 || dt == FRS_DT_U8) && dout.shift == 0 && (obase & 7) == 0 &&
-        (bs & 7) == 0) {
+    if (dfast) {
         // de-normalised 1- and 2-byte outputs: eight samples per lane and step, one 16-byte LDS read and one 16- (8-)
-        // byte store (the per-sample loop issued 64 scattered 2-byte stores per lane: 13.6 of a frame's 137 us)
+        // byte store (the per-sample loop issued 64 scattered 2-byte stores per lane: 13.6 of a frame's 137 us); the
+        // groups stored during the restore are skipped
         const uint4 *x8 = reinterpret_cast<const uint4 *>(xout);
-        const float dnx = dnp.x * (1.0f / 65536.0f);
-        for (int g = lane; g < (bs >> 3); g += 64) {
+        for (int g = (stored >> 3) + lane; g < (bs >> 3); g += 64) {
             const uint4 v = x8[g];
             const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
             uint32_t ob[8];
