@@ -104,6 +104,8 @@ int frs_ctx_create(int device, frs_ctx **out) {
     ctx->force_generic = fg && fg[0] == '1';
     const char *dl = getenv("FRS_DECODE_LANE");
     ctx->decode_lane = dl ? (dl[0] == '1' ? 1 : 0) : -1;
+    const char *po = getenv("FRS_PIPE_OPT");
+    ctx->pipe_opt = !(po && atoi(po) == 0);
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return FRS_E_HIP;

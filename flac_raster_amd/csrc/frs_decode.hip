@@ -3648,9 +3648,8 @@ int decode_job(frs_ctx *ctx, const uint8_t *blob_dev, int64_t blob_bytes, const 
     int *hv = reinterpret_cast<int *>(reinterpret_cast<char *>(htab) + ((3 * tab + dn_bytes + 15) & ~(size_t)15));
     // small mono ranges (C5 queries): the optimistic pipe decode first (no span check, no chain); only when it
     // declined (counts[6]: a false sync, a frame for the one-lane decoder) do the span check, chain and decode below
-    // run, after one more host round trip.  FRS_PIPE_OPT=0 disables it (tests)
-    const char *opt_env = getenv("FRS_PIPE_OPT");
-    const bool pipe_opt = pipe && !lane && max_frame < (int64_t)4096 * 256 && !(opt_env && atoi(opt_env) == 0);
+    // run, after one more host round trip.  FRS_PIPE_OPT=0 at context creation disables it (tests)
+    const bool pipe_opt = pipe && !lane && max_frame < (int64_t)4096 * 256 && ctx->pipe_opt;
     if (pipe_opt) {
         // the last work-group copies the counters into hv (page-locked) itself: no device-to-host copy to wait for
         hv[6] = -1;

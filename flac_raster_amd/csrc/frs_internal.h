@@ -80,6 +80,7 @@ struct frs_ctx {
     // decode scratch
     DevBuf dec_cand, dec_count, dec_pcm, dec_soff, dec_next, dec_status, dec_fb, dec_sel, dec_chass, dec_crc;
     int decode_lane = -1;    // FRS_DECODE_LANE=0/1 (tests): force the pipelined / lane-per-frame decoder
+    bool pipe_opt = true;    // FRS_PIPE_OPT=0 (tests): no optimistic small-range decode (read once, not per query)
     uint32_t dec_epoch = 0;  // call counter tagging the candidate selection's look-back words (24 bits, never 0)
     // profiling
     bool prof = false;
